@@ -1,0 +1,157 @@
+"""Flagship benchmark: ResNet-50 (ImageNet stem, 224x224, 1000 classes) bf16
+training throughput, one process per MI355X, synchronous data parallel with
+SyncBN + bucketed RCCL gradient all-reduce, fused SGD-nesterov -- the
+BASELINE.json metric/config.  Synthetic on-device data, random-init weights.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+
+Every rank does W untimed steps, then K timed steps bracketed by a barrier +
+device synchronize on both sides; the step time is the MAX over ranks and
+rank 0 prints ONE JSON line.  Per-GPU batch is fixed (256) -> weak scaling.
+Each timed step is the full step: forward, loss, backward with overlapped
+gradient all-reduce, optimizer update (nothing cached or skipped).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = ("images/sec (whole node) ResNet-50 224×224 bf16 at 1/2/4/8 MI355X; "
+          "DDP scaling efficiency")
+# stock PyTorch-ROCm reference path (DDP+SyncBN+MIOpen, bench/comparator_torch.py),
+# measured on one MI355X at per-GPU batch 256: profiles/comparator_r01.txt
+STOCK_IPS_PER_GPU = 6612.5
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--classes", type=int, default=1000)
+    ap.add_argument("--sync_bn", default="on", choices=["on", "off"])
+    ap.add_argument("--bucket_mb", type=float, default=25.0)
+    ap.add_argument("--first_bucket_mb", type=float, default=1.0)
+    ap.add_argument("--profile", default="", help="write a torch.profiler table here (rank 0)")
+    return ap.parse_args()
+
+
+def bench_rank(rank, world, a):
+    from pytorch_multiprocessing_distributed_amd import launch
+    from pytorch_multiprocessing_distributed_amd.data.loader import SyntheticImageNet
+    from pytorch_multiprocessing_distributed_amd.engine.optim import FusedSGD
+    from pytorch_multiprocessing_distributed_amd.models import build_model
+    from pytorch_multiprocessing_distributed_amd.ops import functional as OF
+    from pytorch_multiprocessing_distributed_amd.parallel.comm import get_comm
+    from pytorch_multiprocessing_distributed_amd.parallel.dp import DataParallel
+
+    if world > 1:
+        dev = launch.init_process(rank, world, "nccl", "cuda")
+    else:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = build_model(a.model, num_classes=a.classes, stem="imagenet").to(dev)
+    comm = get_comm()
+    OF.set_bn_sync(comm if (comm is not None and a.sync_bn == "on") else None)
+    model = DataParallel(model, comm, bucket_mb=a.bucket_mb, first_bucket_mb=a.first_bucket_mb)
+    opt = FusedSGD(model, lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    data = SyntheticImageNet(a.batch, a.image, a.classes, steps=a.warmup + a.steps, device=dev,
+                             dtype=torch.bfloat16, cpad=8, seed=rank)
+    model.train()
+
+    def step(i):
+        x, y = data.batch_at(i)
+        out = model(x)
+        loss = OF.cross_entropy(out, y)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        return loss
+
+    for i in range(a.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if comm is not None:
+        comm.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        loss = step(a.warmup + i)
+    torch.cuda.synchronize()
+    if comm is not None:
+        comm.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    if comm is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    final_loss = float(loss.item())
+    if rank == 0:
+        ips = a.batch * world * a.steps / dt
+        rec = {
+            "metric": METRIC, "value": round(ips, 1), "unit": "images/sec",
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(1000.0 * dt / a.steps, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (on-device generated ImageNet-shaped batches, random-init weights)",
+            "config": {"model": "ResNet-50", "global_batch": a.batch * world, "seq_len": None,
+                       "image_size": a.image, "per_gpu_batch": a.batch,
+                       "parallelism": f"dp{world}", "sync_bn": a.sync_bn == "on" and world > 1,
+                       "bucket_mb": a.bucket_mb},
+            "vs_stock_pytorch_rocm": round(ips / (STOCK_IPS_PER_GPU * world), 3),
+            "final_loss": round(final_loss, 4),
+        }
+        print(json.dumps(rec), flush=True)
+    if a.profile and rank == 0:
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            for i in range(3):
+                step(i)
+            torch.cuda.synchronize()
+        with open(a.profile, "w") as f:
+            f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=80))
+    if world > 1:
+        launch.shutdown()
+
+
+def _spawn_entry(rank, world, a):
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29517")
+    os.environ["LOCAL_RANK"] = str(rank)
+    bench_rank(rank, world, a)
+
+
+def main():
+    a = parse()
+    if "WORLD_SIZE" in os.environ:
+        world = int(os.environ["WORLD_SIZE"])
+        rank = int(os.environ.get("RANK", "0"))
+        if world != a.gpus and rank == 0:
+            print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE",
+                  file=sys.stderr)
+        bench_rank(rank, world, a)
+    elif a.gpus > 1:
+        import torch.multiprocessing as mp
+        mp.spawn(_spawn_entry, args=(a.gpus, a), nprocs=a.gpus, join=True)
+    else:
+        bench_rank(0, 1, a)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,335 @@
+// Torch <-> gfx950 kernel bindings for pytorch_multiprocessing_distributed_amd._C
+//
+// Every op validates device / dtype / layout and throws on anything the
+// kernels do not support (no silent fallback), allocates its outputs through
+// the PyTorch-ROCm caching allocator and launches on the current HIP stream.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/core/DeviceGuard.h>
+#include <hip/hip_runtime.h>
+
+#include "kernels/launchers.h"
+
+namespace {
+
+using torch::Tensor;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_CONT(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == torch::kBFloat16, #t " must be bf16")
+#define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == torch::kFloat32, #t " must be fp32")
+#define CHECK_RC(rc, what) TORCH_CHECK((rc) == 0, what " rejected the shape (code ", rc, ")")
+
+const pmd::bf16_t* bfp(const Tensor& t) { return reinterpret_cast<const pmd::bf16_t*>(t.data_ptr()); }
+pmd::bf16_t* bfp_mut(Tensor& t) { return reinterpret_cast<pmd::bf16_t*>(t.data_ptr()); }
+
+// ------------------------------------------------------------------ conv
+std::vector<Tensor> conv_weight_prep(Tensor w, int64_t cp, bool want_t) {
+  CHECK_DEV(w);
+  CHECK_F32(w);
+  TORCH_CHECK(w.dim() == 4, "weight must be [K,C,R,S]");
+  const int K = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(cp >= C && cp % 8 == 0, "padded channels must be >= C and a multiple of 8");
+  c10::DeviceGuard g(w.device());
+  Tensor wphys = w.permute({0, 2, 3, 1}).contiguous();  // no-op for channels_last params
+  auto opt = w.options().dtype(torch::kBFloat16);
+  Tensor wk = torch::empty({K, R, S, cp}, opt);
+  Tensor wkt;
+  if (want_t) wkt = torch::empty({cp, R, S, K}, opt);
+  pmd::conv_weight_prep_launch(wphys.data_ptr<float>(), bfp_mut(wk),
+                               want_t ? bfp_mut(wkt) : nullptr, K, R * S, C, (int)cp, cur_stream());
+  if (want_t) return {wk, wkt};
+  return {wk};
+}
+
+std::vector<Tensor> conv_fwd(Tensor x, Tensor wk, int64_t stride, int64_t pad, bool want_stats) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONT(x);
+  CHECK_DEV(wk); CHECK_BF16(wk); CHECK_CONT(wk);
+  TORCH_CHECK(x.dim() == 4 && wk.dim() == 4, "x [N,H,W,C], wk [K,R,S,C]");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int K = wk.size(0), R = wk.size(1), S = wk.size(2);
+  TORCH_CHECK(wk.size(3) == C, "channel mismatch: x has ", C, ", weight has ", wk.size(3));
+  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
+  c10::DeviceGuard g(x.device());
+  Tensor y = torch::empty({N, P, Q, K}, x.options());
+  Tensor stats;
+  if (want_stats) stats = torch::zeros({2, K}, x.options().dtype(torch::kFloat32));
+  const int rc = pmd::conv_igemm_launch(bfp(x), bfp(wk), bfp_mut(y),
+                                        want_stats ? stats.data_ptr<float>() : nullptr, N, H, W, C, P,
+                                        Q, K, R, S, (int)stride, (int)pad, false, cur_stream());
+  CHECK_RC(rc, "conv_fwd");
+  if (want_stats) return {y, stats};
+  return {y};
+}
+
+// dx[N,H,W,Cp] from dy[N,P,Q,K] and wkt[Cp,R,S,K]
+Tensor conv_dgrad(Tensor dy, Tensor wkt, int64_t H, int64_t W, int64_t stride, int64_t pad) {
+  CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONT(dy);
+  CHECK_DEV(wkt); CHECK_BF16(wkt); CHECK_CONT(wkt);
+  const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), K = dy.size(3);
+  const int Cp = wkt.size(0), R = wkt.size(1), S = wkt.size(2);
+  TORCH_CHECK(wkt.size(3) == K, "dgrad weight/K mismatch");
+  TORCH_CHECK((H + 2 * pad - R) / stride + 1 == P && (W + 2 * pad - S) / stride + 1 == Q,
+              "dgrad spatial mismatch");
+  c10::DeviceGuard g(dy.device());
+  Tensor dx = torch::empty({N, H, W, Cp}, dy.options());
+  // the gathered operand is dy (spatial P x Q, K channels); output spatial is H x W
+  const int rc = pmd::conv_igemm_launch(bfp(dy), bfp(wkt), bfp_mut(dx), nullptr, N, P, Q, K, (int)H,
+                                        (int)W, Cp, R, S, (int)stride, (int)pad, true, cur_stream());
+  CHECK_RC(rc, "conv_dgrad");
+  return dx;
+}
+
+Tensor conv_wgrad(Tensor dy, Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad) {
+  CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONT(dy);
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONT(x);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int P = dy.size(1), Q = dy.size(2), K = dy.size(3);
+  TORCH_CHECK(dy.size(0) == N, "batch mismatch");
+  TORCH_CHECK((H + 2 * pad - R) / stride + 1 == P && (W + 2 * pad - S) / stride + 1 == Q,
+              "wgrad spatial mismatch");
+  c10::DeviceGuard g(x.device());
+  Tensor dw = torch::zeros({K, R, S, C}, x.options().dtype(torch::kFloat32));
+  const int rc = pmd::conv_wgrad_launch(bfp(dy), bfp(x), dw.data_ptr<float>(), N, H, W, C, P, Q, K,
+                                        (int)R, (int)S, (int)stride, (int)pad, cur_stream());
+  CHECK_RC(rc, "conv_wgrad");
+  return dw;
+}
+
+// -------------------------------------------------------------------- BN
+Tensor bn_finalize(c10::optional<Tensor> sums, c10::optional<Tensor> count, Tensor gamma, Tensor beta, double eps,
+                   c10::optional<Tensor> rm, c10::optional<Tensor> rv, double momentum,
+                   c10::optional<Tensor> nbt, bool eval_mode) {
+  CHECK_DEV(gamma); CHECK_F32(gamma);
+  const int C = gamma.numel();
+  c10::DeviceGuard g(gamma.device());
+  Tensor params = torch::empty({4, C}, gamma.options());
+  float* rmp = nullptr;
+  float* rvp = nullptr;
+  long long* nb = nullptr;
+  if (rm && rm->defined()) { CHECK_F32(*rm); CHECK_CONT(*rm); rmp = rm->data_ptr<float>(); }
+  if (rv && rv->defined()) { CHECK_F32(*rv); CHECK_CONT(*rv); rvp = rv->data_ptr<float>(); }
+  if (nbt && nbt->defined()) {
+    TORCH_CHECK(nbt->scalar_type() == torch::kInt64 && nbt->is_cuda(), "nbt int64 GPU");
+    nb = reinterpret_cast<long long*>(nbt->data_ptr<int64_t>());
+  }
+  if (eval_mode) TORCH_CHECK(rmp && rvp, "eval BN needs running stats");
+  if (!eval_mode) TORCH_CHECK(sums && sums->defined() && count && count->defined(), "train BN needs sums");
+  Tensor s = eval_mode ? gamma : sums->contiguous();
+  Tensor cnt = eval_mode ? gamma : count->contiguous();
+  Tensor gm = gamma.contiguous(), bt = beta.contiguous();
+  pmd::bn_finalize_launch(eval_mode ? nullptr : s.data_ptr<float>(),
+                          eval_mode ? nullptr : cnt.data_ptr<float>(), gm.data_ptr<float>(),
+                          bt.data_ptr<float>(), params.data_ptr<float>(), rmp, rvp, nb, C, (float)eps,
+                          (float)momentum, eval_mode, cur_stream());
+  return params;
+}
+
+Tensor bn_apply(Tensor y1, Tensor p1, c10::optional<Tensor> res, c10::optional<Tensor> y2,
+                c10::optional<Tensor> p2, bool relu) {
+  CHECK_DEV(y1); CHECK_BF16(y1); CHECK_CONT(y1);
+  const int C = y1.size(-1);
+  const long long M = y1.numel() / C;
+  TORCH_CHECK(p1.numel() == 4 * C, "params size");
+  int mode = 0;
+  const pmd::bf16_t* r = nullptr;
+  const float* pp2 = nullptr;
+  if (y2 && y2->defined()) {
+    CHECK_BF16(*y2); CHECK_CONT(*y2);
+    TORCH_CHECK(y2->sizes() == y1.sizes(), "second branch shape");
+    TORCH_CHECK(p2 && p2->defined() && p2->numel() == 4 * C, "second branch params");
+    mode = 2;
+    r = bfp(*y2);
+    pp2 = p2->data_ptr<float>();
+  } else if (res && res->defined()) {
+    CHECK_BF16(*res); CHECK_CONT(*res);
+    TORCH_CHECK(res->sizes() == y1.sizes(), "residual shape");
+    mode = 1;
+    r = bfp(*res);
+  }
+  c10::DeviceGuard g(y1.device());
+  Tensor out = torch::empty_like(y1);
+  const int rc = pmd::bn_apply_launch(bfp(y1), p1.data_ptr<float>(), r, pp2, bfp_mut(out), M, C, mode,
+                                      relu, cur_stream());
+  CHECK_RC(rc, "bn_apply");
+  return out;
+}
+
+Tensor bn_bwd_reduce(Tensor dout, Tensor out, Tensor y, Tensor params, bool relu) {
+  CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONT(dout);
+  CHECK_BF16(out); CHECK_CONT(out); CHECK_BF16(y); CHECK_CONT(y);
+  const int C = y.size(-1);
+  const long long M = y.numel() / C;
+  TORCH_CHECK(M < (1ll << 31), "too many rows");
+  c10::DeviceGuard g(y.device());
+  Tensor red = torch::zeros({2, C}, y.options().dtype(torch::kFloat32));
+  const int rc = pmd::bn_bwd_reduce_launch(bfp(dout), bfp(out), bfp(y), params.data_ptr<float>(),
+                                           red.data_ptr<float>(), (int)M, C, relu, cur_stream());
+  CHECK_RC(rc, "bn_bwd_reduce");
+  return red;
+}
+
+std::vector<Tensor> bn_bwd_elemt(Tensor dout, Tensor out, Tensor y, Tensor params, Tensor gamma,
+                                 c10::optional<Tensor> red, c10::optional<Tensor> count, bool relu,
+                                 bool want_dzm, bool eval_mode) {
+  CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONT(dout);
+  CHECK_BF16(out); CHECK_CONT(out);
+  const int C = dout.size(-1);
+  const long long M = dout.numel() / C;
+  c10::DeviceGuard g(dout.device());
+  Tensor dy = torch::empty_like(dout);
+  Tensor dzm;
+  if (want_dzm) dzm = torch::empty_like(dout);
+  Tensor rr, cc, gm = gamma.contiguous();
+  if (!eval_mode) {
+    TORCH_CHECK(red && red->defined() && count && count->defined(), "train backward needs sums");
+    CHECK_BF16(y); CHECK_CONT(y);
+    rr = red->contiguous();
+    cc = count->contiguous();
+  }
+  const int rc = pmd::bn_bwd_elemt_launch(
+      bfp(dout), bfp(out), eval_mode ? nullptr : bfp(y), params.data_ptr<float>(), gm.data_ptr<float>(),
+      eval_mode ? nullptr : rr.data_ptr<float>(), eval_mode ? nullptr : cc.data_ptr<float>(),
+      bfp_mut(dy), want_dzm ? bfp_mut(dzm) : nullptr, M, C, relu, eval_mode, cur_stream());
+  CHECK_RC(rc, "bn_bwd_elemt");
+  if (want_dzm) return {dy, dzm};
+  return {dy};
+}
+
+// ----------------------------------------------------------------- pools
+std::vector<Tensor> maxpool_fwd(Tensor x) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONT(x);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int P = (H + 2 - 3) / 2 + 1, Q = (W + 2 - 3) / 2 + 1;
+  c10::DeviceGuard g(x.device());
+  Tensor out = torch::empty({N, P, Q, C}, x.options());
+  Tensor arg = torch::empty({N, P, Q, C}, x.options().dtype(torch::kUInt8));
+  CHECK_RC(pmd::maxpool_fwd_launch(bfp(x), bfp_mut(out), arg.data_ptr<uint8_t>(), N, H, W, C, P, Q,
+                                   cur_stream()), "maxpool_fwd");
+  return {out, arg};
+}
+
+Tensor maxpool_bwd(Tensor dout, Tensor arg, int64_t H, int64_t W) {
+  CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONT(dout); CHECK_CONT(arg);
+  const int N = dout.size(0), P = dout.size(1), Q = dout.size(2), C = dout.size(3);
+  c10::DeviceGuard g(dout.device());
+  Tensor dx = torch::empty({N, H, W, C}, dout.options());
+  CHECK_RC(pmd::maxpool_bwd_launch(bfp(dout), arg.data_ptr<uint8_t>(), bfp_mut(dx), N, (int)H, (int)W,
+                                   C, P, Q, cur_stream()), "maxpool_bwd");
+  return dx;
+}
+
+Tensor avgpool_fwd(Tensor x) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONT(x);
+  const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  c10::DeviceGuard g(x.device());
+  Tensor out = torch::empty({N, C}, x.options().dtype(torch::kFloat32));
+  CHECK_RC(pmd::avgpool_fwd_launch(bfp(x), out.data_ptr<float>(), N, HW, C, cur_stream()), "avgpool");
+  return out;
+}
+
+Tensor avgpool_bwd(Tensor dout, int64_t H, int64_t W) {
+  CHECK_DEV(dout); CHECK_F32(dout); CHECK_CONT(dout);
+  const int N = dout.size(0), C = dout.size(1);
+  c10::DeviceGuard g(dout.device());
+  Tensor dx = torch::empty({N, H, W, C}, dout.options().dtype(torch::kBFloat16));
+  CHECK_RC(pmd::avgpool_bwd_launch(dout.data_ptr<float>(), bfp_mut(dx), N, (int)(H * W), C,
+                                   cur_stream()), "avgpool_bwd");
+  return dx;
+}
+
+// ------------------------------------------------------------------ loss
+std::vector<Tensor> xent_fwd(Tensor logits, Tensor target) {
+  CHECK_DEV(logits); CHECK_F32(logits); CHECK_CONT(logits);
+  TORCH_CHECK(target.scalar_type() == torch::kInt64 && target.is_cuda(), "target int64 GPU");
+  const int N = logits.size(0), V = logits.size(1);
+  c10::DeviceGuard g(logits.device());
+  Tensor loss = torch::zeros({1}, logits.options());
+  Tensor lse = torch::empty({N}, logits.options());
+  Tensor correct = torch::zeros({1}, logits.options().dtype(torch::kInt64));
+  Tensor tg = target.contiguous();
+  pmd::xent_fwd_launch(logits.data_ptr<float>(), reinterpret_cast<const long long*>(tg.data_ptr<int64_t>()),
+                       loss.data_ptr<float>(), lse.data_ptr<float>(),
+                       reinterpret_cast<long long*>(correct.data_ptr<int64_t>()), N, V, cur_stream());
+  return {loss, lse, correct};
+}
+
+Tensor xent_bwd(Tensor logits, Tensor target, Tensor lse, Tensor gloss) {
+  CHECK_DEV(logits); CHECK_F32(logits); CHECK_CONT(logits);
+  const int N = logits.size(0), V = logits.size(1);
+  c10::DeviceGuard g(logits.device());
+  Tensor grad = torch::empty_like(logits);
+  Tensor tg = target.contiguous(), gl = gloss.to(torch::kFloat32).contiguous();
+  pmd::xent_bwd_launch(logits.data_ptr<float>(), reinterpret_cast<const long long*>(tg.data_ptr<int64_t>()),
+                       lse.data_ptr<float>(), gl.data_ptr<float>(), grad.data_ptr<float>(), N, V,
+                       cur_stream());
+  return grad;
+}
+
+// ------------------------------------------------------------------ optim
+void sgd_(Tensor p, Tensor g, Tensor buf, double lr, double momentum, double wd, double damp,
+          bool nesterov, bool first) {
+  CHECK_DEV(p); CHECK_F32(p); CHECK_CONT(p);
+  CHECK_F32(g); CHECK_CONT(g); CHECK_F32(buf); CHECK_CONT(buf);
+  TORCH_CHECK(p.numel() == g.numel() && p.numel() == buf.numel(), "arena sizes differ");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(p.data_ptr()) % 16 == 0 &&
+              reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0 &&
+              reinterpret_cast<uintptr_t>(buf.data_ptr()) % 16 == 0, "arenas must be 16-B aligned");
+  c10::DeviceGuard gd(p.device());
+  pmd::sgd_launch(p.data_ptr<float>(), g.data_ptr<float>(), buf.data_ptr<float>(), p.numel(), (float)lr,
+                  (float)momentum, (float)wd, (float)damp, nesterov, first, cur_stream());
+}
+
+// ------------------------------------------------------------------- data
+std::vector<Tensor> synth_images(int64_t N, int64_t H, int64_t W, int64_t Cp, int64_t Creal,
+                                 int64_t classes, int64_t seed, int64_t device) {
+  auto dev = torch::Device(torch::kCUDA, (c10::DeviceIndex)device);
+  c10::DeviceGuard g(dev);
+  Tensor x = torch::empty({N, H, W, Cp}, torch::TensorOptions().device(dev).dtype(torch::kBFloat16));
+  Tensor y = torch::empty({N}, torch::TensorOptions().device(dev).dtype(torch::kInt64));
+  CHECK_RC(pmd::synth_images_launch(bfp_mut(x), reinterpret_cast<long long*>(y.data_ptr<int64_t>()), N,
+                                    H, W, Cp, Creal, classes, (unsigned long long)seed, cur_stream()),
+           "synth_images");
+  return {x, y};
+}
+
+Tensor cifar_augment(Tensor data, Tensor idx, int64_t Cp, bool train, int64_t pad, int64_t seed,
+                     int64_t epoch, bool out_bf16) {
+  CHECK_DEV(data); CHECK_CONT(data);
+  TORCH_CHECK(data.scalar_type() == torch::kUInt8 && data.dim() == 4 && data.size(1) == 32 &&
+              data.size(2) == 32 && data.size(3) == 3, "data must be uint8 [Nd,32,32,3]");
+  TORCH_CHECK(idx.scalar_type() == torch::kInt64 && idx.is_cuda(), "idx int64 GPU");
+  const int B = idx.numel();
+  c10::DeviceGuard g(data.device());
+  Tensor out = torch::empty({B, 32, 32, Cp}, data.options().dtype(out_bf16 ? torch::kBFloat16 : torch::kFloat32));
+  Tensor ix = idx.contiguous();
+  pmd::cifar_augment_launch(data.data_ptr<uint8_t>(), reinterpret_cast<const long long*>(ix.data_ptr<int64_t>()),
+                            out.data_ptr(), out_bf16, B, Cp, train, pad, (unsigned long long)seed, epoch,
+                            cur_stream());
+  return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "gfx950 (MI355X) kernels for pytorch_multiprocessing_distributed_amd";
+  m.def("conv_weight_prep", &conv_weight_prep);
+  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("bn_finalize", &bn_finalize);
+  m.def("bn_apply", &bn_apply);
+  m.def("bn_bwd_reduce", &bn_bwd_reduce);
+  m.def("bn_bwd_elemt", &bn_bwd_elemt);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("xent_fwd", &xent_fwd);
+  m.def("xent_bwd", &xent_bwd);
+  m.def("sgd_", &sgd_);
+  m.def("synth_images", &synth_images);
+  m.def("cifar_augment", &cifar_augment);
+}

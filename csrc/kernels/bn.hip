@@ -1,0 +1,275 @@
+// Synchronised-BatchNorm family on NHWC bf16 activations (gfx950).
+//
+// Statistics are produced by the conv epilogue (conv_igemm.hip); these
+// kernels cover the rest of torch's SyncBN autograd Function
+// (torch:nn/modules/_functions.py:39-207) with the ReLU and residual add of
+// the ResNet block (reference model/resnet.py:36-39, 66-70) fused in:
+//
+//   bn_finalize   (sum, sum^2, count) -> mean, invstd, scale, shift;
+//                 running_mean/var momentum update (unbiased var) and
+//                 num_batches_tracked += 1, all on device (no host sync)
+//   bn_apply      out = relu(y1*sc1+sh1 [+ y2*sc2+sh2 | + res])       1 pass
+//   bn_bwd_reduce sum(dz*mask), sum(dz*mask*xhat) per channel          1 pass
+//   bn_bwd_elemt  dy = a*dzm + b*y + c (per-channel a,b,c), optional
+//                 dzm output for the identity-shortcut gradient        1 pass
+//
+// All elementwise kernels move 16 B (8 channels) per lane per stream and keep
+// a fixed channel chunk per thread (grid*256 is a multiple of C/8), so the
+// per-channel coefficients are loaded once per thread.
+#include "common.h"
+
+namespace pmd {
+
+__device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// params out: [4][C] = mean, invstd, scale, shift
+__global__ void bn_finalize_kernel(const float* __restrict__ sums, const float* __restrict__ count,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   float* __restrict__ params, float* running_mean,
+                                   float* running_var, long long* nbt, int C, float eps,
+                                   float momentum, int eval_mode) {
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+    float mean, var;
+    if (eval_mode) {
+      mean = running_mean[c];
+      var = running_var[c];
+    } else {
+      const float cnt = count[0];
+      mean = sums[c] / cnt;
+      var = fmaxf(sums[C + c] / cnt - mean * mean, 0.f);
+    }
+    const float invstd = rsqrtf(var + eps);
+    const float sc = gamma[c] * invstd;
+    params[c] = mean;
+    params[C + c] = invstd;
+    params[2 * C + c] = sc;
+    params[3 * C + c] = beta[c] - mean * sc;
+    if (!eval_mode && running_mean) {
+      const float cnt = count[0];
+      const float unb = var * (cnt / fmaxf(cnt - 1.f, 1.f));
+      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+      running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+    }
+  }
+  if (!eval_mode && nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
+}
+
+// MODE 0: out = act(y1*s1+b1); 1: + res; 2: + y2*s2+b2
+template <int MODE, bool RELU>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ y1,
+                                                       const float* __restrict__ p1,
+                                                       const bf16_t* __restrict__ r,
+                                                       const float* __restrict__ p2,
+                                                       bf16_t* __restrict__ out, long long nchunk,
+                                                       int C) {
+  const int C8 = C >> 3;
+  const long long start = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long step = (long long)gridDim.x * blockDim.x;
+  const int c0 = (int)(start % C8) * 8;
+  float s1[8], b1[8], s2[8], b2[8];
+  load8f(p1 + 2 * C + c0, s1);
+  load8f(p1 + 3 * C + c0, b1);
+  if (MODE == 2) {
+    load8f(p2 + 2 * C + c0, s2);
+    load8f(p2 + 3 * C + c0, b2);
+  }
+  for (long long i = start; i < nchunk; i += step) {
+    float v[8], w[8];
+    unpack8(reinterpret_cast<const uint4*>(y1)[i], v);
+    if (MODE >= 1) unpack8(reinterpret_cast<const uint4*>(r)[i], w);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float o = v[k] * s1[k] + b1[k];
+      if (MODE == 1) o += w[k];
+      if (MODE == 2) o += w[k] * s2[k] + b2[k];
+      if (RELU) o = fmaxf(o, 0.f);
+      v[k] = o;
+    }
+    reinterpret_cast<uint4*>(out)[i] = pack8(v);
+  }
+}
+
+// red out: [2][C] += (sum dzm, sum dzm*xhat); TPR = C/8 threads per row (<= 256)
+template <bool RELU>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __restrict__ dout,
+                                                            const bf16_t* __restrict__ out,
+                                                            const bf16_t* __restrict__ y,
+                                                            const float* __restrict__ params,
+                                                            float* __restrict__ red, int M, int C) {
+  __shared__ float part[256 * 17];
+  const int C8 = C >> 3;
+  const int tid = threadIdx.x;
+  const int cc = tid % C8;
+  const int rpi = 256 / C8;
+  const int c0 = cc * 8;
+  float mean[8], inv[8];
+  load8f(params + c0, mean);
+  load8f(params + C + c0, inv);
+  float s1[8], s2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
+  for (int row = blockIdx.x * rpi + tid / C8; row < M; row += gridDim.x * rpi) {
+    const long long i = (long long)row * C8 + cc;
+    float d[8], o[8], v[8];
+    unpack8(reinterpret_cast<const uint4*>(dout)[i], d);
+    if (RELU) unpack8(reinterpret_cast<const uint4*>(out)[i], o);
+    unpack8(reinterpret_cast<const uint4*>(y)[i], v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float dz = (RELU && !(o[k] > 0.f)) ? 0.f : d[k];
+      s1[k] += dz;
+      s2[k] += dz * (v[k] - mean[k]) * inv[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    part[tid * 17 + k] = s1[k];
+    part[tid * 17 + 8 + k] = s2[k];
+  }
+  __syncthreads();
+  if (tid < C8) {
+    float a1[8], a2[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a1[k] = a2[k] = 0.f;
+    for (int rr = 0; rr < rpi; ++rr) {
+      const int t = rr * C8 + tid;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        a1[k] += part[t * 17 + k];
+        a2[k] += part[t * 17 + 8 + k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      atomicAdd(red + c0 + k, a1[k]);
+      atomicAdd(red + C + c0 + k, a2[k]);
+    }
+  }
+}
+
+// dy = a*dzm + b*y + c.  train: a = g*inv, b = -a*inv*mdyx, c = a*(mean*inv*mdyx - mdy)
+//                        eval : a = scale, b = c = 0
+template <bool RELU, bool DZM, bool EVAL>
+__global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(
+    const bf16_t* __restrict__ dout, const bf16_t* __restrict__ out, const bf16_t* __restrict__ y,
+    const float* __restrict__ params, const float* __restrict__ gamma,
+    const float* __restrict__ red, const float* __restrict__ count, bf16_t* __restrict__ dy,
+    bf16_t* __restrict__ dzm_out, long long nchunk, int C) {
+  const int C8 = C >> 3;
+  const long long start = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long step = (long long)gridDim.x * blockDim.x;
+  const int c0 = (int)(start % C8) * 8;
+  float ca[8], cb[8], cc[8];
+  if (EVAL) {
+    load8f(params + 2 * C + c0, ca);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cb[k] = cc[k] = 0.f;
+  } else {
+    const float inv_cnt = 1.f / count[0];
+    float mean[8], inv[8], g[8], r0[8], r1[8];
+    load8f(params + c0, mean);
+    load8f(params + C + c0, inv);
+    load8f(gamma + c0, g);
+    load8f(red + c0, r0);
+    load8f(red + C + c0, r1);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float a = g[k] * inv[k];
+      const float mdy = r0[k] * inv_cnt, mdyx = r1[k] * inv_cnt;
+      ca[k] = a;
+      cb[k] = -a * inv[k] * mdyx;
+      cc[k] = a * (mean[k] * inv[k] * mdyx - mdy);
+    }
+  }
+  for (long long i = start; i < nchunk; i += step) {
+    float d[8], o[8], v[8];
+    unpack8(reinterpret_cast<const uint4*>(dout)[i], d);
+    if (RELU) unpack8(reinterpret_cast<const uint4*>(out)[i], o);
+    if (!EVAL) unpack8(reinterpret_cast<const uint4*>(y)[i], v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float dz = (RELU && !(o[k] > 0.f)) ? 0.f : d[k];
+      d[k] = dz;
+      o[k] = EVAL ? ca[k] * dz : ca[k] * dz + cb[k] * v[k] + cc[k];
+    }
+    reinterpret_cast<uint4*>(dy)[i] = pack8(o);
+    if (DZM) reinterpret_cast<uint4*>(dzm_out)[i] = pack8(d);
+  }
+}
+
+static int ew_grid(long long nchunk, int C8) {
+  long long b = (nchunk + 255) / 256;
+  if (b > 2048) b = 2048;
+  if (b < 1) b = 1;
+  // keep grid*256 a multiple of C8 (C8 is a power of two <= 256, so always true)
+  return (int)b;
+}
+
+int bn_finalize_launch(const float* sums, const float* count, const float* gamma, const float* beta,
+                       float* params, float* rm, float* rv, long long* nbt, int C, float eps,
+                       float momentum, bool eval_mode, hipStream_t st) {
+  const int blocks = (C + 255) / 256;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(blocks), dim3(256), 0, st, sums, count, gamma, beta,
+                     params, rm, rv, nbt, C, eps, momentum, eval_mode ? 1 : 0);
+  return 0;
+}
+
+int bn_apply_launch(const bf16_t* y1, const float* p1, const bf16_t* r, const float* p2, bf16_t* out,
+                    long long M, int C, int mode, bool relu, hipStream_t st) {
+  if (C % 8 || (C >> 3) > 256 || ((C >> 3) & ((C >> 3) - 1))) return 1;
+  const long long nchunk = M * (C / 8);
+  const int g = ew_grid(nchunk, C / 8);
+#define APPLY(MD, RL) \
+  hipLaunchKernelGGL((bn_apply_kernel<MD, RL>), dim3(g), dim3(256), 0, st, y1, p1, r, p2, out, nchunk, C)
+  if (relu) {
+    if (mode == 0) APPLY(0, true); else if (mode == 1) APPLY(1, true); else APPLY(2, true);
+  } else {
+    if (mode == 0) APPLY(0, false); else if (mode == 1) APPLY(1, false); else APPLY(2, false);
+  }
+#undef APPLY
+  return 0;
+}
+
+int bn_bwd_reduce_launch(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const float* params,
+                         float* red, int M, int C, bool relu, hipStream_t st) {
+  const int C8 = C / 8;
+  if (C % 8 || C8 > 256 || (C8 & (C8 - 1))) return 1;
+  const int rpi = 256 / C8;
+  long long b = ((long long)M + rpi - 1) / rpi;
+  if (b > 1024) b = 1024;
+  if (relu)
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true>), dim3((int)b), dim3(256), 0, st, dout, out, y,
+                       params, red, M, C);
+  else
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false>), dim3((int)b), dim3(256), 0, st, dout, out, y,
+                       params, red, M, C);
+  return 0;
+}
+
+int bn_bwd_elemt_launch(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const float* params,
+                        const float* gamma, const float* red, const float* count, bf16_t* dy,
+                        bf16_t* dzm, long long M, int C, bool relu, bool eval_mode, hipStream_t st) {
+  if (C % 8 || (C >> 3) > 256 || ((C >> 3) & ((C >> 3) - 1))) return 1;
+  const long long nchunk = M * (C / 8);
+  const int g = ew_grid(nchunk, C / 8);
+#define EL(RL, DZ, EV)                                                                            \
+  hipLaunchKernelGGL((bn_bwd_elemt_kernel<RL, DZ, EV>), dim3(g), dim3(256), 0, st, dout, out, y, \
+                     params, gamma, red, count, dy, dzm, nchunk, C)
+  const bool dz = dzm != nullptr;
+  if (eval_mode) {
+    if (relu) { if (dz) EL(true, true, true); else EL(true, false, true); }
+    else { if (dz) EL(false, true, true); else EL(false, false, true); }
+  } else {
+    if (relu) { if (dz) EL(true, true, false); else EL(true, false, false); }
+    else { if (dz) EL(false, true, false); else EL(false, false, false); }
+  }
+#undef EL
+  return 0;
+}
+
+}  // namespace pmd

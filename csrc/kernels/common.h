@@ -1,0 +1,64 @@
+// Shared device helpers for the gfx950 (CDNA4, MI355X) kernels.
+// Pure HIP: no torch headers here, so each kernel TU compiles in seconds.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "launchers.h"
+
+namespace pmd {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef unsigned short bf16_t;  // storage type of one bf16
+
+constexpr int kWave = 64;  // CDNA wavefront
+
+__device__ __forceinline__ float bf2f(bf16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
+
+// round-to-nearest-even; hipcc lowers the cast to v_cvt_pk_bf16_f32 (NaN-safe)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 h = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, h);
+}
+
+__device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
+
+// 8 bf16 <-> uint4 helpers
+__device__ __forceinline__ void unpack8(const uint4& v, float (&f)[8]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    w[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// Bijective XCD-aware block remap (MI355X: 8 XCDs, blocks dispatched
+// round-robin).  Blocks that share an XCD (same id % 8) get consecutive
+// logical tile ids so neighbouring tiles reuse operand panels in that XCD's
+// L2.  Speed-only: correctness never depends on placement.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  constexpr int NX = 8;
+  if (nwg < NX) return bid;
+  const int q = nwg / NX, r = nwg % NX;
+  const int x = bid % NX, j = bid / NX;
+  const int base = (x < r) ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  return base + j;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace pmd

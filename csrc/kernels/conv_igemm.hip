@@ -1,0 +1,332 @@
+// Implicit-GEMM convolution on gfx950 MFMA (v_mfma_f32_16x16x32_bf16).
+//
+//   FWD  : Y[m = (n,p,q)][k]  = sum_{r,s,c} X[n, p*st-pad+r, q*st-pad+s, c] * W[k,r,s,c]
+//   DGRAD: dX[m = (n,h,w)][c] = sum_{r,s,k} dY[n, (h+pad-r)/st, (w+pad-s)/st, k] * W[k,r,s,c]
+//                                (taps whose numerator is not divisible by st are skipped)
+//
+// Both are the same GEMM  C[M][Nout] = A[M][Kg] * B[Kg][Nout]  where A is the
+// on-the-fly im2col gather of an NHWC activation (Kg ordered (r, s, c)) and
+// B^T is a [Nout][Kg] row-major bf16 weight image (KRSC for fwd, CRSK for
+// dgrad).  Because NHWC keeps the channel contiguous, every 16-byte (8 x bf16)
+// chunk of an A row is one contiguous load for any C % 8 == 0 -- no im2col
+// buffer, and the 3-channel stem only needs zero-padding to C = 8.
+//
+// Tile: BM x BN x 64, 256 threads = 4 waves in a 2x2 grid, each wave owns a
+// (BM/2)x(BN/2) sub-tile of 16x16 MFMA accumulators.  Operands are register-
+// staged global->VGPR->LDS (double-buffered LDS, one barrier per K-tile; the
+// next tile's global loads are in flight while the current tile's MFMAs run).
+// LDS rows are padded to 144 B so the 16 rows read by one ds_read_b128 lane
+// group hit 16 distinct 16-B bank slots.
+//
+// Epilogue (fwd): optional per-output-channel (sum, sum^2) of the bf16-rounded
+// outputs for BatchNorm (combined across the block's waves in LDS, one fp32
+// atomic per channel per block), then the tile is staged through LDS and
+// written with coalesced 16-byte row stores.
+#include "common.h"
+
+namespace pmd {
+
+struct ConvArgs {
+  const bf16_t* src;  // gathered operand, NHWC [N, H, W, Cs]
+  const bf16_t* wt;   // B^T image [Nout][Kg]
+  bf16_t* out;        // [M][Nout]
+  float* stats;       // [2][Nout] or nullptr
+  int N, H, W, Cs, log2Cs;
+  int OH, OW;
+  int Nout, R, S, stride, log2stride, pad;
+  int M, Kg;
+};
+
+constexpr int BK = 64;
+constexpr int LDA = BK + 8;  // padded LDS row (elements)
+
+template <int BM, int BN, bool DGRAD, bool STATS>
+__global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
+  constexpr int PA = BM / 32;        // A rows per thread
+  constexpr int PB = BN / 32;        // B rows per thread
+  constexpr int MI = BM / 32;        // 16-row MFMA tiles per wave (wave covers BM/2)
+  constexpr int NI = BN / 32;        // 16-col MFMA tiles per wave
+  constexpr int A_ELEMS = BM * LDA;
+  constexpr int B_ELEMS = BN * LDA;
+  constexpr int STAGE = A_ELEMS + B_ELEMS;
+  constexpr int LDC = BN + 8;
+  constexpr int SMEM_MAIN = 2 * STAGE * 2;
+  constexpr int SMEM_EPI = BM * LDC * 2;
+  constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM + (STATS ? 2 * 2 * BN * 4 : 0)];
+  bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  const int tilesN = (a.Nout + BN - 1) / BN;
+  const int tilesM = (a.M + BM - 1) / BM;
+  const int L = xcd_remap(blockIdx.x, tilesM * tilesN);
+  const int m0 = (L / tilesN) * BM;
+  const int n0 = (L % tilesN) * BN;
+
+  // ---- per-thread A-row precompute
+  const int chunk = tid & 7;
+  const int rsub = tid >> 3;  // 0..31
+  int a_base[PA], a_h[PA], a_w[PA];
+  bool a_ok[PA];
+  const int ohw = a.OH * a.OW;
+#pragma unroll
+  for (int i = 0; i < PA; ++i) {
+    const int m = m0 + rsub + 32 * i;
+    a_ok[i] = m < a.M;
+    const int mm = a_ok[i] ? m : 0;
+    const int n = mm / ohw;
+    const int rem = mm - n * ohw;
+    const int oh = rem / a.OW;
+    const int ow = rem - oh * a.OW;
+    a_base[i] = n * a.H * a.W;  // pixel index base
+    if (DGRAD) {
+      a_h[i] = oh + a.pad;
+      a_w[i] = ow + a.pad;
+    } else {
+      a_h[i] = oh * a.stride - a.pad;
+      a_w[i] = ow * a.stride - a.pad;
+    }
+  }
+  const bf16_t* b_row[PB];
+  bool b_ok[PB];
+#pragma unroll
+  for (int i = 0; i < PB; ++i) {
+    const int nn = n0 + rsub + 32 * i;
+    b_ok[i] = nn < a.Nout;
+    b_row[i] = a.wt + (size_t)(b_ok[i] ? nn : 0) * a.Kg;
+  }
+
+  uint4 ra[PA], rb[PB];
+  const int nk = (a.Kg + BK - 1) / BK;
+
+  auto load_tile = [&](int kt) {
+    const int k0 = kt * BK + chunk * 8;
+    const bool kok = k0 < a.Kg;
+    const int tap = k0 >> a.log2Cs;
+    const int c = k0 & (a.Cs - 1);
+    const int r = tap / a.S;
+    const int s = tap - r * a.S;
+#pragma unroll
+    for (int i = 0; i < PA; ++i) {
+      int ih, iw;
+      bool ok = a_ok[i] && kok;
+      if (DGRAD) {
+        const int th = a_h[i] - r, tw = a_w[i] - s;
+        ok = ok && th >= 0 && tw >= 0 && ((th | tw) & (a.stride - 1)) == 0;
+        ih = th >> a.log2stride;
+        iw = tw >> a.log2stride;
+      } else {
+        ih = a_h[i] + r;
+        iw = a_w[i] + s;
+      }
+      ok = ok && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (ok) {
+        const size_t pix = (size_t)(a_base[i] + ih * a.W + iw);
+        v = *reinterpret_cast<const uint4*>(a.src + (pix << a.log2Cs) + c);
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (b_ok[i] && kok) v = *reinterpret_cast<const uint4*>(b_row[i] + k0);
+      rb[i] = v;
+    }
+  };
+  auto store_tile = [&](int buf) {
+    bf16_t* As = lds + buf * STAGE;
+    bf16_t* Bs = As + A_ELEMS;
+#pragma unroll
+    for (int i = 0; i < PA; ++i)
+      *reinterpret_cast<uint4*>(As + (rsub + 32 * i) * LDA + chunk * 8) = ra[i];
+#pragma unroll
+    for (int i = 0; i < PB; ++i)
+      *reinterpret_cast<uint4*>(Bs + (rsub + 32 * i) * LDA + chunk * 8) = rb[i];
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+
+  const int frow = lane & 15;
+  const int fk = (lane >> 4) * 8;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) load_tile(kt + 1);
+    const bf16_t* As = lds + buf * STAGE + (wm * (BM / 2)) * LDA;
+    const bf16_t* Bs = lds + buf * STAGE + A_ELEMS + (wn * (BN / 2)) * LDA;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 af[MI], bfg[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(As + (i * 16 + frow) * LDA + ks * 32 + fk);
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        bfg[j] = *reinterpret_cast<const bf16x8*>(Bs + (j * 16 + frow) * LDA + ks * 32 + fk);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue
+  bf16_t* Cs = lds;
+  const int crow0 = wm * (BM / 2) + (lane >> 4) * 4;
+  const int ccol0 = wn * (BN / 2) + (lane & 15);
+  float csum[NI], csq[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    csum[j] = 0.f;
+    csq[j] = 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bf16_t h = f2bf(acc[i][j][e]);
+        Cs[(crow0 + i * 16 + e) * LDC + ccol0 + j * 16] = h;
+        if (STATS) {
+          const float v = bf2f(h);
+          csum[j] += v;
+          csq[j] += v * v;
+        }
+      }
+  if (STATS) {
+    float* st = reinterpret_cast<float*>(smem + SMEM);  // [2 wm][2][BN]
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      float s1 = csum[j], s2 = csq[j];
+      s1 += __shfl_xor(s1, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (lane < 16) {
+        st[(wm * 2 + 0) * BN + ccol0 + j * 16] = s1;
+        st[(wm * 2 + 1) * BN + ccol0 + j * 16] = s2;
+      }
+    }
+  }
+  __syncthreads();
+  if (STATS) {
+    const float* st = reinterpret_cast<const float*>(smem + SMEM);
+    for (int c = tid; c < 2 * BN; c += 256) {
+      const int which = c / BN, col = c % BN;
+      if (n0 + col < a.Nout) {
+        const float v = st[(0 * 2 + which) * BN + col] + st[(1 * 2 + which) * BN + col];
+        atomicAdd(a.stats + which * a.Nout + n0 + col, v);
+      }
+    }
+  }
+  constexpr int CPR = BN / 8;  // 16-B chunks per output row
+  for (int idx = tid; idx < BM * CPR; idx += 256) {
+    const int row = idx / CPR, cc = idx % CPR;
+    const int m = m0 + row, n = n0 + cc * 8;
+    if (m < a.M && n < a.Nout)
+      *reinterpret_cast<uint4*>(a.out + (size_t)m * a.Nout + n) =
+          *reinterpret_cast<const uint4*>(Cs + row * LDC + cc * 8);
+  }
+}
+
+// fp32 param (physical K,R,S,C = channels_last [K,C,R,S]) -> bf16 images:
+//   wk  [K][R][S][Cp]   (B^T of the forward GEMM, zero-padded channels)
+//   wkt [Cp][R][S][K]   (B^T of the dgrad GEMM), optional
+__global__ void conv_weight_prep_kernel(const float* __restrict__ w, bf16_t* __restrict__ wk,
+                                        bf16_t* __restrict__ wkt, int K, int RS, int C, int Cp) {
+  const int total = K * RS * Cp;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c = i % Cp;
+    const int rs = (i / Cp) % RS;
+    const int k = i / (Cp * RS);
+    const float v = c < C ? w[((size_t)k * RS + rs) * C + c] : 0.f;
+    const bf16_t h = f2bf(v);
+    wk[i] = h;
+    if (wkt) wkt[((size_t)c * RS + rs) * K + k] = h;
+  }
+}
+
+static int ilog2(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return l;
+}
+
+template <int BM, int BN, bool DGRAD, bool STATS>
+static void launch_t(const ConvArgs& a, hipStream_t st) {
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, DGRAD, STATS>), dim3(tiles), dim3(256), 0, st, a);
+}
+
+template <bool DGRAD, bool STATS>
+static void launch_sel(const ConvArgs& a, hipStream_t st) {
+  if (a.Nout <= 64)
+    launch_t<128, 64, DGRAD, STATS>(a, st);
+  else
+    launch_t<128, 128, DGRAD, STATS>(a, st);
+}
+
+// Returns 0 on success, nonzero on unsupported shape.
+int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* stats, int N, int H,
+                      int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
+                      bool dgrad, hipStream_t st) {
+  if (Cs % 8 != 0 || (Cs & (Cs - 1)) != 0) return 1;  // power-of-two channels (>= 8)
+  if (Nout % 8 != 0) return 2;
+  if (stride != 1 && stride != 2) return 3;
+  ConvArgs a;
+  a.src = src;
+  a.wt = wt;
+  a.out = out;
+  a.stats = stats;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.Cs = Cs;
+  a.log2Cs = ilog2(Cs);
+  a.OH = OH;
+  a.OW = OW;
+  a.Nout = Nout;
+  a.R = R;
+  a.S = S;
+  a.stride = stride;
+  a.log2stride = ilog2(stride);
+  a.pad = pad;
+  const long long M = (long long)N * OH * OW;
+  if (M >= (1ll << 31) || (long long)N * H * W >= (1ll << 31)) return 4;
+  a.M = (int)M;
+  a.Kg = R * S * Cs;
+  if (dgrad) {
+    if (stats) launch_sel<true, true>(a, st);
+    else launch_sel<true, false>(a, st);
+  } else {
+    if (stats) launch_sel<false, true>(a, st);
+    else launch_sel<false, false>(a, st);
+  }
+  return 0;
+}
+
+void conv_weight_prep_launch(const float* w, bf16_t* wk, bf16_t* wkt, int K, int RS, int C, int Cp,
+                             hipStream_t st) {
+  const int total = K * RS * Cp;
+  const int blocks = (total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096;
+  hipLaunchKernelGGL(conv_weight_prep_kernel, dim3(blocks), dim3(256), 0, st, w, wk, wkt, K, RS, C,
+                     Cp);
+}
+
+}  // namespace pmd

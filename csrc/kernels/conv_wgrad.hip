@@ -1,0 +1,258 @@
+// Convolution weight gradient on gfx950 MFMA, split-K over the batch*spatial axis.
+//
+//   dW[k][(r,s,c)] = sum_{m=(n,p,q)} dY[m][k] * X[n, p*st-pad+r, q*st-pad+s, c]
+//
+// GEMM view: rows = output channels (BM), cols = Kg = R*S*C (BN), reduction
+// over m = N*P*Q (hundreds of thousands).  Both operands arrive reduction-
+// major (m rows, channels contiguous), so each 64-row chunk of dY and of the
+// im2col'd X is staged into LDS in natural row order and the MFMA fragments
+// (8 consecutive m of one column) are read with the CDNA4 hardware transpose
+// read ds_read_b64_tr_b16.  LDS rows are XOR-swizzled at 32-byte granularity
+// so the 8 rows a 32-lane half touches in one transposed read land in 8
+// distinct bank windows.
+//
+// The m axis is split over blocks (enough blocks to fill the 256 CUs); each
+// block reduces its range in registers and adds its fp32 tile into dW with
+// one atomic per element.  Each thread's im2col column (r, s, c) is fixed for
+// the whole kernel and the per-row (n, p, q) coordinates advance by
+// single-carry increments, so the gather costs no integer divisions in the
+// main loop.
+#include "common.h"
+
+namespace pmd {
+
+struct WgradArgs {
+  const bf16_t* dy;  // [M][K]
+  const bf16_t* x;   // NHWC [N, H, W, C]
+  float* dw;         // [K][Kg] fp32, pre-zeroed
+  int N, H, W, C, log2C;
+  int P, Q, K, R, S, stride, pad;
+  int M, Kg;
+  int chunks_per_split;  // 64-row chunks per block
+};
+
+constexpr int BR = 64;  // reduction rows per stage
+
+template <int ROWB>
+__device__ __forceinline__ int swz(int row) {
+  if (ROWB == 256) return (row & 3) | (((row >> 3) & 1) << 2);
+  return ((row >> 1) & 1) | ((row >> 2) & 2);  // 128-byte rows
+}
+
+// byte offset of element `col` of `row` in a [BR][COLS] bf16 tile with 32-B-window swizzle
+template <int COLS>
+__device__ __forceinline__ int toff(int row, int col) {
+  constexpr int ROWB = COLS * 2;
+  const int byte = col * 2;
+  return row * ROWB + (((byte >> 5) ^ swz<ROWB>(row)) << 5) + (byte & 31);
+}
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
+  constexpr int MI = BM / 32, NI = BN / 32;
+  constexpr int A_BYTES = BR * BM * 2, B_BYTES = BR * BN * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tilesM = a.K / BM + (a.K % BM != 0);
+  const int tilesN = (a.Kg + BN - 1) / BN;
+  const int tiles = tilesM * tilesN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = L / tiles;
+  const int t = L % tiles;
+  const int k0 = (t / tilesN) * BM;
+  const int g0 = (t % tilesN) * BN;
+  const int mbeg = split * a.chunks_per_split * BR;
+  if (mbeg >= a.M) return;
+  int mend = mbeg + a.chunks_per_split * BR;
+  if (mend > a.M) mend = a.M;
+  const int nchunks = (mend - mbeg + BR - 1) / BR;
+
+  // dY loader: CA chunks (16 B) per row, RA rows per pass
+  constexpr int CA = BM / 8, RA = 256 / CA, PA = BR / RA;
+  const int a_col = (tid % CA) * 8;
+  const int a_row = tid / CA;
+  const bool a_colok = k0 + a_col < a.K;
+  // X loader: CB chunks per row
+  constexpr int CB = BN / 8, RB = 256 / CB, PB = BR / RB;
+  const int b_col = (tid % CB) * 8;
+  const int b_row = tid / CB;
+  const int kg = g0 + b_col;
+  const bool b_colok = kg < a.Kg;
+  const int tap = kg >> a.log2C;
+  const int cch = kg & (a.C - 1);
+  const int rr = tap / a.S, ss = tap - (tap / a.S) * a.S;
+  // per-pass row coordinates (n, p, q) of m = mbeg + b_row + RB*i, advanced by BR per chunk
+  int bn_[PB], bp_[PB], bq_[PB];
+  const int pq = a.P * a.Q;
+#pragma unroll
+  for (int i = 0; i < PB; ++i) {
+    const int m = mbeg + b_row + RB * i;
+    const int n = m / pq, rem = m - n * pq;
+    bn_[i] = n;
+    bp_[i] = rem / a.Q;
+    bq_[i] = rem - bp_[i] * a.Q;
+  }
+  const int dq = BR % a.Q, dp = (BR / a.Q) % a.P, dn = BR / pq;
+
+  uint4 ra[PA], rb[PB];
+  auto load = [&](int ch) {
+    const int mb = mbeg + ch * BR;
+#pragma unroll
+    for (int i = 0; i < PA; ++i) {
+      const int m = mb + a_row + RA * i;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (a_colok && m < mend) v = *reinterpret_cast<const uint4*>(a.dy + (size_t)m * a.K + k0 + a_col);
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+      const int m = mb + b_row + RB * i;
+      const int ih = bp_[i] * a.stride - a.pad + rr;
+      const int iw = bq_[i] * a.stride - a.pad + ss;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (b_colok && m < mend && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W) {
+        const size_t pix = ((size_t)bn_[i] * a.H + ih) * a.W + iw;
+        v = *reinterpret_cast<const uint4*>(a.x + (pix << a.log2C) + cch);
+      }
+      rb[i] = v;
+      // advance this row by BR (single-carry; dq < Q, dp < P)
+      int q = bq_[i] + dq, c1 = q >= a.Q;
+      q -= c1 ? a.Q : 0;
+      int p = bp_[i] + dp + c1, c2 = p >= a.P;
+      p -= c2 ? a.P : 0;
+      bq_[i] = q;
+      bp_[i] = p;
+      bn_[i] += dn + c2;
+    }
+  };
+  auto store = [&](int buf) {
+    char* As = smem + buf * STAGE;
+    char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < PA; ++i)
+      *reinterpret_cast<uint4*>(As + toff<BM>(a_row + RA * i, a_col)) = ra[i];
+#pragma unroll
+    for (int i = 0; i < PB; ++i)
+      *reinterpret_cast<uint4*>(Bs + toff<BN>(b_row + RB * i, b_col)) = rb[i];
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load(0);
+  store(0);
+  __syncthreads();
+
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const int buf = ch & 1;
+    if (ch + 1 < nchunks) load(ch + 1);
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < BR / 32; ++ks) {
+      bf16x8 af[MI], bfg[NI];
+      const int r0 = ks * 32 + 8 * g + q4;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int col = wm * (BM / 2) + i * 16 + 4 * p4;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(As + toff<BM>(r0, col)));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(As + toff<BM>(r0 + 4, col)));
+        typedef __attribute__((ext_vector_type(8))) short s16x8;
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int col = wn * (BN / 2) + j * 16 + 4 * p4;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(Bs + toff<BN>(r0, col)));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(Bs + toff<BN>(r0 + 4, col)));
+        typedef __attribute__((ext_vector_type(8))) short s16x8;
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfg[j] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+    }
+    if (ch + 1 < nchunks) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: fp32 atomics into dW[k][kg]
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = k0 + wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + e;
+        const int gg = g0 + wn * (BN / 2) + j * 16 + (lane & 15);
+        if (k < a.K && gg < a.Kg) atomicAdd(a.dw + (size_t)k * a.Kg + gg, acc[i][j][e]);
+      }
+}
+
+static int ilog2w(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return l;
+}
+
+template <int BM, int BN>
+static void launch_w(WgradArgs a, hipStream_t st) {
+  const int tiles = ((a.K + BM - 1) / BM) * ((a.Kg + BN - 1) / BN);
+  const int chunks = (a.M + BR - 1) / BR;
+  int splits = (1024 + tiles - 1) / tiles;
+  const int max_splits = (chunks + 3) / 4;
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  a.chunks_per_split = (chunks + splits - 1) / splits;
+  splits = (chunks + a.chunks_per_split - 1) / a.chunks_per_split;
+  hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN>), dim3(tiles * splits), dim3(256), 0, st, a);
+}
+
+int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, int N, int H, int W, int C, int P,
+                      int Q, int K, int R, int S, int stride, int pad, hipStream_t st) {
+  if (C % 8 != 0 || (C & (C - 1)) != 0) return 1;
+  if (K % 64 != 0) return 2;
+  const long long M = (long long)N * P * Q;
+  if (M >= (1ll << 31)) return 4;
+  WgradArgs a;
+  a.dy = dy;
+  a.x = x;
+  a.dw = dw;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.C = C;
+  a.log2C = ilog2w(C);
+  a.P = P;
+  a.Q = Q;
+  a.K = K;
+  a.R = R;
+  a.S = S;
+  a.stride = stride;
+  a.pad = pad;
+  a.M = (int)M;
+  a.Kg = R * S * C;
+  a.chunks_per_split = 1;
+  if (K == 64)
+    launch_w<64, 128>(a, st);
+  else
+    launch_w<128, 128>(a, st);
+  return 0;
+}
+
+}  // namespace pmd

@@ -1,0 +1,46 @@
+// Host-side launch entry points of the gfx950 kernels (implemented in the .hip TUs).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pmd {
+typedef unsigned short bf16_t;
+
+int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* stats, int N, int H,
+                      int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
+                      bool dgrad, hipStream_t st);
+void conv_weight_prep_launch(const float* w, bf16_t* wk, bf16_t* wkt, int K, int RS, int C, int Cp,
+                             hipStream_t st);
+int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, int N, int H, int W, int C, int P,
+                      int Q, int K, int R, int S, int stride, int pad, hipStream_t st);
+
+int bn_finalize_launch(const float* sums, const float* count, const float* gamma, const float* beta,
+                       float* params, float* rm, float* rv, long long* nbt, int C, float eps,
+                       float momentum, bool eval_mode, hipStream_t st);
+int bn_apply_launch(const bf16_t* y1, const float* p1, const bf16_t* r, const float* p2, bf16_t* out,
+                    long long M, int C, int mode, bool relu, hipStream_t st);
+int bn_bwd_reduce_launch(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const float* params,
+                         float* red, int M, int C, bool relu, hipStream_t st);
+int bn_bwd_elemt_launch(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const float* params,
+                        const float* gamma, const float* red, const float* count, bf16_t* dy,
+                        bf16_t* dzm, long long M, int C, bool relu, bool eval_mode, hipStream_t st);
+
+int maxpool_fwd_launch(const bf16_t* x, bf16_t* out, uint8_t* arg, int N, int H, int W, int C, int P,
+                       int Q, hipStream_t st);
+int maxpool_bwd_launch(const bf16_t* dout, const uint8_t* arg, bf16_t* dx, int N, int H, int W, int C,
+                       int P, int Q, hipStream_t st);
+int avgpool_fwd_launch(const bf16_t* x, float* out, int N, int HW, int C, hipStream_t st);
+int avgpool_bwd_launch(const float* dout, bf16_t* dx, int N, int HW, int C, hipStream_t st);
+int xent_fwd_launch(const float* logits, const long long* target, float* loss, float* lse,
+                    long long* correct, int N, int V, hipStream_t st);
+int xent_bwd_launch(const float* logits, const long long* target, const float* lse, const float* gloss,
+                    float* grad, int N, int V, hipStream_t st);
+int sgd_launch(float* p, const float* g, float* buf, long long n, float lr, float momentum, float wd,
+               float damp, bool nesterov, bool first, hipStream_t st);
+
+int synth_images_launch(bf16_t* x, long long* labels, int N, int H, int W, int Cp, int Creal,
+                        int classes, unsigned long long seed, hipStream_t st);
+int cifar_augment_launch(const uint8_t* data, const long long* idx, void* out, bool out_bf16, int B,
+                         int Cp, bool train, int pad, unsigned long long seed, long long epoch,
+                         hipStream_t st);
+}  // namespace pmd

@@ -1,0 +1,62 @@
+"""Fused SGD (momentum / Nesterov / weight decay) over the flat arena.
+
+Math is exactly ``torch.optim.SGD`` (torch:optim/sgd.py:383-477) as used by
+the reference (lr 0.1, momentum 0.9, wd 1e-4, nesterov; main.py:51-55):
+
+    g   = g + wd * p
+    buf = g                      (first step)   | m * buf + (1 - dampening) * g
+    g   = g + m * buf            (nesterov)     | buf
+    p   = p - lr * g
+
+but the whole model is ONE kernel launch over the flat param/grad/momentum
+arenas (K16) instead of ~5 multi-tensor launches.  It subclasses
+``torch.optim.Optimizer`` so ``torch.optim.lr_scheduler.MultiStepLR`` (the
+reference scheduler, main.py:57-59) drives ``param_groups[0]['lr']``.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..ops.functional import prims_for
+from ..parallel.flat import flatten_module, get_flat
+
+
+class FusedSGD(torch.optim.Optimizer):
+    def __init__(self, module, lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True,
+                 dampening=0.0):
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        inner = getattr(module, "module", module)
+        self.flat = get_flat(inner) or flatten_module(inner)
+        defaults = dict(lr=lr, momentum=momentum, weight_decay=weight_decay, nesterov=nesterov,
+                        dampening=dampening)
+        super().__init__(self.flat.params, defaults)
+        self.momentum_arena = torch.zeros_like(self.flat.param_arena)
+        self.steps = 0
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        g = self.param_groups[0]
+        P = prims_for(self.flat.param_arena)
+        P.sgd_nesterov_(self.flat.param_arena, self.flat.grad_arena, self.momentum_arena,
+                        g["lr"], g["momentum"], g["weight_decay"], g["nesterov"],
+                        self.steps == 0, g["dampening"])
+        self.steps += 1
+        return loss
+
+    def zero_grad(self, set_to_none: bool = False):
+        # grads are views into the arena: always zero in place
+        self.flat.zero_grad()
+
+    # ------------------------------------------------------ resume state
+    def state_dict(self):
+        return {"steps": self.steps, "momentum": self.momentum_arena.detach().cpu(),
+                "param_groups": [{k: v for k, v in g.items() if k != "params"}
+                                 for g in self.param_groups]}
+
+    def load_state_dict(self, sd):
+        self.steps = int(sd["steps"])
+        self.momentum_arena.copy_(sd["momentum"].to(self.momentum_arena.device))
+        for g, s in zip(self.param_groups, sd["param_groups"]):
+            g.update(s)

@@ -1,0 +1,197 @@
+"""Training engine: per-rank orchestration, train and validate epochs.
+
+Mirrors the reference's L5 (main.py:32-171) with the same stdout formats and
+log files, minus its bugs: the LR schedule steps on every rank
+(B4), the sampler epoch advances (B5, ``--fixed_order`` keeps the reference
+behaviour), and test accuracy is all-reduced over ranks (B2,
+``--compat_metrics`` reproduces the reference number).  The hot loop keeps
+loss/accuracy on the device and only synchronises when it prints.
+"""
+from __future__ import annotations
+
+import os
+import time
+
+import torch
+import torch.distributed as dist
+
+from .. import launch
+from ..data.cifar import get_cifar10
+from ..data.loader import DeviceLoader, SyntheticImageNet
+from ..models import build_model
+from ..ops import functional as OF
+from ..parallel.comm import get_comm
+from ..parallel.dp import DataParallel
+from ..utils.checkpoint import load_resume, save_model, save_resume
+from ..utils.logger import DeviceMeter, Logger
+from .optim import FusedSGD
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def build_loaders(args, rank, world, dev, dtype, cpad):
+    if args.stem == "imagenet":
+        tr = SyntheticImageNet(int(args.batch_size / world), args.image_size, args.num_classes,
+                               steps=args.max_steps or args.steps_per_epoch, device=dev,
+                               dtype=dtype, cpad=cpad, seed=1234 + rank)
+        te = SyntheticImageNet(int(args.batch_size / world), args.image_size, args.num_classes,
+                               steps=args.eval_batches or 2, device=dev, dtype=dtype, cpad=cpad,
+                               seed=99991 + rank, dataset_len=50000)
+        return tr, te
+    xtr, ytr = get_cifar10(args.data_root, True, args.synthetic, args.train_samples)
+    xte, yte = get_cifar10(args.data_root, False, args.synthetic,
+                           None if args.train_samples is None else max(args.train_samples // 5, 1))
+    tr = DeviceLoader(xtr, ytr, args.batch_size, world, rank, train=True, device=dev, dtype=dtype,
+                      cpad=cpad, fixed_order=args.fixed_order, max_batches=args.max_steps)
+    te = DeviceLoader(xte, yte, args.batch_size, world, rank, train=False, device=dev, dtype=dtype,
+                      cpad=cpad, shuffle=False, max_batches=args.eval_batches)
+    if rank == 0:
+        print("-------------------Make loader-------------------")
+        print("Train Dataset :", tr.dataset_len, "   Test Dataset :", te.dataset_len)
+    return tr, te
+
+
+def train_epoch(loader, model, optimizer, epoch, logger, args, rank, dev, comm=None,
+                step_offset=0):
+    batch_time = DeviceMeter()
+    data_time = DeviceMeter()
+    losses = DeviceMeter()
+    top1 = DeviceMeter()
+    model.train()
+    n = len(loader)
+    end = time.time()
+    t_epoch = time.time()
+    images = 0
+    for i, (inp, target) in enumerate(loader):
+        data_time.update(time.time() - end)
+        launch.maybe_inject_fault(rank, step_offset + i)
+        output = model(inp)
+        loss = OF.cross_entropy(output, target)
+        optimizer.zero_grad()
+        loss.backward()
+        optimizer.step()
+        bsz = inp.size(0)
+        images += bsz
+        correct = OF.correct_count(output.detach(), target)
+        losses.update(loss.detach(), bsz)
+        top1.update(correct.float().squeeze(0) * (100.0 / bsz), bsz)
+        if i % args.print_freq == 0 or i == n - 1:
+            _sync(dev)
+        batch_time.update(time.time() - end)
+        end = time.time()
+        if rank == 0 and i % args.print_freq == 0:
+            print("Epoch: [{0}][{1}/{2}]\t"
+                  "Time {batch_time.val:.3f} ({batch_time.avg:.3f})\t"
+                  "Data {data_time.val:.3f} ({data_time.avg:.3f})\t"
+                  "Loss {loss.val:.4f} ({loss.avg:.4f})\t"
+                  "Prec {top1.val:.3f}% ({top1.avg:.3f}%)".format(
+                      epoch, i, n, batch_time=batch_time, data_time=data_time, loss=losses,
+                      top1=top1), flush=True)
+    _sync(dev)
+    elapsed = time.time() - t_epoch
+    world = comm.world_size if comm is not None else 1
+    ips = images * world / max(elapsed, 1e-9)
+    if rank == 0:
+        logger.write([epoch, losses.avg, top1.avg])
+        print(f"Epoch {epoch} throughput: {ips:.1f} images/sec (all ranks)", flush=True)
+    return losses.avg, top1.avg, ips
+
+
+@torch.no_grad()
+def validate(loader, model, epoch, logger, args, rank, dev, comm=None, mode="test"):
+    batch_time = DeviceMeter()
+    losses = DeviceMeter()
+    model.eval()
+    total_correct = torch.zeros(1, dtype=torch.float64, device=dev)
+    seen = torch.zeros(1, dtype=torch.float64, device=dev)
+    end = time.time()
+    n = len(loader)
+    for i, (inp, target) in enumerate(loader):
+        output = model(inp)
+        loss = OF.cross_entropy(output, target)
+        total_correct += OF.correct_count(output, target).double()
+        seen += target.numel()
+        losses.update(loss, inp.size(0))
+        batch_time.update(time.time() - end)
+        end = time.time()
+        if rank == 0 and i % args.print_freq == 0:
+            print(mode, ": [{0}/{1}]\t"
+                  "Time {batch_time.val:.3f} ({batch_time.avg:.3f})\t"
+                  "Loss {loss.val:.4f} ({loss.avg:.4f})".format(
+                      i, n, batch_time=batch_time, loss=losses), flush=True)
+    if args.compat_metrics or comm is None:
+        # reference semantics (main.py:168): local correct / full dataset size
+        denom = float(loader.dataset_len) if args.compat_metrics else float(seen.item())
+        acc = 100.0 * total_correct.item() / max(denom, 1.0)
+    else:
+        buf = torch.cat([total_correct, seen])
+        if dist.get_backend() == "gloo":
+            buf = buf.cpu()
+        comm.all_reduce_(buf)
+        acc = 100.0 * float(buf[0]) / max(float(buf[1]), 1.0)
+    if rank == 0:
+        print("Accuracy {:.2f}".format(acc), flush=True)
+        logger.write([epoch, losses.avg, float(acc)])
+    return losses.avg, acc
+
+
+def run_rank(rank, world_size, args):
+    """Per-rank orchestrator (reference ``main(rank, world_size)``, main.py:32-84)."""
+    dev = launch.init_process(rank, world_size, args.backend, args.device, args.master_addr,
+                              args.master_port, args.timeout_min)
+    try:
+        _run(rank, world_size, args, dev)
+    finally:
+        launch.shutdown()
+
+
+def _run(rank, world_size, args, dev):
+    on_gpu = dev.type == "cuda"
+    dtype = torch.bfloat16 if (args.dtype == "bf16" or (args.dtype == "auto" and on_gpu)) \
+        else torch.float32
+    if on_gpu and dtype != torch.bfloat16:
+        raise ValueError("the gfx950 kernels compute in bf16; use --dtype bf16 on GPU")
+    cpad = 8 if on_gpu else 3
+    train_loader, test_loader = build_loaders(args, rank, world_size, dev, dtype, cpad)
+    if args.seed is not None:
+        torch.manual_seed(args.seed)
+    model = build_model(args.model, num_classes=args.num_classes, stem=args.stem).to(dev)
+    comm = get_comm()
+    OF.set_bn_sync(comm if (comm is not None and args.sync_bn == "on") else None)
+    model = DataParallel(model, comm, bucket_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb,
+                         broadcast_buffers=args.broadcast_buffers)
+    optimizer = FusedSGD(model, lr=args.lr, momentum=args.momentum, weight_decay=args.wd,
+                         nesterov=True)
+    scheduler = torch.optim.lr_scheduler.MultiStepLR(optimizer, milestones=args.milestone_list,
+                                                     gamma=args.gamma)
+    train_logger = Logger(os.path.join(args.save_path, "train.log"))
+    test_logger = Logger(os.path.join(args.save_path, "test.log"))
+    start_epoch = 1
+    if args.resume:
+        last, _ = load_resume(args.resume, model, optimizer, scheduler)
+        start_epoch = last + 1
+    step = 0
+    import warnings
+    for epoch in range(start_epoch, args.epochs + 1):
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")   # "scheduler.step() before optimizer.step()"
+            scheduler.step()                  # every rank, at epoch start (B4 fixed)
+        train_loader.set_epoch(epoch)
+        train_epoch(train_loader, model, optimizer, epoch, train_logger, args, rank, dev, comm,
+                    step_offset=step)
+        step += len(train_loader)
+        validate(test_loader, model, epoch, test_logger, args, rank, dev, comm, "test")
+        if rank == 0:
+            if epoch == int(args.epochs):
+                save_model(model, args.save_path, epoch)
+            if args.resume_every and epoch % args.resume_every == 0:
+                save_resume(os.path.join(args.save_path, "resume.pth"), model, optimizer, scheduler,
+                            epoch)
+    if comm is not None:
+        comm.barrier()
+    if rank == 0 and not args.no_plot:
+        from ..utils.plot import draw_plot
+        draw_plot(args.save_path)

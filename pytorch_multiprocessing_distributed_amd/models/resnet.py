@@ -1,0 +1,238 @@
+"""ResNet family with the reference's module / state_dict naming.
+
+Parity notes (reference = /root/reference):
+  * block layout and key names follow model/resnet.py:15-105 (``conv1, bn1,
+    layerX.Y.{conv1,bn1,conv2,bn2[,conv3,bn3]}, layerX.Y.shortcut.{0,1}, linear``)
+  * ``ResNet18()`` keeps the reference's ``[1,1,1,1]`` block counts
+    (model/resnet.py:108-109); ``ResNet18Full()`` is the real
+    ``[2,2,2,2]`` network.
+  * ``stem='cifar'`` is the reference stem (3x3/s1 conv, no max-pool,
+    4x4 average pool, resnet.py:79-81,102); ``stem='imagenet'`` adds the
+    7x7/s2 conv + 3x3/s2 max-pool + global average pool needed for 224x224
+    inputs.  Key names are identical in both stems.
+
+Two implementations share the module tree:
+  * ``impl='fused'`` (default): activations are NHWC; every block calls the
+    fused ops in :mod:`..ops.functional` (conv + BN-statistics epilogue,
+    BN-apply + residual + ReLU, SyncBN statistics through the comm layer).
+    On an MI355X these are the hand-written gfx950 kernels; on CPU the same
+    autograd graph runs on the PyTorch reference primitives.
+  * ``impl='stock'``: plain ``nn.Conv2d`` / ``nn.BatchNorm2d`` NCHW modules;
+    used only as the comparator (stock PyTorch path of the reference) and as
+    a numerical oracle in tests.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import functional as OF
+
+
+class Conv2d(nn.Module):
+    """Bias-free convolution whose weight is stored channels-last (K,R,S,C
+    physical order) so the gfx950 implicit-GEMM kernels read it directly.
+
+    The logical shape stays ``[K, C, R, S]`` so checkpoints are identical to
+    ``nn.Conv2d`` (reference resnet.py:20-33)."""
+
+    def __init__(self, in_planes, planes, kernel_size, stride=1, padding=0):
+        super().__init__()
+        self.in_channels = in_planes
+        self.out_channels = planes
+        self.kernel_size = kernel_size
+        self.stride = stride
+        self.padding = padding
+        w = torch.empty(planes, in_planes, kernel_size, kernel_size)
+        # nn.Conv2d default init: kaiming_uniform_(a=sqrt(5))
+        nn.init.kaiming_uniform_(w, a=math.sqrt(5))
+        self.weight = nn.Parameter(w.contiguous(memory_format=torch.channels_last))
+
+    def extra_repr(self):
+        return (f"{self.in_channels}, {self.out_channels}, kernel_size={self.kernel_size}, "
+                f"stride={self.stride}, padding={self.padding}, bias=False")
+
+
+class BatchNorm(nn.Module):
+    """Synchronised BatchNorm parameters/buffers (keys identical to
+    ``nn.BatchNorm2d``; ``_version = 2`` like torch's BN so the saved
+    ``_metadata`` matches)."""
+
+    _version = 2
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1):
+        super().__init__()
+        self.num_features = num_features
+        self.eps = eps
+        self.momentum = momentum
+        self.weight = nn.Parameter(torch.ones(num_features))
+        self.bias = nn.Parameter(torch.zeros(num_features))
+        self.register_buffer("running_mean", torch.zeros(num_features))
+        self.register_buffer("running_var", torch.ones(num_features))
+        self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
+
+    def extra_repr(self):
+        return f"{self.num_features}, eps={self.eps}, momentum={self.momentum}"
+
+
+def _conv(impl, cin, cout, k, stride, padding):
+    if impl == "stock":
+        return nn.Conv2d(cin, cout, kernel_size=k, stride=stride, padding=padding, bias=False)
+    return Conv2d(cin, cout, k, stride=stride, padding=padding)
+
+
+def _bn(impl, c):
+    if impl == "stock":
+        return nn.BatchNorm2d(c)
+    return BatchNorm(c)
+
+
+class BasicBlock(nn.Module):
+    """conv3x3-BN-ReLU-conv3x3-BN + shortcut, ReLU (reference resnet.py:15-40)."""
+
+    expansion = 1
+
+    def __init__(self, in_planes, planes, stride=1, impl="fused"):
+        super().__init__()
+        self.impl = impl
+        self.conv1 = _conv(impl, in_planes, planes, 3, stride, 1)
+        self.bn1 = _bn(impl, planes)
+        self.conv2 = _conv(impl, planes, planes, 3, 1, 1)
+        self.bn2 = _bn(impl, planes)
+        self.shortcut = nn.Sequential()
+        if stride != 1 or in_planes != self.expansion * planes:
+            self.shortcut = nn.Sequential(
+                _conv(impl, in_planes, self.expansion * planes, 1, stride, 0),
+                _bn(impl, self.expansion * planes),
+            )
+
+    def forward(self, x):
+        if self.impl == "stock":
+            out = F.relu(self.bn1(self.conv1(x)))
+            out = self.bn2(self.conv2(out))
+            out = out + self.shortcut(x)
+            return F.relu(out)
+        o = OF.conv_bn_act(x, self.conv1, self.bn1, relu=True)
+        y2, s2 = OF.conv(o, self.conv2)
+        if len(self.shortcut) == 0:
+            return OF.bn_add_act(y2, s2, self.bn2, residual=x, relu=True)
+        ysc, ssc = OF.conv(x, self.shortcut[0])
+        return OF.bn_add_act(y2, s2, self.bn2, res_y=ysc, res_stats=ssc,
+                             res_bn=self.shortcut[1], relu=True)
+
+
+class Bottleneck(nn.Module):
+    """1x1-3x3(stride)-1x1 bottleneck, stride on the 3x3 ("v1.5"),
+    reference resnet.py:43-71."""
+
+    expansion = 4
+
+    def __init__(self, in_planes, planes, stride=1, impl="fused"):
+        super().__init__()
+        self.impl = impl
+        self.conv1 = _conv(impl, in_planes, planes, 1, 1, 0)
+        self.bn1 = _bn(impl, planes)
+        self.conv2 = _conv(impl, planes, planes, 3, stride, 1)
+        self.bn2 = _bn(impl, planes)
+        self.conv3 = _conv(impl, planes, self.expansion * planes, 1, 1, 0)
+        self.bn3 = _bn(impl, self.expansion * planes)
+        self.shortcut = nn.Sequential()
+        if stride != 1 or in_planes != self.expansion * planes:
+            self.shortcut = nn.Sequential(
+                _conv(impl, in_planes, self.expansion * planes, 1, stride, 0),
+                _bn(impl, self.expansion * planes),
+            )
+
+    def forward(self, x):
+        if self.impl == "stock":
+            out = F.relu(self.bn1(self.conv1(x)))
+            out = F.relu(self.bn2(self.conv2(out)))
+            out = self.bn3(self.conv3(out))
+            out = out + self.shortcut(x)
+            return F.relu(out)
+        o = OF.conv_bn_act(x, self.conv1, self.bn1, relu=True)
+        o = OF.conv_bn_act(o, self.conv2, self.bn2, relu=True)
+        y3, s3 = OF.conv(o, self.conv3)
+        if len(self.shortcut) == 0:
+            return OF.bn_add_act(y3, s3, self.bn3, residual=x, relu=True)
+        ysc, ssc = OF.conv(x, self.shortcut[0])
+        return OF.bn_add_act(y3, s3, self.bn3, res_y=ysc, res_stats=ssc,
+                             res_bn=self.shortcut[1], relu=True)
+
+
+class ResNet(nn.Module):
+    """ResNet trunk (reference resnet.py:74-105) with a selectable stem.
+
+    Fused-impl input: NHWC ``[N, H, W, C]`` (C may be zero-padded to a
+    multiple of 8 for the MFMA stem); stock-impl input: NCHW."""
+
+    def __init__(self, block, num_blocks, num_classes=10, stem="cifar", impl="fused"):
+        super().__init__()
+        if stem not in ("cifar", "imagenet"):
+            raise ValueError(f"unknown stem {stem!r}")
+        self.impl = impl
+        self.stem = stem
+        self.in_planes = 64
+        if stem == "cifar":
+            self.conv1 = _conv(impl, 3, 64, 3, 1, 1)
+        else:
+            self.conv1 = _conv(impl, 3, 64, 7, 2, 3)
+        self.bn1 = _bn(impl, 64)
+        self.layer1 = self._make_layer(block, 64, num_blocks[0], stride=1)
+        self.layer2 = self._make_layer(block, 128, num_blocks[1], stride=2)
+        self.layer3 = self._make_layer(block, 256, num_blocks[2], stride=2)
+        self.layer4 = self._make_layer(block, 512, num_blocks[3], stride=2)
+        self.linear = nn.Linear(512 * block.expansion, num_classes)
+
+    def _make_layer(self, block, planes, num_blocks, stride):
+        strides = [stride] + [1] * (num_blocks - 1)
+        layers = []
+        for s in strides:
+            layers.append(block(self.in_planes, planes, s, impl=self.impl))
+            self.in_planes = planes * block.expansion
+        return nn.Sequential(*layers)
+
+    def forward(self, x):
+        if self.impl == "stock":
+            out = F.relu(self.bn1(self.conv1(x)))
+            if self.stem == "imagenet":
+                out = F.max_pool2d(out, 3, 2, 1)
+            out = self.layer4(self.layer3(self.layer2(self.layer1(out))))
+            out = F.adaptive_avg_pool2d(out, 1).flatten(1)
+            return self.linear(out)
+        out = OF.conv_bn_act(x, self.conv1, self.bn1, relu=True)
+        if self.stem == "imagenet":
+            out = OF.max_pool3x3s2(out)
+        out = self.layer4(self.layer3(self.layer2(self.layer1(out))))
+        out = OF.global_avg_pool(out)            # [N, C] fp32
+        return OF.linear(out, self.linear)
+
+
+def _factory(block, nb):
+    def make(num_classes=10, stem="cifar", impl="fused"):
+        return ResNet(block, nb, num_classes=num_classes, stem=stem, impl=impl)
+    return make
+
+
+ResNet18 = _factory(BasicBlock, [1, 1, 1, 1])        # reference quirk B1 (really ResNet-10)
+ResNet18Full = _factory(BasicBlock, [2, 2, 2, 2])
+ResNet34 = _factory(BasicBlock, [3, 4, 6, 3])
+ResNet50 = _factory(Bottleneck, [3, 4, 6, 3])
+ResNet101 = _factory(Bottleneck, [3, 4, 23, 3])
+ResNet152 = _factory(Bottleneck, [3, 8, 36, 3])
+
+MODELS = {
+    "res": ResNet18, "resnet18": ResNet18, "resnet18full": ResNet18Full,
+    "resnet34": ResNet34, "resnet50": ResNet50, "resnet101": ResNet101,
+    "resnet152": ResNet152,
+}
+
+
+def build_model(name, num_classes=10, stem="cifar", impl="fused"):
+    key = name.lower()
+    if key not in MODELS:
+        raise ValueError(f"unknown model {name!r}; choose from {sorted(MODELS)}")
+    return MODELS[key](num_classes=num_classes, stem=stem, impl=impl)

@@ -1,0 +1,104 @@
+"""gfx950 primitives: thin Python shims over the in-tree ``_C`` extension.
+
+Same contracts as :mod:`.torch_prims` (NHWC bf16 activations, fp32
+statistics, BN params packed [4, C]).  There is deliberately no fallback:
+importing this module on a GPU box without the built extension raises.
+"""
+from __future__ import annotations
+
+import torch
+
+from .native import C as _C
+
+
+# --------------------------------------------------------------------- conv
+def conv_weight(w, dtype, cin, want_t=True):
+    if dtype != torch.bfloat16:
+        raise TypeError(f"gfx950 conv path computes in bf16, got activations of {dtype}")
+    return tuple(_C.conv_weight_prep(w.detach(), int(cin), bool(want_t)))
+
+
+def conv_fwd(x, wpack, stride, pad, want_stats):
+    r = _C.conv_fwd(x, wpack[0], int(stride), int(pad), bool(want_stats))
+    return (r[0], r[1]) if want_stats else (r[0], None)
+
+
+def conv_dgrad(dy, wpack, x_shape, stride, pad):
+    if len(wpack) < 2:
+        raise RuntimeError("dgrad image was not prepared (input did not require grad)")
+    return _C.conv_dgrad(dy, wpack[1], int(x_shape[1]), int(x_shape[2]), int(stride), int(pad))
+
+
+def conv_wgrad(dy, x, wk_shape, stride, pad):
+    return _C.conv_wgrad(dy, x, int(wk_shape[1]), int(wk_shape[2]), int(stride), int(pad))
+
+
+# ----------------------------------------------------------------------- BN
+def bn_finalize(sums, count, gamma, beta, eps, running_mean=None, running_var=None,
+                momentum=0.1, num_batches_tracked=None):
+    return _C.bn_finalize(sums, count, gamma.detach(), beta.detach(), float(eps), running_mean,
+                          running_var, float(momentum), num_batches_tracked, False)
+
+
+def bn_eval_params(running_mean, running_var, gamma, beta, eps):
+    return _C.bn_finalize(None, None, gamma.detach(), beta.detach(), float(eps), running_mean,
+                          running_var, 0.0, None, True)
+
+
+def bn_apply(y1, p1, res=None, y2=None, p2=None, relu=True):
+    return _C.bn_apply(y1, p1, res, y2, p2, bool(relu))
+
+
+def bn_bwd_reduce(dout, out, y, p, relu):
+    return _C.bn_bwd_reduce(dout, out, y, p, bool(relu))
+
+
+def bn_bwd_elemt(dout, out, y, p, gamma, red, count, relu, want_dzm=False):
+    r = _C.bn_bwd_elemt(dout, out, y, p, gamma.detach(), red, count, bool(relu), bool(want_dzm),
+                        False)
+    return (r[0], r[1]) if want_dzm else (r[0], None)
+
+
+def bn_bwd_elemt_eval(dout, out, p, relu, want_dzm=False):
+    r = _C.bn_bwd_elemt(dout, out, out, p, p[2], None, None, bool(relu), bool(want_dzm), True)
+    return (r[0], r[1]) if want_dzm else (r[0], None)
+
+
+# -------------------------------------------------------------------- pools
+def maxpool_fwd(x):
+    out, arg = _C.maxpool_fwd(x)
+    return out, arg
+
+
+def maxpool_bwd(dout, arg, x_shape):
+    return _C.maxpool_bwd(dout, arg, int(x_shape[1]), int(x_shape[2]))
+
+
+def avgpool_fwd(x):
+    return _C.avgpool_fwd(x)
+
+
+def avgpool_bwd(dout, x_shape, dtype):
+    return _C.avgpool_bwd(dout.float().contiguous(), int(x_shape[1]), int(x_shape[2]))
+
+
+# --------------------------------------------------------------- loss/acc
+def xent_fwd(logits, target):
+    loss, lse, _ = _C.xent_fwd(logits.float().contiguous(), target)
+    return loss, lse
+
+
+def xent_bwd(gloss, logits, target, lse):
+    g = _C.xent_bwd(logits.float().contiguous(), target, lse, gloss)
+    return g.to(logits.dtype)
+
+
+def correct_count(logits, target):
+    return _C.xent_fwd(logits.float().contiguous(), target)[2]
+
+
+# -------------------------------------------------------------------- optim
+def sgd_nesterov_(params, grads, bufs, lr, momentum, weight_decay, nesterov, first_step,
+                  dampening=0.0):
+    _C.sgd_(params, grads, bufs, float(lr), float(momentum), float(weight_decay),
+            float(dampening), bool(nesterov), bool(first_step))

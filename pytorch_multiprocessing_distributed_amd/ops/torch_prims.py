@@ -1,0 +1,191 @@
+"""PyTorch reference implementations of every primitive the fused ops use.
+
+Each function here has the exact contract of the matching gfx950 kernel in
+``csrc/kernels`` (NHWC activations, channel = last dim, fp32 statistics).
+They serve two roles:
+  * the CPU backend (BASELINE config 1: ResNet-18 CIFAR on gloo), and
+  * the fp32 oracle the GPU numerics tests compare each HIP kernel against.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+
+def _nchw(x):
+    return x.permute(0, 3, 1, 2)
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+# --------------------------------------------------------------------- conv
+def conv_weight(w, dtype, cin, want_t=True):
+    """[K,C,R,S] param -> (wk,) with wk the [K,R,S,cin] compute copy
+    (zero-padded channels).  The HIP backend also returns the dgrad image."""
+    wk = w.detach().permute(0, 2, 3, 1).to(dtype)
+    if cin != wk.shape[-1]:
+        wk = F.pad(wk, (0, cin - wk.shape[-1]))
+    return (wk.contiguous(),)
+
+
+def conv_fwd(x, wpack, stride, pad, want_stats):
+    wk = wpack[0]
+    y = F.conv2d(_nchw(x).float(), wk.permute(0, 3, 1, 2).float(), stride=stride, padding=pad)
+    y = _nhwc(y).to(x.dtype)
+    stats = None
+    if want_stats:
+        yf = y.float().reshape(-1, y.shape[-1])
+        stats = torch.stack([yf.sum(0), (yf * yf).sum(0)])
+    return y, stats
+
+
+def conv_dgrad(dy, wpack, x_shape, stride, pad):
+    wk = wpack[0]
+    n, h, w, c = x_shape
+    dx = torch.nn.grad.conv2d_input((n, c, h, w), wk.permute(0, 3, 1, 2).float(),
+                                    _nchw(dy).float(), stride=stride, padding=pad)
+    return _nhwc(dx).to(dy.dtype)
+
+
+def conv_wgrad(dy, x, wk_shape, stride, pad):
+    k, r, s, c = wk_shape
+    dw = torch.nn.grad.conv2d_weight(_nchw(x).float(), (k, c, r, s), _nchw(dy).float(),
+                                     stride=stride, padding=pad)
+    return dw.permute(0, 2, 3, 1).contiguous()          # fp32 [K,R,S,C]
+
+
+# ----------------------------------------------------------------------- BN
+# BN "params" are one fp32 [4, C] tensor: rows mean, invstd, scale=gamma*invstd,
+# shift=beta-mean*scale (the same packing the HIP kernels use).
+def bn_finalize(sums, count, gamma, beta, eps, running_mean=None, running_var=None,
+                momentum=0.1, num_batches_tracked=None):
+    """Global (sum, sum^2, count) -> params; updates running stats with the
+    unbiased variance (torch batch_norm_gather_stats_with_counts semantics).
+    ``count`` is a 1-element fp32 tensor so no host sync is needed."""
+    cnt = count.float()
+    mean = sums[0] / cnt
+    var = (sums[1] / cnt - mean * mean).clamp_min(0.0)
+    invstd = torch.rsqrt(var + eps)
+    scale = gamma.detach().float() * invstd
+    shift = beta.detach().float() - mean * scale
+    if running_mean is not None:
+        unbiased = var * (cnt / (cnt - 1.0).clamp_min(1.0))
+        running_mean.mul_(1.0 - momentum).add_(mean.to(running_mean.dtype), alpha=momentum)
+        running_var.mul_(1.0 - momentum).add_(unbiased.to(running_var.dtype), alpha=momentum)
+    if num_batches_tracked is not None:
+        num_batches_tracked.add_(1)
+    return torch.stack([mean, invstd, scale, shift])
+
+
+def bn_eval_params(running_mean, running_var, gamma, beta, eps):
+    mean = running_mean.float()
+    invstd = torch.rsqrt(running_var.float() + eps)
+    scale = gamma.detach().float() * invstd
+    shift = beta.detach().float() - mean * scale
+    return torch.stack([mean, invstd, scale, shift])
+
+
+def bn_apply(y1, p1, res=None, y2=None, p2=None, relu=True):
+    o = y1.float() * p1[2] + p1[3]
+    if y2 is not None:
+        o = o + y2.float() * p2[2] + p2[3]
+    elif res is not None:
+        o = o + res.float()
+    if relu:
+        o = o.clamp_min(0.0)
+    return o.to(y1.dtype)
+
+
+def _dzm(dout, out, relu):
+    d = dout.float()
+    if relu:
+        d = d * (out > 0)
+    return d
+
+
+def bn_bwd_reduce(dout, out, y, p, relu):
+    """-> fp32 [2, C]: (sum dzm, sum dzm*xhat), dzm = dout * relu_mask."""
+    c = y.shape[-1]
+    d = _dzm(dout, out, relu).reshape(-1, c)
+    xhat = (y.float().reshape(-1, c) - p[0]) * p[1]
+    return torch.stack([d.sum(0), (d * xhat).sum(0)])
+
+
+def bn_bwd_elemt(dout, out, y, p, gamma, red, count, relu, want_dzm=False):
+    d = _dzm(dout, out, relu)
+    xhat = (y.float() - p[0]) * p[1]
+    cnt = count.float()
+    mdy = red[0] / cnt
+    mdyx = red[1] / cnt
+    dy = ((d - mdy - xhat * mdyx) * (gamma.detach().float() * p[1])).to(y.dtype)
+    return dy, (d.to(y.dtype) if want_dzm else None)
+
+
+def bn_bwd_elemt_eval(dout, out, p, relu, want_dzm=False):
+    d = _dzm(dout, out, relu)
+    dy = (d * p[2]).to(dout.dtype)
+    return dy, (d.to(dout.dtype) if want_dzm else None)
+
+
+# -------------------------------------------------------------------- pools
+def maxpool_fwd(x):
+    """3x3/s2/p1 max-pool; the auxiliary output is the input itself (the
+    backward re-derives the routing so overlapping windows that pick the
+    same element accumulate, which max_unpool2d would not)."""
+    out = F.max_pool2d(_nchw(x).float(), 3, 2, 1)
+    return _nhwc(out).to(x.dtype), x
+
+
+def maxpool_bwd(dout, x, x_shape):
+    with torch.enable_grad():
+        xf = _nchw(x).float().detach().requires_grad_(True)
+        out = F.max_pool2d(xf, 3, 2, 1)
+        (dx,) = torch.autograd.grad(out, xf, _nchw(dout).float())
+    return _nhwc(dx).to(dout.dtype)
+
+
+def avgpool_fwd(x):
+    return x.float().mean(dim=(1, 2))
+
+
+def avgpool_bwd(dout, x_shape, dtype):
+    n, h, w, c = x_shape
+    return (dout.float() / (h * w)).reshape(n, 1, 1, c).expand(n, h, w, c).to(dtype).contiguous()
+
+
+# --------------------------------------------------------------- loss/acc
+def xent_fwd(logits, target):
+    """Mean softmax cross-entropy; returns (loss[1] fp32, lse[N] fp32)."""
+    lf = logits.float()
+    lse = torch.logsumexp(lf, dim=1)
+    loss = (lse - lf.gather(1, target.view(-1, 1)).squeeze(1)).mean()
+    return loss.reshape(1), lse
+
+
+def xent_bwd(gloss, logits, target, lse):
+    lf = logits.float()
+    p = torch.exp(lf - lse[:, None])
+    p[torch.arange(lf.shape[0], device=lf.device), target] -= 1.0
+    return (p * (gloss.float() / lf.shape[0])).to(logits.dtype)
+
+
+def correct_count(logits, target):
+    return (logits.argmax(1) == target).sum().to(torch.int64).reshape(1)
+
+
+# -------------------------------------------------------------------- optim
+def sgd_nesterov_(params, grads, bufs, lr, momentum, weight_decay, nesterov, first_step,
+                  dampening=0.0):
+    """In-place SGD over flat fp32 arenas (torch.optim.SGD semantics)."""
+    g = grads
+    if weight_decay != 0:
+        g = g.add(params, alpha=weight_decay)
+    if momentum != 0:
+        if first_step:
+            bufs.copy_(g)
+        else:
+            bufs.mul_(momentum).add_(g, alpha=1.0 - dampening)
+        g = g.add(bufs, alpha=momentum) if nesterov else bufs
+    params.add_(g, alpha=-lr)

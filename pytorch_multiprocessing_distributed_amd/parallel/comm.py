@@ -1,0 +1,85 @@
+"""Communicator used by the reducer, SyncBN and metric reduction.
+
+On an MI355X node the process group backend is ``"nccl"``, which on
+PyTorch-ROCm *is* RCCL: collectives run over xGMI on RCCL's own HIP stream
+and are ordered against the caller's current stream with HIP events (no host
+blocking).  On CPU the same interface runs on gloo (BASELINE config 1).
+
+Reference touchpoints: C1 init_process_group (main.py:190-193),
+C3 initial broadcast, C5/C6 SyncBN statistics, C7 bucketed gradient
+all-reduce, C8 metric reduction (main.py:173-177, dead in the reference),
+C9 teardown (main.py:84).
+"""
+from __future__ import annotations
+
+import hashlib
+
+import torch
+import torch.distributed as dist
+
+
+class Comm:
+    def __init__(self, group=None):
+        if not dist.is_available() or not dist.is_initialized():
+            raise RuntimeError("torch.distributed is not initialised")
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world_size = dist.get_world_size(group)
+        self.backend = dist.get_backend(group)
+        # RCCL implements ncclAvg; gloo does not -> pre-scale there
+        self.supports_avg = self.backend == "nccl"
+
+    # ------------------------------------------------------------ blocking
+    def all_reduce_(self, t, op=dist.ReduceOp.SUM):
+        dist.all_reduce(t, op=op, group=self.group)
+        return t
+
+    def broadcast_(self, t, src=0):
+        dist.broadcast(t, src=src, group=self.group)
+        return t
+
+    def all_gather(self, t):
+        out = [torch.empty_like(t) for _ in range(self.world_size)]
+        dist.all_gather(out, t, group=self.group)
+        return out
+
+    def barrier(self):
+        if self.backend == "nccl" and torch.cuda.is_available():
+            dist.barrier(group=self.group, device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier(group=self.group)
+
+    # --------------------------------------------------------------- async
+    def all_reduce_mean_async(self, t):
+        """Average ``t`` in place across ranks; returns a Work handle."""
+        if self.supports_avg:
+            return dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
+        t.mul_(1.0 / self.world_size)
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
+    # --------------------------------------------------------------- utils
+    def reduce_mean(self, t):
+        """Reference ``reduce_tensor`` (main.py:173-177): clone, SUM, /W."""
+        rt = t.clone()
+        self.all_reduce_(rt)
+        rt /= self.world_size
+        return rt
+
+    def check_same(self, text: str, what="value"):
+        """Verify a host string is identical on all ranks (param-shape check,
+        collective-order check).  Raises on mismatch."""
+        h = int(hashlib.sha1(text.encode()).hexdigest()[:15], 16)
+        dev = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else "cpu"
+        t = torch.tensor([h, -h], dtype=torch.int64, device=dev)
+        mx = t.clone()
+        self.all_reduce_(mx, op=dist.ReduceOp.MAX)
+        if int(mx[0]) != h or int(mx[1]) != -h:
+            raise RuntimeError(f"{what} differs across ranks (rank {self.rank})")
+
+
+def get_comm(group=None):
+    if not dist.is_available() or not dist.is_initialized():
+        return None
+    if dist.get_world_size(group) == 1:
+        return None
+    return Comm(group)

@@ -1,0 +1,177 @@
+"""Synchronous data parallelism: the framework's replacement for
+``torch.nn.parallel.DistributedDataParallel`` (reference main.py:44).
+
+What it does:
+  * construction: verifies parameter names/shapes agree on every rank (C2),
+    re-homes parameters/grads into flat arenas (:mod:`.flat`), then
+    broadcasts the parameter arena and all buffers from rank 0 in one
+    collective per dtype (C3) -- replicas start identical (README.md:6);
+  * backward: gradients accumulate straight into the grad arena; a
+    post-accumulate hook counts readiness per bucket and, when a bucket is
+    complete, launches an asynchronous in-place *average* all-reduce on it
+    (RCCL ``ncclAvg`` over xGMI; pre-scale + SUM on gloo), overlapping the
+    rest of backward.  Buckets are contiguous arena slices in reverse
+    registration order with a small first bucket (DDP: 1 MiB first / 25 MiB
+    rest; defaults here are sized for xGMI rings, see ``bucket_mb``);
+  * end of backward (autograd engine callback): waits on every bucket's Work
+    (a stream-side wait, no host block) and checks each bucket fired exactly
+    once (race / double-launch detector);
+  * ``no_sync()`` skips communication for gradient accumulation;
+  * ``broadcast_buffers=True`` re-broadcasts BN buffers from rank 0 before
+    each training forward (reference DDP default, C4); off by default since
+    SyncBN keeps them identical.
+
+``state_dict()`` carries the ``module.`` prefix exactly like the reference's
+DDP checkpoint (main.py:77).
+"""
+from __future__ import annotations
+
+import contextlib
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from .comm import Comm
+from .flat import flatten_module
+
+
+class _Bucket:
+    __slots__ = ("index", "start", "end", "params", "pending", "work", "fired")
+
+    def __init__(self, index, start, end, params):
+        self.index = index
+        self.start = start
+        self.end = end
+        self.params = params
+        self.pending = len(params)
+        self.work = None
+        self.fired = 0
+
+
+class DataParallel(nn.Module):
+    def __init__(self, module: nn.Module, comm: Comm | None = None, bucket_mb: float = 25.0,
+                 first_bucket_mb: float = 1.0, broadcast_buffers: bool = False,
+                 check_collectives: bool = True):
+        super().__init__()
+        self.module = module
+        self.comm = comm
+        self.world_size = comm.world_size if comm is not None else 1
+        self.broadcast_buffers = broadcast_buffers
+        self.check_collectives = check_collectives
+        if comm is not None:
+            desc = ";".join(f"{n}:{tuple(p.shape)}" for n, p in module.named_parameters())
+            comm.check_same(desc, "parameter names/shapes")
+        self.flat = flatten_module(module)
+        self._build_buckets(bucket_mb, first_bucket_mb)
+        if comm is not None:
+            self._sync_module_states()
+        self._sync_enabled = True
+        self._callback_queued = False
+        self._hooks = []
+        if comm is not None:
+            for i, p in enumerate(self.flat.params):
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+        self.iteration = 0
+
+    # ------------------------------------------------------------ buckets
+    def _build_buckets(self, bucket_mb, first_mb):
+        fp = self.flat
+        groups, cur, nbytes = [], [], 0
+        cap = int(first_mb * 2 ** 20)
+        for i, p in enumerate(fp.params):
+            cur.append(i)
+            nbytes += p.numel() * p.element_size()
+            if nbytes >= cap:
+                groups.append(cur)
+                cur, nbytes = [], 0
+                cap = int(bucket_mb * 2 ** 20)
+        if cur:
+            groups.append(cur)
+        # bucket = contiguous arena slice from its first param to the next bucket's start
+        starts = [fp.offsets[g[0]] for g in groups] + [fp.numel]
+        self.buckets = [_Bucket(j, starts[j], starts[j + 1], g) for j, g in enumerate(groups)]
+        self._param_bucket = [None] * len(fp.params)
+        for b in self.buckets:
+            for i in b.params:
+                self._param_bucket[i] = b
+
+    def bucket_sizes_mb(self):
+        return [(b.end - b.start) * 4 / 2 ** 20 for b in self.buckets]
+
+    # --------------------------------------------------------- state sync
+    @torch.no_grad()
+    def _sync_module_states(self):
+        self.comm.broadcast_(self.flat.param_arena, 0)
+        self._broadcast_buffers()
+
+    @torch.no_grad()
+    def _broadcast_buffers(self):
+        by_dtype = {}
+        for b in self.module.buffers():
+            by_dtype.setdefault(b.dtype, []).append(b)
+        for bufs in by_dtype.values():
+            flat = torch.cat([b.reshape(-1) for b in bufs])
+            self.comm.broadcast_(flat, 0)
+            off = 0
+            for b in bufs:
+                n = b.numel()
+                b.copy_(flat[off: off + n].view_as(b))
+                off += n
+
+    # --------------------------------------------------------------- hooks
+    def _make_hook(self, i):
+        def hook(_p):
+            if not self._sync_enabled:
+                return
+            if not self._callback_queued:
+                self._callback_queued = True
+                torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+            b = self._param_bucket[i]
+            b.pending -= 1
+            if b.pending == 0:
+                self._launch(b)
+        return hook
+
+    def _launch(self, b):
+        if b.work is not None:
+            raise RuntimeError(f"bucket {b.index} launched twice in one iteration")
+        b.fired += 1
+        b.work = self.comm.all_reduce_mean_async(self.flat.grad_arena[b.start: b.end])
+
+    def _finalize(self):
+        # params that received no gradient this iteration (unused): launch their bucket anyway
+        for b in self.buckets:
+            if b.work is None:
+                self._launch(b)
+        for b in self.buckets:
+            b.work.wait()
+        if self.check_collectives:
+            bad = [b.index for b in self.buckets if b.fired != 1]
+            if bad:
+                raise RuntimeError(f"buckets {bad} fired != 1 times this iteration")
+        for b in self.buckets:
+            b.work = None
+            b.fired = 0
+            b.pending = len(b.params)
+        self._callback_queued = False
+        self.iteration += 1
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        old = self._sync_enabled
+        self._sync_enabled = False
+        try:
+            yield
+        finally:
+            self._sync_enabled = old
+
+    # ------------------------------------------------------------- forward
+    def forward(self, *args, **kwargs):
+        if self.comm is not None and self.broadcast_buffers and self.module.training \
+                and torch.is_grad_enabled():
+            self._broadcast_buffers()
+        return self.module(*args, **kwargs)
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.flat.zero_grad()

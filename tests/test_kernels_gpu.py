@@ -1,0 +1,176 @@
+"""Numerics of every gfx950 kernel against the PyTorch fp32 reference
+primitive of the same op (ops/torch_prims.py), on the same bf16 inputs.
+
+Conv shapes cover the ResNet-18-ref CIFAR layers and all 23
+unique ResNet-50 ImageNet layers at a small batch, in the
+fwd, dgrad and wgrad passes.
+"""
+import pytest
+import torch
+
+from pytorch_multiprocessing_distributed_amd.ops import torch_prims as TP
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+# (C, H, K, R, stride)  pad = R // 2
+R50_SHAPES = [
+    (8, 224, 64, 7, 2),  # stem (C padded 3 -> 8)
+    (64, 56, 64, 1, 1), (64, 56, 64, 3, 1), (64, 56, 256, 1, 1), (256, 56, 64, 1, 1),
+    (256, 56, 128, 1, 1), (128, 56, 128, 3, 2), (256, 56, 512, 1, 2), (128, 28, 512, 1, 1),
+    (512, 28, 128, 1, 1), (128, 28, 128, 3, 1), (512, 28, 256, 1, 1), (256, 28, 256, 3, 2),
+    (512, 28, 1024, 1, 2), (256, 14, 1024, 1, 1), (1024, 14, 256, 1, 1), (256, 14, 256, 3, 1),
+    (1024, 14, 512, 1, 1), (512, 14, 512, 3, 2), (1024, 14, 2048, 1, 2), (512, 7, 2048, 1, 1),
+    (2048, 7, 512, 1, 1), (512, 7, 512, 3, 1),
+]
+CIFAR_SHAPES = [(8, 32, 64, 3, 1), (64, 32, 64, 3, 1), (64, 32, 128, 3, 2), (64, 32, 128, 1, 2),
+                (128, 16, 128, 3, 1), (512, 4, 512, 3, 1)]
+
+
+def _hp():
+    from pytorch_multiprocessing_distributed_amd.ops import hip_prims
+    return hip_prims
+
+
+def _close(a, b, rel):
+    a = a.float()
+    b = b.float()
+    scale = b.abs().max().clamp_min(1e-6)
+    err = (a - b).abs().max() / scale
+    assert err < rel, f"max rel err {err.item():.3e} >= {rel}"
+
+
+def _batch_for(h):
+    return 2 if h >= 112 else (4 if h >= 28 else 8)
+
+
+@pytest.mark.parametrize("shape", R50_SHAPES + CIFAR_SHAPES, ids=lambda s: "C%d_H%d_K%d_R%d_s%d" % s)
+def test_conv_fwd_dgrad_wgrad(shape):
+    HP = _hp()
+    torch.manual_seed(0)
+    C, H, K, R, st = shape
+    pad = R // 2
+    N = _batch_for(H)
+    x = torch.randn(N, H, H, C, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(K, C, R, R, device=DEV) / (C * R * R) ** 0.5).contiguous(
+        memory_format=torch.channels_last)
+    wp = HP.conv_weight(w, torch.bfloat16, C, True)
+    wref = TP.conv_weight(w, torch.bfloat16, C)
+    assert torch.equal(wp[0], wref[0])
+    assert torch.equal(wp[1], wref[0].permute(3, 1, 2, 0).contiguous())
+    y, st_ = HP.conv_fwd(x, wp, st, pad, True)
+    yr, sr = TP.conv_fwd(x, wref, st, pad, True)
+    _close(y, yr, 2e-2)
+    _close(st_, sr, 2e-2)
+    dy = torch.randn_like(y)
+    dx = HP.conv_dgrad(dy, wp, tuple(x.shape), st, pad)
+    dxr = TP.conv_dgrad(dy, wref, tuple(x.shape), st, pad)
+    _close(dx, dxr, 2e-2)
+    dw = HP.conv_wgrad(dy, x, tuple(wp[0].shape), st, pad)
+    dwr = TP.conv_wgrad(dy, x, tuple(wref[0].shape), st, pad)
+    _close(dw, dwr, 2e-3)
+
+
+@pytest.mark.parametrize("mode", ["plain", "res", "two", "norelu"])
+@pytest.mark.parametrize("C", [64, 256, 2048])
+def test_bn_family(mode, C):
+    HP = _hp()
+    torch.manual_seed(1)
+    M = 4 * 7 * 7 * 3
+    y1 = (torch.randn(M, C, device=DEV) * 2 + 0.5).to(torch.bfloat16)
+    y2 = torch.randn(M, C, device=DEV).to(torch.bfloat16)
+    res = torch.randn(M, C, device=DEV).to(torch.bfloat16)
+    g = torch.rand(C, device=DEV) + 0.5
+    b = torch.randn(C, device=DEV)
+    yf = y1.float()
+    sums = torch.stack([yf.sum(0), (yf * yf).sum(0)])
+    count = torch.tensor([float(M)], device=DEV)
+    rm1, rv1 = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    nb1 = torch.zeros((), dtype=torch.long, device=DEV)
+    nb2 = nb1.clone()
+    p = HP.bn_finalize(sums, count, g, b, 1e-5, rm1, rv1, 0.1, nb1)
+    pr = TP.bn_finalize(sums, count, g, b, 1e-5, rm2, rv2, 0.1, nb2)
+    _close(p, pr, 1e-5)
+    _close(rm1, rm2, 1e-5)
+    _close(rv1, rv2, 1e-5)
+    assert nb1.item() == nb2.item() == 1
+    relu = mode != "norelu"
+    kw = {}
+    if mode == "res":
+        kw = dict(res=res)
+    if mode == "two":
+        kw = dict(y2=y2, p2=pr)
+    out = HP.bn_apply(y1, p, relu=relu, **kw)
+    outr = TP.bn_apply(y1, pr, relu=relu, **kw)
+    _close(out, outr, 1e-2)
+    dout = torch.randn(M, C, device=DEV).to(torch.bfloat16)
+    red = HP.bn_bwd_reduce(dout, outr, y1, pr, relu)
+    redr = TP.bn_bwd_reduce(dout, outr, y1, pr, relu)
+    _close(red, redr, 1e-3)
+    dy, dzm = HP.bn_bwd_elemt(dout, outr, y1, pr, g, redr, count, relu, want_dzm=True)
+    dyr, dzmr = TP.bn_bwd_elemt(dout, outr, y1, pr, g, redr, count, relu, want_dzm=True)
+    _close(dy, dyr, 1e-2)
+    _close(dzm, dzmr, 1e-2)
+    dye, _ = HP.bn_bwd_elemt_eval(dout, outr, pr, relu)
+    dyer, _ = TP.bn_bwd_elemt_eval(dout, outr, pr, relu)
+    _close(dye, dyer, 1e-2)
+    pe = HP.bn_eval_params(rm2, rv2, g, b, 1e-5)
+    per = TP.bn_eval_params(rm2, rv2, g, b, 1e-5)
+    _close(pe, per, 1e-5)
+
+
+def test_pools_loss_sgd():
+    HP = _hp()
+    torch.manual_seed(2)
+    # every 3x3 window sees the 9 distinct values of a per-channel permutation: no argmax ties
+    perm = torch.stack([torch.randperm(9, device=DEV) for _ in range(64)], 1).float()  # [9, C]
+    hh = torch.arange(112, device=DEV) % 3
+    slot = (hh.view(112, 1) * 3 + hh.view(1, 112)).view(1, 112, 112, 1).expand(2, 112, 112, 64)
+    x = torch.gather(perm.view(9, 1, 1, 64).expand(9, 112, 112, 64).unsqueeze(0).expand(2, -1, -1, -1, -1),
+                     1, slot.unsqueeze(1)).squeeze(1).to(torch.bfloat16)
+    o, a = HP.maxpool_fwd(x)
+    orf, ar = TP.maxpool_fwd(x)
+    assert torch.equal(o, orf)
+    do = torch.randn_like(o)
+    _close(HP.maxpool_bwd(do, a, tuple(x.shape)), TP.maxpool_bwd(do, ar, tuple(x.shape)), 1e-2)
+    x7 = torch.randn(4, 7, 7, 2048, device=DEV).to(torch.bfloat16)
+    _close(HP.avgpool_fwd(x7), TP.avgpool_fwd(x7), 1e-4)
+    g = torch.randn(4, 2048, device=DEV)
+    _close(HP.avgpool_bwd(g, tuple(x7.shape), torch.bfloat16),
+           TP.avgpool_bwd(g, tuple(x7.shape), torch.bfloat16), 1e-2)
+    logits = torch.randn(64, 1000, device=DEV) * 3
+    tgt = torch.randint(0, 1000, (64,), device=DEV)
+    tgt[:8] = logits[:8].argmax(1)
+    loss, lse = HP.xent_fwd(logits, tgt)
+    lossr, lser = TP.xent_fwd(logits, tgt)
+    _close(loss, lossr, 1e-5)
+    _close(lse, lser, 1e-5)
+    gl = torch.ones(1, device=DEV)
+    _close(HP.xent_bwd(gl, logits, tgt, lse), TP.xent_bwd(gl, logits, tgt, lser), 1e-5)
+    assert HP.correct_count(logits, tgt).item() == TP.correct_count(logits, tgt).item()
+    n = 1000003
+    p = torch.randn(n, device=DEV)
+    gg = torch.randn(n, device=DEV)
+    b1 = torch.zeros(n, device=DEV)
+    p2, b2 = p.clone(), b1.clone()
+    for first in (True, False):
+        HP.sgd_nesterov_(p, gg, b1, 0.1, 0.9, 1e-4, True, first)
+        TP.sgd_nesterov_(p2, gg, b2, 0.1, 0.9, 1e-4, True, first)
+    _close(p, p2, 1e-6)
+    _close(b1, b2, 1e-6)
+
+
+def test_data_kernels():
+    from pytorch_multiprocessing_distributed_amd.ops.native import C
+    x, y = C.synth_images(4, 224, 224, 8, 3, 1000, 123, 0)
+    assert x.shape == (4, 224, 224, 8) and y.shape == (4,)
+    assert x[..., 3:].abs().max().item() == 0
+    assert 0.5 < x[..., :3].float().std().item() < 1.5
+    assert int(y.min()) >= 0 and int(y.max()) < 1000
+    data = torch.randint(0, 256, (10, 32, 32, 3), dtype=torch.uint8, device=DEV)
+    idx = torch.tensor([3, 1, 7], device=DEV)
+    out = C.cifar_augment(data, idx, 3, False, 8, 0, 0, False)
+    ref = (data[idx].float() / 255 - 0.5) / 0.5
+    _close(out, ref, 1e-6)
