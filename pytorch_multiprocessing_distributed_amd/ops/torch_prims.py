@@ -12,6 +12,11 @@ import torch
 import torch.nn.functional as F
 
 
+def _f(x):
+    """Upcast to the accumulation dtype: fp32, or fp64 for fp64 inputs (tests)."""
+    return x if x.dtype == torch.float64 else x.float()
+
+
 def _nchw(x):
     return x.permute(0, 3, 1, 2)
 
@@ -32,11 +37,11 @@ def conv_weight(w, dtype, cin, want_t=True):
 
 def conv_fwd(x, wpack, stride, pad, want_stats):
     wk = wpack[0]
-    y = F.conv2d(_nchw(x).float(), wk.permute(0, 3, 1, 2).float(), stride=stride, padding=pad)
+    y = F.conv2d(_f(_nchw(x)), _f(wk.permute(0, 3, 1, 2)), stride=stride, padding=pad)
     y = _nhwc(y).to(x.dtype)
     stats = None
     if want_stats:
-        yf = y.float().reshape(-1, y.shape[-1])
+        yf = _f(y).reshape(-1, y.shape[-1])
         stats = torch.stack([yf.sum(0), (yf * yf).sum(0)])
     return y, stats
 
@@ -44,14 +49,14 @@ def conv_fwd(x, wpack, stride, pad, want_stats):
 def conv_dgrad(dy, wpack, x_shape, stride, pad):
     wk = wpack[0]
     n, h, w, c = x_shape
-    dx = torch.nn.grad.conv2d_input((n, c, h, w), wk.permute(0, 3, 1, 2).float(),
-                                    _nchw(dy).float(), stride=stride, padding=pad)
+    dx = torch.nn.grad.conv2d_input((n, c, h, w), _f(wk.permute(0, 3, 1, 2)),
+                                    _f(_nchw(dy)), stride=stride, padding=pad)
     return _nhwc(dx).to(dy.dtype)
 
 
 def conv_wgrad(dy, x, wk_shape, stride, pad):
     k, r, s, c = wk_shape
-    dw = torch.nn.grad.conv2d_weight(_nchw(x).float(), (k, c, r, s), _nchw(dy).float(),
+    dw = torch.nn.grad.conv2d_weight(_f(_nchw(x)), (k, c, r, s), _f(_nchw(dy)),
                                      stride=stride, padding=pad)
     return dw.permute(0, 2, 3, 1).contiguous()          # fp32 [K,R,S,C]
 
@@ -64,12 +69,12 @@ def bn_finalize(sums, count, gamma, beta, eps, running_mean=None, running_var=No
     """Global (sum, sum^2, count) -> params; updates running stats with the
     unbiased variance (torch batch_norm_gather_stats_with_counts semantics).
     ``count`` is a 1-element fp32 tensor so no host sync is needed."""
-    cnt = count.float()
+    cnt = _f(count)
     mean = sums[0] / cnt
     var = (sums[1] / cnt - mean * mean).clamp_min(0.0)
     invstd = torch.rsqrt(var + eps)
-    scale = gamma.detach().float() * invstd
-    shift = beta.detach().float() - mean * scale
+    scale = _f(gamma.detach()) * invstd
+    shift = _f(beta.detach()) - mean * scale
     if running_mean is not None:
         unbiased = var * (cnt / (cnt - 1.0).clamp_min(1.0))
         running_mean.mul_(1.0 - momentum).add_(mean.to(running_mean.dtype), alpha=momentum)
@@ -80,26 +85,26 @@ def bn_finalize(sums, count, gamma, beta, eps, running_mean=None, running_var=No
 
 
 def bn_eval_params(running_mean, running_var, gamma, beta, eps):
-    mean = running_mean.float()
-    invstd = torch.rsqrt(running_var.float() + eps)
-    scale = gamma.detach().float() * invstd
-    shift = beta.detach().float() - mean * scale
+    mean = _f(running_mean)
+    invstd = torch.rsqrt(_f(running_var) + eps)
+    scale = _f(gamma.detach()) * invstd
+    shift = _f(beta.detach()) - mean * scale
     return torch.stack([mean, invstd, scale, shift])
 
 
 def bn_apply(y1, p1, res=None, y2=None, p2=None, relu=True):
-    o = y1.float() * p1[2] + p1[3]
+    o = _f(y1) * p1[2] + p1[3]
     if y2 is not None:
-        o = o + y2.float() * p2[2] + p2[3]
+        o = o + _f(y2) * p2[2] + p2[3]
     elif res is not None:
-        o = o + res.float()
+        o = o + _f(res)
     if relu:
         o = o.clamp_min(0.0)
     return o.to(y1.dtype)
 
 
 def _dzm(dout, out, relu):
-    d = dout.float()
+    d = _f(dout)
     if relu:
         d = d * (out > 0)
     return d
@@ -109,17 +114,17 @@ def bn_bwd_reduce(dout, out, y, p, relu):
     """-> fp32 [2, C]: (sum dzm, sum dzm*xhat), dzm = dout * relu_mask."""
     c = y.shape[-1]
     d = _dzm(dout, out, relu).reshape(-1, c)
-    xhat = (y.float().reshape(-1, c) - p[0]) * p[1]
+    xhat = (_f(y).reshape(-1, c) - p[0]) * p[1]
     return torch.stack([d.sum(0), (d * xhat).sum(0)])
 
 
 def bn_bwd_elemt(dout, out, y, p, gamma, red, count, relu, want_dzm=False):
     d = _dzm(dout, out, relu)
-    xhat = (y.float() - p[0]) * p[1]
-    cnt = count.float()
+    xhat = (_f(y) - p[0]) * p[1]
+    cnt = _f(count)
     mdy = red[0] / cnt
     mdyx = red[1] / cnt
-    dy = ((d - mdy - xhat * mdyx) * (gamma.detach().float() * p[1])).to(y.dtype)
+    dy = ((d - mdy - xhat * mdyx) * (_f(gamma.detach()) * p[1])).to(y.dtype)
     return dy, (d.to(y.dtype) if want_dzm else None)
 
 
@@ -134,41 +139,41 @@ def maxpool_fwd(x):
     """3x3/s2/p1 max-pool; the auxiliary output is the input itself (the
     backward re-derives the routing so overlapping windows that pick the
     same element accumulate, which max_unpool2d would not)."""
-    out = F.max_pool2d(_nchw(x).float(), 3, 2, 1)
+    out = F.max_pool2d(_f(_nchw(x)), 3, 2, 1)
     return _nhwc(out).to(x.dtype), x
 
 
 def maxpool_bwd(dout, x, x_shape):
     with torch.enable_grad():
-        xf = _nchw(x).float().detach().requires_grad_(True)
+        xf = _f(_nchw(x)).detach().requires_grad_(True)
         out = F.max_pool2d(xf, 3, 2, 1)
-        (dx,) = torch.autograd.grad(out, xf, _nchw(dout).float())
+        (dx,) = torch.autograd.grad(out, xf, _f(_nchw(dout)))
     return _nhwc(dx).to(dout.dtype)
 
 
 def avgpool_fwd(x):
-    return x.float().mean(dim=(1, 2))
+    return _f(x).mean(dim=(1, 2))
 
 
 def avgpool_bwd(dout, x_shape, dtype):
     n, h, w, c = x_shape
-    return (dout.float() / (h * w)).reshape(n, 1, 1, c).expand(n, h, w, c).to(dtype).contiguous()
+    return (_f(dout) / (h * w)).reshape(n, 1, 1, c).expand(n, h, w, c).to(dtype).contiguous()
 
 
 # --------------------------------------------------------------- loss/acc
 def xent_fwd(logits, target):
     """Mean softmax cross-entropy; returns (loss[1] fp32, lse[N] fp32)."""
-    lf = logits.float()
+    lf = _f(logits)
     lse = torch.logsumexp(lf, dim=1)
     loss = (lse - lf.gather(1, target.view(-1, 1)).squeeze(1)).mean()
     return loss.reshape(1), lse
 
 
 def xent_bwd(gloss, logits, target, lse):
-    lf = logits.float()
+    lf = _f(logits)
     p = torch.exp(lf - lse[:, None])
     p[torch.arange(lf.shape[0], device=lf.device), target] -= 1.0
-    return (p * (gloss.float() / lf.shape[0])).to(logits.dtype)
+    return (p * (_f(gloss) / lf.shape[0])).to(logits.dtype)
 
 
 def correct_count(logits, target):

@@ -1,0 +1,177 @@
+"""Host-side parity: sampler, logger format, meters, accuracy, LR schedule, SGD."""
+import os
+
+import pytest
+import torch
+
+from pytorch_multiprocessing_distributed_amd.data.sampler import DistributedSampler
+from pytorch_multiprocessing_distributed_amd.utils.logger import (AverageMeter, DeviceMeter, Logger,
+                                                                  accuracy)
+
+
+class _DS:
+    def __init__(self, n):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+
+@pytest.mark.parametrize("n,w", [(50000, 2), (10000, 3), (10, 4), (7, 8), (64, 1)])
+@pytest.mark.parametrize("shuffle", [True, False])
+@pytest.mark.parametrize("drop_last", [False, True])
+def test_sampler_matches_torch(n, w, shuffle, drop_last):
+    for rank in range(w):
+        for epoch in (0, 3):
+            ref = torch.utils.data.DistributedSampler(_DS(n), num_replicas=w, rank=rank,
+                                                      shuffle=shuffle, seed=0, drop_last=drop_last)
+            ref.set_epoch(epoch)
+            ours = DistributedSampler(n, w, rank, shuffle=shuffle, seed=0, drop_last=drop_last)
+            ours.set_epoch(epoch)
+            assert list(ref) == ours.indices()
+            assert len(ref) == len(ours)
+
+
+def test_sampler_fixed_order_reproduces_reference():
+    s = DistributedSampler(100, 2, 0, fixed_order=True)
+    a = s.indices()
+    s.set_epoch(5)
+    assert s.indices() == a        # reference never calls set_epoch
+
+
+def test_logger_format(tmp_path):
+    p = tmp_path / "train.log"
+    lg = Logger(str(p))
+    lg.write([1, 2.5, 33.3333333])
+    lg.write([2, 0.1234567, 50.0])
+    assert p.read_text() == "0001 2.500000 33.333333\n0002 0.123457 50.000000\n"
+    rows = lg.read()
+    assert rows[0][:3] == [1.0, 2.5, 33.333333]
+    assert len(lg) == 2
+    with pytest.raises(AssertionError):
+        lg.write([1, 2.0])
+    lg2 = Logger(str(tmp_path / "x.log"))
+    lg2.write("abc")
+    with pytest.raises(TypeError):
+        Logger(str(tmp_path / "y.log")).write([object()])
+
+
+def test_meters():
+    m = AverageMeter()
+    m.update(2.0, 4)
+    m.update(4.0, 4)
+    assert m.val == 4.0 and m.avg == 3.0 and m.count == 8
+    d = DeviceMeter()
+    d.update(torch.tensor(2.0), 4)
+    d.update(torch.tensor(4.0), 4)
+    assert d.val == 4.0 and abs(d.avg - 3.0) < 1e-6
+
+
+def test_accuracy():
+    out = torch.tensor([[0.1, 0.9], [0.8, 0.2], [0.3, 0.7], [0.6, 0.4]])
+    tgt = torch.tensor([1, 0, 0, 0])
+    prec, correct = accuracy(out, tgt)
+    assert abs(prec.item() - 75.0) < 1e-6
+    assert correct.tolist() == [True, True, False, True]
+    p1 = accuracy(out, tgt, topk=(1, 2))[0]
+    assert abs(p1.item() - 75.0) < 1e-6
+
+
+def test_multistep_schedule_matches_reference_timing():
+    """Reference steps the scheduler at epoch start: epoch 60 already runs at 0.01."""
+    from pytorch_multiprocessing_distributed_amd.engine.optim import FusedSGD
+    from pytorch_multiprocessing_distributed_amd.models import ResNet18
+    opt = FusedSGD(ResNet18(), lr=0.1)
+    sch = torch.optim.lr_scheduler.MultiStepLR(opt, milestones=[60, 80], gamma=0.1)
+    lrs = {}
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for epoch in range(1, 91):
+            sch.step()
+            lrs[epoch] = opt.param_groups[0]["lr"]
+    assert lrs[59] == pytest.approx(0.1)
+    assert lrs[60] == pytest.approx(0.01)
+    assert lrs[80] == pytest.approx(0.001)
+
+
+def test_fused_sgd_matches_torch_sgd():
+    from pytorch_multiprocessing_distributed_amd.engine.optim import FusedSGD
+    torch.manual_seed(0)
+    a = torch.nn.Sequential(torch.nn.Linear(7, 5), torch.nn.Linear(5, 3))
+    b = torch.nn.Sequential(torch.nn.Linear(7, 5), torch.nn.Linear(5, 3))
+    b.load_state_dict(a.state_dict())
+    oa = FusedSGD(a, lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    ob = torch.optim.SGD(b.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    for step in range(4):
+        x = torch.randn(9, 7)
+        for m, o in ((a, oa), (b, ob)):
+            o.zero_grad()
+            m(x).pow(2).sum().backward()
+            o.step()
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(pa, pb, rtol=1e-6, atol=1e-6)
+
+
+def test_config_reference_flags():
+    from pytorch_multiprocessing_distributed_amd.config import parse_args
+    a = parse_args([])
+    assert (a.batch_size, a.epochs, a.model, a.save_path, a.gpu, a.print_freq, a.world_size) == \
+        (64, 20, "res", "./test/", "7", 10, 2)
+    a = parse_args(["-p", "5", "--stem", "imagenet"])
+    assert a.print_freq == 5 and a.image_size == 224 and a.num_classes == 1000
+    assert a.milestone_list == [60, 80]
+
+
+def test_cifar_binary_reader(tmp_path):
+    import numpy as np
+    from pytorch_multiprocessing_distributed_amd.data.cifar import load_cifar10
+    d = tmp_path / "cifar-10-batches-bin"
+    d.mkdir()
+    rng = np.random.default_rng(0)
+    recs = {}
+    for name in [f"data_batch_{i}.bin" for i in range(1, 6)] + ["test_batch.bin"]:
+        r = rng.integers(0, 256, size=(4, 3073), dtype=np.uint8)
+        r[:, 0] %= 10
+        r.tofile(d / name)
+        recs[name] = r
+    x, y = load_cifar10(str(tmp_path), train=False)
+    r = recs["test_batch.bin"]
+    assert x.shape == (4, 32, 32, 3) and y.tolist() == r[:, 0].tolist()
+    # CHW planes -> HWC
+    assert x[1, 2, 3, 1].item() == r[1, 1 + 1024 + 2 * 32 + 3]
+    x, y = load_cifar10(str(tmp_path), train=True)
+    assert x.shape[0] == 20
+    assert load_cifar10(str(tmp_path / "nope"), True) is None
+
+
+def test_cifar_py_reader_refuses_code(tmp_path):
+    import pickle
+    import numpy as np
+    from pytorch_multiprocessing_distributed_amd.data.cifar import _load_py_batch
+    good = tmp_path / "good"
+    with open(good, "wb") as f:
+        pickle.dump({"data": np.zeros((2, 3072), np.uint8), "labels": [1, 2]}, f)
+    x, y = _load_py_batch(str(good))
+    assert x.shape == (2, 32, 32, 3) and y.tolist() == [1, 2]
+    bad = tmp_path / "bad"
+    with open(bad, "wb") as f:
+        pickle.dump({"data": os.getcwd}, f)
+    with pytest.raises(pickle.UnpicklingError):
+        _load_py_batch(str(bad))
+
+
+def test_augment_reference_semantics():
+    from pytorch_multiprocessing_distributed_amd.data.loader import augment_params, cifar_augment_torch
+    data = torch.randint(0, 256, (5, 32, 32, 3), dtype=torch.uint8)
+    idx = torch.tensor([4, 0, 2])
+    x = cifar_augment_torch(data, idx, 3, False, 8, 0, 0, torch.float32)
+    torch.testing.assert_close(x, (data[idx].float() / 255 - 0.5) / 0.5)
+    x = cifar_augment_torch(data, idx, 8, True, 8, 0, 3, torch.float32)
+    assert x.shape == (3, 32, 32, 8) and x[..., 3:].abs().max() == 0
+    oy, ox, fl = augment_params(idx.numpy(), 0, 3)
+    assert ((oy >= 0) & (oy <= 16) & (ox >= 0) & (ox <= 16)).all()
+    # pixels that came from the zero padding normalise to -1 like torchvision
+    for i in range(3):
+        if oy[i] < 8:
+            assert torch.all(x[i, 0, :, :3] == -1.0)
