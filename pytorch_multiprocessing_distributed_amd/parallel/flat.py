@@ -31,13 +31,14 @@ def _phys_shape_and_perm(p):
 
 
 class FlatParams:
-    def __init__(self, module: torch.nn.Module, dtype=torch.float32):
+    def __init__(self, module: torch.nn.Module, dtype=None):
         named = [(n, p) for n, p in module.named_parameters() if p.requires_grad]
         if not named:
             raise ValueError("module has no trainable parameters")
         self.names = [n for n, _ in reversed(named)]
         self.params = [p for _, p in reversed(named)]
         dev = self.params[0].device
+        dtype = dtype or self.params[0].dtype
         for p in self.params:
             if p.dtype != dtype:
                 raise TypeError(f"flat arena expects {dtype} master params, got {p.dtype}")
