@@ -16,6 +16,8 @@ using torch::Tensor;
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
+constexpr int64_t pmd_slots() { return 64; }  // == pmd::kStatSlots (kernels/common.h)
+
 #define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
 #define CHECK_CONT(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
 #define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == torch::kBFloat16, #t " must be bf16")
@@ -55,7 +57,7 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor wk, int64_t stride, int64_t pad, b
   c10::DeviceGuard g(x.device());
   Tensor y = torch::empty({N, P, Q, K}, x.options());
   Tensor stats;
-  if (want_stats) stats = torch::zeros({2, K}, x.options().dtype(torch::kFloat32));
+  if (want_stats) stats = torch::zeros({pmd_slots(), 2, K}, x.options().dtype(torch::kFloat32));
   const int rc = pmd::conv_igemm_launch(bfp(x), bfp(wk), bfp_mut(y),
                                         want_stats ? stats.data_ptr<float>() : nullptr, N, H, W, C, P,
                                         Q, K, R, S, (int)stride, (int)pad, false, cur_stream());
@@ -127,6 +129,27 @@ Tensor bn_finalize(c10::optional<Tensor> sums, c10::optional<Tensor> count, Tens
   return params;
 }
 
+// slot-stats [S,2,Ca] (+ [S,2,Cb]) -> flat [2Ca (+2Cb) (+1 count)]
+Tensor stats_collapse(Tensor a, c10::optional<Tensor> b, c10::optional<double> count) {
+  CHECK_DEV(a); CHECK_F32(a); CHECK_CONT(a);
+  TORCH_CHECK(a.dim() == 3 && a.size(0) == pmd_slots() && a.size(1) == 2, "slot stats [S,2,C]");
+  const int Ca = a.size(2);
+  int Cb = 0;
+  const float* bp = nullptr;
+  if (b && b->defined()) {
+    CHECK_F32(*b); CHECK_CONT(*b);
+    TORCH_CHECK(b->dim() == 3 && b->size(0) == pmd_slots(), "slot stats [S,2,C]");
+    Cb = b->size(2);
+    bp = b->data_ptr<float>();
+  }
+  const bool wc = count.has_value();
+  c10::DeviceGuard g(a.device());
+  Tensor out = torch::empty({2 * Ca + 2 * Cb + (wc ? 1 : 0)}, a.options());
+  pmd::stats_collapse_launch(a.data_ptr<float>(), Ca, bp, Cb, wc ? (float)*count : 0.f,
+                             out.data_ptr<float>(), wc, cur_stream());
+  return out;
+}
+
 Tensor bn_apply(Tensor y1, Tensor p1, c10::optional<Tensor> res, c10::optional<Tensor> y2,
                 c10::optional<Tensor> p2, bool relu) {
   CHECK_DEV(y1); CHECK_BF16(y1); CHECK_CONT(y1);
@@ -164,7 +187,7 @@ Tensor bn_bwd_reduce(Tensor dout, Tensor out, Tensor y, Tensor params, bool relu
   const long long M = y.numel() / C;
   TORCH_CHECK(M < (1ll << 31), "too many rows");
   c10::DeviceGuard g(y.device());
-  Tensor red = torch::zeros({2, C}, y.options().dtype(torch::kFloat32));
+  Tensor red = torch::zeros({pmd_slots(), 2, C}, y.options().dtype(torch::kFloat32));
   const int rc = pmd::bn_bwd_reduce_launch(bfp(dout), bfp(out), bfp(y), params.data_ptr<float>(),
                                            red.data_ptr<float>(), (int)M, C, relu, cur_stream());
   CHECK_RC(rc, "bn_bwd_reduce");
@@ -321,6 +344,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad", &conv_wgrad);
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_apply", &bn_apply);
+  m.def("stats_collapse", &stats_collapse);
   m.def("bn_bwd_reduce", &bn_bwd_reduce);
   m.def("bn_bwd_elemt", &bn_bwd_elemt);
   m.def("maxpool_fwd", &maxpool_fwd);

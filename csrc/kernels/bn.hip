@@ -146,8 +146,9 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      atomicAdd(red + c0 + k, a1[k]);
-      atomicAdd(red + C + c0 + k, a2[k]);
+      float* slot = red + (size_t)(blockIdx.x % kStatSlots) * 2 * C;
+      atomicAdd(slot + c0 + k, a1[k]);
+      atomicAdd(slot + C + c0 + k, a2[k]);
     }
   }
 }
@@ -200,6 +201,35 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(
     reinterpret_cast<uint4*>(dy)[i] = pack8(o);
     if (DZM) reinterpret_cast<uint4*>(dzm_out)[i] = pack8(d);
   }
+}
+
+// out[0:2Ca] = sum_slots a[slot][2][Ca]; out[2Ca:2Ca+2Cb] = same for b; out[last] = count
+__global__ void stats_collapse_kernel(const float* __restrict__ a, int Ca, const float* __restrict__ b,
+                                      int Cb, float count, float* __restrict__ out, int with_count) {
+  const int na = 2 * Ca, nb = b ? 2 * Cb : 0;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < na) {
+    float s = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < kStatSlots; ++k) s += a[(size_t)k * na + i];
+    out[i] = s;
+  } else if (i < na + nb) {
+    const int j = i - na;
+    float s = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < kStatSlots; ++k) s += b[(size_t)k * nb + j];
+    out[i] = s;
+  } else if (with_count && i == na + nb) {
+    out[i] = count;
+  }
+}
+
+int stats_collapse_launch(const float* a, int Ca, const float* b, int Cb, float count, float* out,
+                          bool with_count, hipStream_t st) {
+  const int n = 2 * Ca + (b ? 2 * Cb : 0) + (with_count ? 1 : 0);
+  hipLaunchKernelGGL(stats_collapse_kernel, dim3((n + 255) / 256), dim3(256), 0, st, a, Ca, b, Cb,
+                     count, out, with_count ? 1 : 0);
+  return 0;
 }
 
 static int ew_grid(long long nchunk, int C8) {

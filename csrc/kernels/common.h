@@ -13,6 +13,10 @@ typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef unsigned short bf16_t;  // storage type of one bf16
 
 constexpr int kWave = 64;  // CDNA wavefront
+// Per-channel statistics are accumulated into kStatSlots copies ([slot][2][C])
+// picked by block index, so thousands of blocks do not serialise their fp32
+// atomics on the same 2C addresses; stats_collapse sums the slots.
+constexpr int kStatSlots = 64;
 
 __device__ __forceinline__ float bf2f(bf16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
 

@@ -61,27 +61,48 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
   const int wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
 
+  // Strided dgrad is split into stride^2 output phases (blockIdx.y): in phase
+  // (ph, pw) only taps r == (ph+pad) mod 2 (resp. s) contribute, so every
+  // gathered tap is real work (no 3/4-masked MFMAs); rows of the phase GEMM
+  // are the output pixels (n, 2*hh+ph, 2*ww+pw).
+  int ph = 0, pw = 0, OHp = a.OH, OWp = a.OW, r0 = 0, s0 = 0, rstep = 1, ns = a.S, Mp = a.M,
+      Kgp = a.Kg;
+  if (DGRAD && a.stride == 2) {
+    ph = blockIdx.y >> 1;
+    pw = blockIdx.y & 1;
+    OHp = (a.OH - ph + 1) >> 1;
+    OWp = (a.OW - pw + 1) >> 1;
+    r0 = (ph + a.pad) & 1;
+    s0 = (pw + a.pad) & 1;
+    rstep = 2;
+    const int nr = (a.R - r0 + 1) >> 1;
+    ns = (a.S - s0 + 1) >> 1;
+    Mp = a.N * OHp * OWp;
+    Kgp = nr * ns * a.Cs;
+  }
   const int tilesN = (a.Nout + BN - 1) / BN;
-  const int tilesM = (a.M + BM - 1) / BM;
+  const int Mgrid = (DGRAD && a.stride == 2) ? a.N * ((a.OH + 1) >> 1) * ((a.OW + 1) >> 1) : a.M;
+  const int tilesM = (Mgrid + BM - 1) / BM;  // grid.x sized for the largest phase
   const int L = xcd_remap(blockIdx.x, tilesM * tilesN);
   const int m0 = (L / tilesN) * BM;
   const int n0 = (L % tilesN) * BN;
+  if (m0 >= Mp) return;  // uniform per block, before any barrier
 
   // ---- per-thread A-row precompute
   const int chunk = tid & 7;
   const int rsub = tid >> 3;  // 0..31
   int a_base[PA], a_h[PA], a_w[PA];
   bool a_ok[PA];
-  const int ohw = a.OH * a.OW;
+  const int ohw = OHp * OWp;
 #pragma unroll
   for (int i = 0; i < PA; ++i) {
     const int m = m0 + rsub + 32 * i;
-    a_ok[i] = m < a.M;
+    a_ok[i] = m < Mp;
     const int mm = a_ok[i] ? m : 0;
     const int n = mm / ohw;
     const int rem = mm - n * ohw;
-    const int oh = rem / a.OW;
-    const int ow = rem - oh * a.OW;
+    const int oh = (rem / OWp) * rstep + ph;
+    const int ow = (rem - (rem / OWp) * OWp) * rstep + pw;
     a_base[i] = n * a.H * a.W;  // pixel index base
     if (DGRAD) {
       a_h[i] = oh + a.pad;
@@ -101,15 +122,17 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
   }
 
   uint4 ra[PA], rb[PB];
-  const int nk = (a.Kg + BK - 1) / BK;
+  const int nk = (Kgp + BK - 1) / BK;
 
   auto load_tile = [&](int kt) {
     const int k0 = kt * BK + chunk * 8;
-    const bool kok = k0 < a.Kg;
+    const bool kok = k0 < Kgp;
     const int tap = k0 >> a.log2Cs;
     const int c = k0 & (a.Cs - 1);
-    const int r = tap / a.S;
-    const int s = tap - r * a.S;
+    const int tr = tap / ns;
+    const int r = r0 + rstep * tr;
+    const int s = s0 + rstep * (tap - tr * ns);
+    const int boff = ((r * a.S + s) << a.log2Cs) + c;
 #pragma unroll
     for (int i = 0; i < PA; ++i) {
       int ih, iw;
@@ -134,7 +157,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (b_ok[i] && kok) v = *reinterpret_cast<const uint4*>(b_row[i] + k0);
+      if (b_ok[i] && kok) v = *reinterpret_cast<const uint4*>(b_row[i] + boff);
       rb[i] = v;
     }
   };
@@ -155,8 +178,10 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  load_tile(0);
-  store_tile(0);
+  if (nk > 0) {
+    load_tile(0);
+    store_tile(0);
+  }
   __syncthreads();
 
   const int frow = lane & 15;
@@ -231,7 +256,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
       const int which = c / BN, col = c % BN;
       if (n0 + col < a.Nout) {
         const float v = st[(0 * 2 + which) * BN + col] + st[(1 * 2 + which) * BN + col];
-        atomicAdd(a.stats + which * a.Nout + n0 + col, v);
+        atomicAdd(a.stats + ((size_t)((m0 / BM) % kStatSlots) * 2 + which) * a.Nout + n0 + col, v);
       }
     }
   }
@@ -239,9 +264,16 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
   for (int idx = tid; idx < BM * CPR; idx += 256) {
     const int row = idx / CPR, cc = idx % CPR;
     const int m = m0 + row, n = n0 + cc * 8;
-    if (m < a.M && n < a.Nout)
-      *reinterpret_cast<uint4*>(a.out + (size_t)m * a.Nout + n) =
+    if (m < Mp && n < a.Nout) {
+      size_t orow = m;
+      if (DGRAD && a.stride == 2) {
+        const int nb = m / ohw, rem = m - nb * ohw;
+        const int hh = rem / OWp, ww = rem - hh * OWp;
+        orow = ((size_t)nb * a.OH + 2 * hh + ph) * a.OW + 2 * ww + pw;
+      }
+      *reinterpret_cast<uint4*>(a.out + orow * a.Nout + n) =
           *reinterpret_cast<const uint4*>(Cs + row * LDC + cc * 8);
+    }
   }
 }
 
@@ -270,8 +302,12 @@ static int ilog2(int v) {
 
 template <int BM, int BN, bool DGRAD, bool STATS>
 static void launch_t(const ConvArgs& a, hipStream_t st) {
-  const int tiles = ((a.M + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, DGRAD, STATS>), dim3(tiles), dim3(256), 0, st, a);
+  const bool ph2 = DGRAD && a.stride == 2;
+  const int Mgrid = ph2 ? a.N * ((a.OH + 1) >> 1) * ((a.OW + 1) >> 1) : a.M;
+  const int tiles = ((Mgrid + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
+  const int phases = ph2 ? 4 : 1;
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, DGRAD, STATS>), dim3(tiles, phases), dim3(256), 0, st,
+                     a);
 }
 
 template <bool DGRAD, bool STATS>

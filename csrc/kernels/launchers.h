@@ -17,6 +17,8 @@ int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, int N, int H
 int bn_finalize_launch(const float* sums, const float* count, const float* gamma, const float* beta,
                        float* params, float* rm, float* rv, long long* nbt, int C, float eps,
                        float momentum, bool eval_mode, hipStream_t st);
+int stats_collapse_launch(const float* a, int Ca, const float* b, int Cb, float count, float* out,
+                          bool with_count, hipStream_t st);
 int bn_apply_launch(const bf16_t* y1, const float* p1, const bf16_t* r, const float* p2, bf16_t* out,
                     long long M, int C, int mode, bool relu, hipStream_t st);
 int bn_bwd_reduce_launch(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const float* params,

@@ -113,11 +113,9 @@ class _BNActFn(torch.autograd.Function):
         m_local = y1.numel() // c1
         two = y2 is not None
         if training:
-            parts = [s1.reshape(-1)]
-            if two:
-                parts.append(s2.reshape(-1))
-            parts.append(torch.full((1,), float(m_local), device=y1.device, dtype=torch.float32))
-            buf = torch.cat(parts)
+            # local (sum, sum^2) of both branches + element count in ONE buffer
+            # -> one all-reduce per BN site (both BNs of a projection block share it)
+            buf = P.stats_collapse(s1, s2 if two else None, float(m_local))
             if sync is not None:
                 sync.all_reduce_(buf)
             count = buf[-1:]
@@ -155,19 +153,21 @@ class _BNActFn(torch.autograd.Function):
         P = prims_for(y1)
         dout = dout.contiguous()
         d_y1 = d_g1 = d_b1 = d_res = d_y2 = d_g2 = d_b2 = None
-        red1 = P.bn_bwd_reduce(dout, out, y1, p1, relu)
-        red2 = P.bn_bwd_reduce(dout, out, y2, p2, relu) if two else None
-        d_g1, d_b1 = red1[1].clone(), red1[0].clone()
+        r1 = P.bn_bwd_reduce(dout, out, y1, p1, relu)
+        r2 = P.bn_bwd_reduce(dout, out, y2, p2, relu) if two else None
+        red = P.stats_collapse(r1, r2, None)            # flat [2C1 (+2C2)], local sums
+        c1 = y1.shape[-1]
+        # gamma/beta grads use the LOCAL sums (DDP averages them), like torch SyncBN
+        d_b1, d_g1 = red[:c1], red[c1:2 * c1]
         if two:
-            d_g2, d_b2 = red2[1].clone(), red2[0].clone()
+            c2 = y2.shape[-1]
+            d_b2, d_g2 = red[2 * c1:2 * c1 + c2], red[2 * c1 + c2:]
         if training:
             if sync is not None:
-                gbuf = torch.cat([red1.reshape(-1), red2.reshape(-1)]) if two else red1.reshape(-1).clone()
-                sync.all_reduce_(gbuf)
-                c1 = y1.shape[-1]
-                red1 = gbuf[: 2 * c1].view(2, c1)
-                if two:
-                    red2 = gbuf[2 * c1:].view(2, -1)
+                red = red.clone()
+                sync.all_reduce_(red)
+            red1 = red[:2 * c1].view(2, c1)
+            red2 = red[2 * c1:].view(2, -1) if two else None
             d_y1, dzm = P.bn_bwd_elemt(dout, out, y1, p1, g1, red1, count, relu,
                                        want_dzm=has_res)
             if two:

@@ -45,6 +45,11 @@ def bn_eval_params(running_mean, running_var, gamma, beta, eps):
                           running_var, 0.0, None, True)
 
 
+def stats_collapse(a, b=None, count=None):
+    """[S,2,Ca] (+[S,2,Cb]) slot statistics -> flat [2Ca (+2Cb) (+1 count)]."""
+    return _C.stats_collapse(a, b, None if count is None else float(count))
+
+
 def bn_apply(y1, p1, res=None, y2=None, p2=None, relu=True):
     return _C.bn_apply(y1, p1, res, y2, p2, bool(relu))
 

@@ -92,6 +92,16 @@ def bn_eval_params(running_mean, running_var, gamma, beta, eps):
     return torch.stack([mean, invstd, scale, shift])
 
 
+def stats_collapse(a, b=None, count=None):
+    """Per-channel stat blocks -> one flat buffer [2Ca (+2Cb) (+1 count)]."""
+    parts = [a.reshape(-1)]
+    if b is not None:
+        parts.append(b.reshape(-1))
+    if count is not None:
+        parts.append(torch.full((1,), float(count), dtype=a.dtype, device=a.device))
+    return torch.cat(parts)
+
+
 def bn_apply(y1, p1, res=None, y2=None, p2=None, relu=True):
     o = _f(y1) * p1[2] + p1[3]
     if y2 is not None:
