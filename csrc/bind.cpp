@@ -46,7 +46,16 @@ std::vector<Tensor> conv_weight_prep(Tensor w, int64_t cp, bool want_t) {
   return {wk};
 }
 
-std::vector<Tensor> conv_fwd(Tensor x, Tensor wk, int64_t stride, int64_t pad, bool want_stats) {
+float* opt_f32(const c10::optional<Tensor>& t, const char* what) {
+  if (!t || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kFloat32 && t->is_contiguous(), what,
+              " must be a contiguous fp32 GPU tensor");
+  return t->data_ptr<float>();
+}
+
+// stats_buf: optional pre-zeroed [S,2,K] slot buffer (pool); allocated zeroed otherwise
+std::vector<Tensor> conv_fwd(Tensor x, Tensor wk, int64_t stride, int64_t pad, bool want_stats,
+                             c10::optional<Tensor> stats_buf) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_CONT(x);
   CHECK_DEV(wk); CHECK_BF16(wk); CHECK_CONT(wk);
   TORCH_CHECK(x.dim() == 4 && wk.dim() == 4, "x [N,H,W,C], wk [K,R,S,C]");
@@ -57,17 +66,27 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor wk, int64_t stride, int64_t pad, b
   c10::DeviceGuard g(x.device());
   Tensor y = torch::empty({N, P, Q, K}, x.options());
   Tensor stats;
-  if (want_stats) stats = torch::zeros({pmd_slots(), 2, K}, x.options().dtype(torch::kFloat32));
+  if (want_stats) {
+    if (stats_buf && stats_buf->defined()) {
+      TORCH_CHECK(stats_buf->numel() == pmd_slots() * 2 * K, "stats buffer must be [S,2,K]");
+      opt_f32(stats_buf, "stats_buf");
+      stats = *stats_buf;
+    } else {
+      stats = torch::zeros({pmd_slots(), 2, K}, x.options().dtype(torch::kFloat32));
+    }
+  }
   const int rc = pmd::conv_igemm_launch(bfp(x), bfp(wk), bfp_mut(y),
                                         want_stats ? stats.data_ptr<float>() : nullptr, N, H, W, C, P,
-                                        Q, K, R, S, (int)stride, (int)pad, false, cur_stream());
+                                        Q, K, R, S, (int)stride, (int)pad, false, nullptr, cur_stream());
   CHECK_RC(rc, "conv_fwd");
   if (want_stats) return {y, stats};
   return {y};
 }
 
 // dx[N,H,W,Cp] from dy[N,P,Q,K] and wkt[Cp,R,S,K]
-Tensor conv_dgrad(Tensor dy, Tensor wkt, int64_t H, int64_t W, int64_t stride, int64_t pad) {
+// addend: optional [N,H,W,Cp] bf16 added in the epilogue (dx = dgrad + addend)
+Tensor conv_dgrad(Tensor dy, Tensor wkt, int64_t H, int64_t W, int64_t stride, int64_t pad,
+                  c10::optional<Tensor> addend) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONT(dy);
   CHECK_DEV(wkt); CHECK_BF16(wkt); CHECK_CONT(wkt);
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), K = dy.size(3);
@@ -77,14 +96,23 @@ Tensor conv_dgrad(Tensor dy, Tensor wkt, int64_t H, int64_t W, int64_t stride, i
               "dgrad spatial mismatch");
   c10::DeviceGuard g(dy.device());
   Tensor dx = torch::empty({N, H, W, Cp}, dy.options());
+  const pmd::bf16_t* add = nullptr;
+  if (addend && addend->defined()) {
+    CHECK_BF16(*addend); CHECK_CONT(*addend);
+    TORCH_CHECK(addend->sizes() == dx.sizes(), "addend shape");
+    add = bfp(*addend);
+  }
   // the gathered operand is dy (spatial P x Q, K channels); output spatial is H x W
   const int rc = pmd::conv_igemm_launch(bfp(dy), bfp(wkt), bfp_mut(dx), nullptr, N, P, Q, K, (int)H,
-                                        (int)W, Cp, R, S, (int)stride, (int)pad, true, cur_stream());
+                                        (int)W, Cp, R, S, (int)stride, (int)pad, true, add,
+                                        cur_stream());
   CHECK_RC(rc, "conv_dgrad");
   return dx;
 }
 
-Tensor conv_wgrad(Tensor dy, Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad) {
+// out: optional [K,R,S,C] fp32 accumulation target (e.g. a grad-arena view); dW is ADDED to it
+Tensor conv_wgrad(Tensor dy, Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad,
+                  c10::optional<Tensor> out) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONT(dy);
   CHECK_DEV(x); CHECK_BF16(x); CHECK_CONT(x);
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
@@ -93,7 +121,14 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int64_t R, int64_t S, int64_t stride, int
   TORCH_CHECK((H + 2 * pad - R) / stride + 1 == P && (W + 2 * pad - S) / stride + 1 == Q,
               "wgrad spatial mismatch");
   c10::DeviceGuard g(x.device());
-  Tensor dw = torch::zeros({K, R, S, C}, x.options().dtype(torch::kFloat32));
+  Tensor dw;
+  if (out && out->defined()) {
+    TORCH_CHECK(out->sizes() == torch::IntArrayRef({K, R, S, C}), "wgrad out shape");
+    opt_f32(out, "wgrad out");
+    dw = *out;
+  } else {
+    dw = torch::zeros({K, R, S, C}, x.options().dtype(torch::kFloat32));
+  }
   const int rc = pmd::conv_wgrad_launch(bfp(dy), bfp(x), dw.data_ptr<float>(), N, H, W, C, P, Q, K,
                                         (int)R, (int)S, (int)stride, (int)pad, cur_stream());
   CHECK_RC(rc, "conv_wgrad");
@@ -129,25 +164,53 @@ Tensor bn_finalize(c10::optional<Tensor> sums, c10::optional<Tensor> count, Tens
   return params;
 }
 
-// slot-stats [S,2,Ca] (+ [S,2,Cb]) -> flat [2Ca (+2Cb) (+1 count)]
-Tensor stats_collapse(Tensor a, c10::optional<Tensor> b, c10::optional<double> count) {
+// slot-stats [S,2,Ca] (+ [S,2,Cb]) -> flat [2Ca (+2Cb) (+1 count)]; clear: zero the
+// slot buffers after reading; acc_*: optional d_beta/d_gamma targets that get += the sums
+Tensor stats_collapse(Tensor a, c10::optional<Tensor> b, c10::optional<double> count, bool clear,
+                      c10::optional<Tensor> acc_a0, c10::optional<Tensor> acc_a1,
+                      c10::optional<Tensor> acc_b0, c10::optional<Tensor> acc_b1) {
   CHECK_DEV(a); CHECK_F32(a); CHECK_CONT(a);
   TORCH_CHECK(a.dim() == 3 && a.size(0) == pmd_slots() && a.size(1) == 2, "slot stats [S,2,C]");
   const int Ca = a.size(2);
   int Cb = 0;
-  const float* bp = nullptr;
+  float* bp = nullptr;
   if (b && b->defined()) {
     CHECK_F32(*b); CHECK_CONT(*b);
     TORCH_CHECK(b->dim() == 3 && b->size(0) == pmd_slots(), "slot stats [S,2,C]");
     Cb = b->size(2);
     bp = b->data_ptr<float>();
   }
+  auto chk = [&](const c10::optional<Tensor>& t, int C) {
+    float* p = opt_f32(t, "grad target");
+    if (p) TORCH_CHECK(t->numel() == C, "grad target size");
+    return p;
+  };
   const bool wc = count.has_value();
   c10::DeviceGuard g(a.device());
   Tensor out = torch::empty({2 * Ca + 2 * Cb + (wc ? 1 : 0)}, a.options());
   pmd::stats_collapse_launch(a.data_ptr<float>(), Ca, bp, Cb, wc ? (float)*count : 0.f,
-                             out.data_ptr<float>(), wc, cur_stream());
+                             out.data_ptr<float>(), wc, clear, chk(acc_a0, Ca), chk(acc_a1, Ca),
+                             chk(acc_b0, Cb), chk(acc_b1, Cb), cur_stream());
   return out;
+}
+
+// collapse(+clear) slot stats and finalize BN params in one launch (no all-reduce case)
+Tensor stats_finalize_local(Tensor slots, double count, Tensor gamma, Tensor beta, double eps,
+                            c10::optional<Tensor> rm, c10::optional<Tensor> rv, double momentum,
+                            c10::optional<Tensor> nbt) {
+  CHECK_DEV(slots); CHECK_F32(slots); CHECK_CONT(slots);
+  const int C = gamma.numel();
+  TORCH_CHECK(slots.numel() == pmd_slots() * 2 * C, "slot stats [S,2,C]");
+  c10::DeviceGuard g(slots.device());
+  Tensor params = torch::empty({4, C}, gamma.options());
+  long long* nb = nullptr;
+  if (nbt && nbt->defined()) nb = reinterpret_cast<long long*>(nbt->data_ptr<int64_t>());
+  Tensor gm = gamma.contiguous(), bt = beta.contiguous();
+  pmd::stats_finalize_local_launch(slots.data_ptr<float>(), (float)count, gm.data_ptr<float>(),
+                                   bt.data_ptr<float>(), params.data_ptr<float>(), opt_f32(rm, "rm"),
+                                   opt_f32(rv, "rv"), nb, C, (float)eps, (float)momentum,
+                                   cur_stream());
+  return params;
 }
 
 Tensor bn_apply(Tensor y1, Tensor p1, c10::optional<Tensor> res, c10::optional<Tensor> y2,
@@ -180,23 +243,32 @@ Tensor bn_apply(Tensor y1, Tensor p1, c10::optional<Tensor> res, c10::optional<T
   return out;
 }
 
-Tensor bn_bwd_reduce(Tensor dout, Tensor out, Tensor y, Tensor params, bool relu) {
+Tensor bn_bwd_reduce(Tensor dout, Tensor out, Tensor y, Tensor params, bool relu,
+                     c10::optional<Tensor> red_buf) {
   CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONT(dout);
   CHECK_BF16(out); CHECK_CONT(out); CHECK_BF16(y); CHECK_CONT(y);
   const int C = y.size(-1);
   const long long M = y.numel() / C;
   TORCH_CHECK(M < (1ll << 31), "too many rows");
   c10::DeviceGuard g(y.device());
-  Tensor red = torch::zeros({pmd_slots(), 2, C}, y.options().dtype(torch::kFloat32));
+  Tensor red;
+  if (red_buf && red_buf->defined()) {
+    TORCH_CHECK(red_buf->numel() == pmd_slots() * 2 * C, "reduce buffer must be [S,2,C]");
+    opt_f32(red_buf, "red_buf");
+    red = *red_buf;
+  } else {
+    red = torch::zeros({pmd_slots(), 2, C}, y.options().dtype(torch::kFloat32));
+  }
   const int rc = pmd::bn_bwd_reduce_launch(bfp(dout), bfp(out), bfp(y), params.data_ptr<float>(),
                                            red.data_ptr<float>(), (int)M, C, relu, cur_stream());
   CHECK_RC(rc, "bn_bwd_reduce");
   return red;
 }
 
+// count: device scalar (SyncBN global count) or, if absent, count_h from the host
 std::vector<Tensor> bn_bwd_elemt(Tensor dout, Tensor out, Tensor y, Tensor params, Tensor gamma,
-                                 c10::optional<Tensor> red, c10::optional<Tensor> count, bool relu,
-                                 bool want_dzm, bool eval_mode) {
+                                 c10::optional<Tensor> red, c10::optional<Tensor> count,
+                                 double count_h, bool relu, bool want_dzm, bool eval_mode) {
   CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONT(dout);
   CHECK_BF16(out); CHECK_CONT(out);
   const int C = dout.size(-1);
@@ -207,15 +279,15 @@ std::vector<Tensor> bn_bwd_elemt(Tensor dout, Tensor out, Tensor y, Tensor param
   if (want_dzm) dzm = torch::empty_like(dout);
   Tensor rr, cc, gm = gamma.contiguous();
   if (!eval_mode) {
-    TORCH_CHECK(red && red->defined() && count && count->defined(), "train backward needs sums");
+    TORCH_CHECK(red && red->defined(), "train backward needs sums");
     CHECK_BF16(y); CHECK_CONT(y);
     rr = red->contiguous();
-    cc = count->contiguous();
+    if (count && count->defined()) cc = count->contiguous();
   }
   const int rc = pmd::bn_bwd_elemt_launch(
       bfp(dout), bfp(out), eval_mode ? nullptr : bfp(y), params.data_ptr<float>(), gm.data_ptr<float>(),
-      eval_mode ? nullptr : rr.data_ptr<float>(), eval_mode ? nullptr : cc.data_ptr<float>(),
-      bfp_mut(dy), want_dzm ? bfp_mut(dzm) : nullptr, M, C, relu, eval_mode, cur_stream());
+      eval_mode ? nullptr : rr.data_ptr<float>(),
+      (eval_mode || !cc.defined()) ? nullptr : cc.data_ptr<float>(), (float)count_h, bfp_mut(dy), want_dzm ? bfp_mut(dzm) : nullptr, M, C, relu, eval_mode, cur_stream());
   CHECK_RC(rc, "bn_bwd_elemt");
   if (want_dzm) return {dy, dzm};
   return {dy};
@@ -345,6 +417,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_finalize", &bn_finalize);
   m.def("bn_apply", &bn_apply);
   m.def("stats_collapse", &stats_collapse);
+  m.def("stats_finalize_local", &stats_finalize_local);
   m.def("bn_bwd_reduce", &bn_bwd_reduce);
   m.def("bn_bwd_elemt", &bn_bwd_elemt);
   m.def("maxpool_fwd", &maxpool_fwd);

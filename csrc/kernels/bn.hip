@@ -159,8 +159,8 @@ template <bool RELU, bool DZM, bool EVAL>
 __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(
     const bf16_t* __restrict__ dout, const bf16_t* __restrict__ out, const bf16_t* __restrict__ y,
     const float* __restrict__ params, const float* __restrict__ gamma,
-    const float* __restrict__ red, const float* __restrict__ count, bf16_t* __restrict__ dy,
-    bf16_t* __restrict__ dzm_out, long long nchunk, int C) {
+    const float* __restrict__ red, const float* __restrict__ count, float count_h,
+    bf16_t* __restrict__ dy, bf16_t* __restrict__ dzm_out, long long nchunk, int C) {
   const int C8 = C >> 3;
   const long long start = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long step = (long long)gridDim.x * blockDim.x;
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(
 #pragma unroll
     for (int k = 0; k < 8; ++k) cb[k] = cc[k] = 0.f;
   } else {
-    const float inv_cnt = 1.f / count[0];
+    const float inv_cnt = 1.f / (count ? count[0] : count_h);
     float mean[8], inv[8], g[8], r0[8], r1[8];
     load8f(params + c0, mean);
     load8f(params + C + c0, inv);
@@ -203,32 +203,86 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(
   }
 }
 
-// out[0:2Ca] = sum_slots a[slot][2][Ca]; out[2Ca:2Ca+2Cb] = same for b; out[last] = count
-__global__ void stats_collapse_kernel(const float* __restrict__ a, int Ca, const float* __restrict__ b,
-                                      int Cb, float count, float* __restrict__ out, int with_count) {
+// out[0:2Ca] = sum_slots a[slot][2][Ca]; out[2Ca:2Ca+2Cb] = same for b; out[last] = count.
+// clear: zero the slot buffers after reading (they return to the host-side pool
+// ready for the next conv epilogue / reduce -- no memset launch).
+// acc_a/acc_b: optional [2][C] fp32 gradient targets (d_beta | d_gamma rows)
+// that receive += the collapsed local sums (direct-to-arena BN param grads).
+__global__ void stats_collapse_kernel(float* __restrict__ a, int Ca, float* __restrict__ b, int Cb,
+                                      float count, float* __restrict__ out, int with_count, int clear,
+                                      float* __restrict__ acc_a0, float* __restrict__ acc_a1,
+                                      float* __restrict__ acc_b0, float* __restrict__ acc_b1) {
   const int na = 2 * Ca, nb = b ? 2 * Cb : 0;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < na) {
+  if (i < na + nb) {
+    float* src = i < na ? a + i : b + (i - na);
+    const int n = i < na ? na : nb;
     float s = 0.f;
 #pragma unroll 8
-    for (int k = 0; k < kStatSlots; ++k) s += a[(size_t)k * na + i];
-    out[i] = s;
-  } else if (i < na + nb) {
-    const int j = i - na;
-    float s = 0.f;
+    for (int k = 0; k < kStatSlots; ++k) s += src[(size_t)k * n];
+    if (clear) {
 #pragma unroll 8
-    for (int k = 0; k < kStatSlots; ++k) s += b[(size_t)k * nb + j];
+      for (int k = 0; k < kStatSlots; ++k) src[(size_t)k * n] = 0.f;
+    }
     out[i] = s;
+    const int j = i < na ? i : i - na;
+    const int C = i < na ? Ca : Cb;
+    float* acc = i < na ? (j < C ? acc_a0 : acc_a1) : (j < C ? acc_b0 : acc_b1);
+    if (acc) acc[j < C ? j : j - C] += s;
   } else if (with_count && i == na + nb) {
     out[i] = count;
   }
 }
 
-int stats_collapse_launch(const float* a, int Ca, const float* b, int Cb, float count, float* out,
-                          bool with_count, hipStream_t st) {
+int stats_collapse_launch(float* a, int Ca, float* b, int Cb, float count, float* out,
+                          bool with_count, bool clear, float* acc_a0, float* acc_a1, float* acc_b0,
+                          float* acc_b1, hipStream_t st) {
   const int n = 2 * Ca + (b ? 2 * Cb : 0) + (with_count ? 1 : 0);
   hipLaunchKernelGGL(stats_collapse_kernel, dim3((n + 255) / 256), dim3(256), 0, st, a, Ca, b, Cb,
-                     count, out, with_count ? 1 : 0);
+                     count, out, with_count ? 1 : 0, clear ? 1 : 0, acc_a0, acc_a1, acc_b0, acc_b1);
+  return 0;
+}
+
+// Single-replica BN statistics: collapse (and clear) the slots and finalize
+// in one launch -- used when there is no SyncBN all-reduce between the two.
+__global__ void stats_finalize_local_kernel(float* __restrict__ slots, float count,
+                                            const float* __restrict__ gamma,
+                                            const float* __restrict__ beta, float* __restrict__ params,
+                                            float* running_mean, float* running_var, long long* nbt,
+                                            int C, float eps, float momentum) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C) {
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < kStatSlots; ++k) {
+      float* p = slots + (size_t)k * 2 * C;
+      s1 += p[c];
+      s2 += p[C + c];
+      p[c] = 0.f;
+      p[C + c] = 0.f;
+    }
+    const float mean = s1 / count;
+    const float var = fmaxf(s2 / count - mean * mean, 0.f);
+    const float invstd = rsqrtf(var + eps);
+    const float sc = gamma[c] * invstd;
+    params[c] = mean;
+    params[C + c] = invstd;
+    params[2 * C + c] = sc;
+    params[3 * C + c] = beta[c] - mean * sc;
+    if (running_mean) {
+      const float unb = var * (count / fmaxf(count - 1.f, 1.f));
+      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+      running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+    }
+  }
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
+}
+
+int stats_finalize_local_launch(float* slots, float count, const float* gamma, const float* beta,
+                                float* params, float* rm, float* rv, long long* nbt, int C, float eps,
+                                float momentum, hipStream_t st) {
+  hipLaunchKernelGGL(stats_finalize_local_kernel, dim3((C + 255) / 256), dim3(256), 0, st, slots, count,
+                     gamma, beta, params, rm, rv, nbt, C, eps, momentum);
   return 0;
 }
 
@@ -282,14 +336,15 @@ int bn_bwd_reduce_launch(const bf16_t* dout, const bf16_t* out, const bf16_t* y,
 }
 
 int bn_bwd_elemt_launch(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const float* params,
-                        const float* gamma, const float* red, const float* count, bf16_t* dy,
-                        bf16_t* dzm, long long M, int C, bool relu, bool eval_mode, hipStream_t st) {
+                        const float* gamma, const float* red, const float* count, float count_h,
+                        bf16_t* dy, bf16_t* dzm, long long M, int C, bool relu, bool eval_mode,
+                        hipStream_t st) {
   if (C % 8 || (C >> 3) > 256 || ((C >> 3) & ((C >> 3) - 1))) return 1;
   const long long nchunk = M * (C / 8);
   const int g = ew_grid(nchunk, C / 8);
 #define EL(RL, DZ, EV)                                                                            \
   hipLaunchKernelGGL((bn_bwd_elemt_kernel<RL, DZ, EV>), dim3(g), dim3(256), 0, st, dout, out, y, \
-                     params, gamma, red, count, dy, dzm, nchunk, C)
+                     params, gamma, red, count, count_h, dy, dzm, nchunk, C)
   const bool dz = dzm != nullptr;
   if (eval_mode) {
     if (relu) { if (dz) EL(true, true, true); else EL(true, false, true); }

@@ -30,7 +30,8 @@ struct ConvArgs {
   const bf16_t* src;  // gathered operand, NHWC [N, H, W, Cs]
   const bf16_t* wt;   // B^T image [Nout][Kg]
   bf16_t* out;        // [M][Nout]
-  float* stats;       // [2][Nout] or nullptr
+  float* stats;       // [kStatSlots][2][Nout] or nullptr
+  const bf16_t* addend;  // optional [M][Nout] tensor added to the output (grad accumulation)
   int N, H, W, Cs, log2Cs;
   int OH, OW;
   int Nout, R, S, stride, log2stride, pad;
@@ -271,8 +272,16 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
         const int hh = rem / OWp, ww = rem - hh * OWp;
         orow = ((size_t)nb * a.OH + 2 * hh + ph) * a.OW + 2 * ww + pw;
       }
-      *reinterpret_cast<uint4*>(a.out + orow * a.Nout + n) =
-          *reinterpret_cast<const uint4*>(Cs + row * LDC + cc * 8);
+      uint4 v = *reinterpret_cast<const uint4*>(Cs + row * LDC + cc * 8);
+      if (a.addend) {
+        float f[8], g[8];
+        unpack8(v, f);
+        unpack8(*reinterpret_cast<const uint4*>(a.addend + orow * a.Nout + n), g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] += g[e];
+        v = pack8(f);
+      }
+      *reinterpret_cast<uint4*>(a.out + orow * a.Nout + n) = v;
     }
   }
 }
@@ -321,7 +330,7 @@ static void launch_sel(const ConvArgs& a, hipStream_t st) {
 // Returns 0 on success, nonzero on unsupported shape.
 int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* stats, int N, int H,
                       int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
-                      bool dgrad, hipStream_t st) {
+                      bool dgrad, const bf16_t* addend, hipStream_t st) {
   if (Cs % 8 != 0 || (Cs & (Cs - 1)) != 0) return 1;  // power-of-two channels (>= 8)
   if (Nout % 8 != 0) return 2;
   if (stride != 1 && stride != 2) return 3;
@@ -330,6 +339,7 @@ int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* s
   a.wt = wt;
   a.out = out;
   a.stats = stats;
+  a.addend = addend;
   a.N = N;
   a.H = H;
   a.W = W;

@@ -8,7 +8,7 @@ typedef unsigned short bf16_t;
 
 int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* stats, int N, int H,
                       int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
-                      bool dgrad, hipStream_t st);
+                      bool dgrad, const bf16_t* addend, hipStream_t st);
 void conv_weight_prep_launch(const float* w, bf16_t* wk, bf16_t* wkt, int K, int RS, int C, int Cp,
                              hipStream_t st);
 int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, int N, int H, int W, int C, int P,
@@ -17,15 +17,20 @@ int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, int N, int H
 int bn_finalize_launch(const float* sums, const float* count, const float* gamma, const float* beta,
                        float* params, float* rm, float* rv, long long* nbt, int C, float eps,
                        float momentum, bool eval_mode, hipStream_t st);
-int stats_collapse_launch(const float* a, int Ca, const float* b, int Cb, float count, float* out,
-                          bool with_count, hipStream_t st);
+int stats_collapse_launch(float* a, int Ca, float* b, int Cb, float count, float* out,
+                          bool with_count, bool clear, float* acc_a0, float* acc_a1, float* acc_b0,
+                          float* acc_b1, hipStream_t st);
+int stats_finalize_local_launch(float* slots, float count, const float* gamma, const float* beta,
+                                float* params, float* rm, float* rv, long long* nbt, int C, float eps,
+                                float momentum, hipStream_t st);
 int bn_apply_launch(const bf16_t* y1, const float* p1, const bf16_t* r, const float* p2, bf16_t* out,
                     long long M, int C, int mode, bool relu, hipStream_t st);
 int bn_bwd_reduce_launch(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const float* params,
                          float* red, int M, int C, bool relu, hipStream_t st);
 int bn_bwd_elemt_launch(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const float* params,
-                        const float* gamma, const float* red, const float* count, bf16_t* dy,
-                        bf16_t* dzm, long long M, int C, bool relu, bool eval_mode, hipStream_t st);
+                        const float* gamma, const float* red, const float* count, float count_h,
+                        bf16_t* dy, bf16_t* dzm, long long M, int C, bool relu, bool eval_mode,
+                        hipStream_t st);
 
 int maxpool_fwd_launch(const bf16_t* x, bf16_t* out, uint8_t* arg, int N, int H, int W, int C, int P,
                        int Q, hipStream_t st);

@@ -115,13 +115,9 @@ class BasicBlock(nn.Module):
             out = self.bn2(self.conv2(out))
             out = out + self.shortcut(x)
             return F.relu(out)
-        o = OF.conv_bn_act(x, self.conv1, self.bn1, relu=True)
-        y2, s2 = OF.conv(o, self.conv2)
-        if len(self.shortcut) == 0:
-            return OF.bn_add_act(y2, s2, self.bn2, residual=x, relu=True)
-        ysc, ssc = OF.conv(x, self.shortcut[0])
-        return OF.bn_add_act(y2, s2, self.bn2, res_y=ysc, res_stats=ssc,
-                             res_bn=self.shortcut[1], relu=True)
+        sc = (self.shortcut[0], self.shortcut[1]) if len(self.shortcut) else None
+        return OF.residual_block(x, [(self.conv1, self.bn1)], (self.conv2, self.bn2), sc,
+                                 self.bn1.training)
 
 
 class Bottleneck(nn.Module):
@@ -153,14 +149,9 @@ class Bottleneck(nn.Module):
             out = self.bn3(self.conv3(out))
             out = out + self.shortcut(x)
             return F.relu(out)
-        o = OF.conv_bn_act(x, self.conv1, self.bn1, relu=True)
-        o = OF.conv_bn_act(o, self.conv2, self.bn2, relu=True)
-        y3, s3 = OF.conv(o, self.conv3)
-        if len(self.shortcut) == 0:
-            return OF.bn_add_act(y3, s3, self.bn3, residual=x, relu=True)
-        ysc, ssc = OF.conv(x, self.shortcut[0])
-        return OF.bn_add_act(y3, s3, self.bn3, res_y=ysc, res_stats=ssc,
-                             res_bn=self.shortcut[1], relu=True)
+        sc = (self.shortcut[0], self.shortcut[1]) if len(self.shortcut) else None
+        return OF.residual_block(x, [(self.conv1, self.bn1), (self.conv2, self.bn2)],
+                                 (self.conv3, self.bn3), sc, self.bn1.training)
 
 
 class ResNet(nn.Module):

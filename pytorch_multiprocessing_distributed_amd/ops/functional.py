@@ -2,23 +2,35 @@
 
 Every op is a ``torch.autograd.Function`` whose forward/backward are written
 in terms of *primitives* (:mod:`.torch_prims` on CPU, :mod:`.hip_prims` =
-hand-written gfx950 kernels on an MI355X).  The op graph is what the
-reference gets from ``nn.Conv2d`` + ``nn.SyncBatchNorm`` + ``F.relu`` +
-in-place residual add (reference model/resnet.py:35-39, 65-70; main.py:43),
-re-cut so that memory-bound work is fused:
+hand-written gfx950 kernels on an MI355X).  The graph is what the reference
+gets from ``nn.Conv2d`` + ``nn.SyncBatchNorm`` + ``F.relu`` + the in-place
+residual add (reference model/resnet.py:35-39, 65-70; main.py:43), re-cut so
+memory-bound work is fused and every residual block is ONE autograd node:
 
-  conv            -> implicit-GEMM conv whose epilogue also emits the
-                     per-channel (sum, sum^2) BN statistics
-  bn_add_act      -> [SyncBN all-reduce of the statistics] -> finalize
-                     (+ running-stat update) -> one elementwise pass that
-                     normalises, adds the (optionally BN'd) residual and ReLUs
-  backward        -> one reduce pass (sum dz, sum dz*xhat) -> [SyncBN
-                     all-reduce] -> one elementwise pass
+forward, per conv->BN(->ReLU) stage
+  conv        implicit-GEMM conv; its epilogue also accumulates per-channel
+              (sum, sum^2) BN statistics
+  stats       SyncBN: one all-reduce of [sum | sum^2 | count] per BN site (the
+              two BNs of a projection block share one); single replica: a
+              single collapse+finalize kernel
+  apply       one elementwise pass: normalise, add the (BN'd) shortcut, ReLU
+backward, per stage
+  reduce      one pass: sum(dz*mask), sum(dz*mask*xhat) -> [all-reduce] ->
+              gamma/beta grads written straight into the reducer's arena
+  elemt       one pass -> dy
+  dgrad       implicit-GEMM; the block's input gradient from the residual /
+              projection path is added in the epilogue (no separate add pass)
+  wgrad       split-K MFMA kernel accumulating straight into the arena view
+              of ``weight.grad``
+
+Gradients of parameters that live in the flat arena (:mod:`..parallel.flat`)
+are written in place and the data-parallel reducer is notified directly
+(``param._pmd_ready``), so AccumulateGrad never runs for them.
 
 SyncBN semantics follow torch.nn.SyncBatchNorm (torch:nn/modules/
 _functions.py:39-207): global statistics in forward, globally reduced
-``sum_dy``/``sum_dy_xmu`` in backward, *local* gamma/beta gradients (DDP
-averages them).  Unlike torch there is no device->host sync.
+``sum_dy``/``sum_dy_xmu`` in backward, *local* gamma/beta gradients (the
+reducer averages them).  Unlike torch there is no device->host sync (B13).
 """
 from __future__ import annotations
 
@@ -61,6 +73,117 @@ def _empty(dev):
     return e
 
 
+# ------------------------------------------------------------- grad routing
+def _grad_target(p):
+    """Arena view to accumulate ``p``'s gradient into directly, or None."""
+    if p is not None and p.requires_grad and getattr(p, "_pmd_direct", False) and p.grad is not None:
+        return p.grad
+    return None
+
+
+def _ready(*ps):
+    for p in ps:
+        h = getattr(p, "_pmd_ready", None)
+        if h is not None:
+            h(p)
+
+
+def _wgrad(P, dy, x, wpack, stride, pad, w):
+    """Weight gradient: accumulated into the arena (returns None) or returned."""
+    if not w.requires_grad:
+        return None
+    cx = wpack[0].shape[-1]
+    tgt = _grad_target(w)
+    if tgt is not None and cx == w.shape[1]:
+        P.conv_wgrad(dy, x, tuple(wpack[0].shape), stride, pad, out=tgt.permute(0, 2, 3, 1))
+        _ready(w)
+        return None
+    dwk = P.conv_wgrad(dy, x, tuple(wpack[0].shape), stride, pad)   # fp32 [K,R,S,Cx]
+    if cx != w.shape[1]:
+        dwk = dwk[..., : w.shape[1]].contiguous()
+    return dwk.permute(0, 3, 1, 2)                                   # [K,C,R,S] channels_last
+
+
+def _bn_acc(bn):
+    """(d_beta, d_gamma) arena targets for a BN module, or None."""
+    tb, tg = _grad_target(bn.bias), _grad_target(bn.weight)
+    if tb is None or tg is None:
+        return None
+    return (tb, tg)
+
+
+# ---------------------------------------------------------------- BN pieces
+def _bn_forward_params(P, y, st, bn, training, sync, y2=None, st2=None, bn2=None):
+    """-> (p1, p2, count); count is a host float (local) or device scalar (SyncBN)."""
+    if not training:
+        p1 = P.bn_eval_params(bn.running_mean, bn.running_var, bn.weight, bn.bias, bn.eps)
+        p2 = None
+        if bn2 is not None:
+            p2 = P.bn_eval_params(bn2.running_mean, bn2.running_var, bn2.weight, bn2.bias, bn2.eps)
+        return p1, p2, None
+    c1 = y.shape[-1]
+    m_local = y.numel() // c1
+    if sync is None:
+        p1 = P.stats_finalize_local(st, float(m_local), bn.weight, bn.bias, bn.eps,
+                                    bn.running_mean, bn.running_var, bn.momentum,
+                                    bn.num_batches_tracked)
+        p2 = None
+        if bn2 is not None:
+            p2 = P.stats_finalize_local(st2, float(m_local), bn2.weight, bn2.bias, bn2.eps,
+                                        bn2.running_mean, bn2.running_var, bn2.momentum,
+                                        bn2.num_batches_tracked)
+        return p1, p2, float(m_local)
+    buf = P.stats_collapse(st, st2, float(m_local))
+    sync.all_reduce_(buf)
+    count = buf[-1:]
+    p1 = P.bn_finalize(buf[: 2 * c1].view(2, c1), count, bn.weight, bn.bias, bn.eps,
+                       bn.running_mean, bn.running_var, bn.momentum, bn.num_batches_tracked)
+    p2 = None
+    if bn2 is not None:
+        c2 = y2.shape[-1]
+        p2 = P.bn_finalize(buf[2 * c1: 2 * c1 + 2 * c2].view(2, c2), count, bn2.weight, bn2.bias,
+                           bn2.eps, bn2.running_mean, bn2.running_var, bn2.momentum,
+                           bn2.num_batches_tracked)
+    return p1, p2, count
+
+
+def _bn_backward(P, dout, out, relu, training, sync, count, y1, p1, bn1, y2=None, p2=None,
+                 bn2=None, want_dzm=False):
+    """BN(+second BN)(+ReLU) backward. Returns (dy1, dy2, dzm, grads) with
+    grads = [d_g1, d_b1, d_g2, d_b2] for params that were NOT written directly."""
+    r1 = P.bn_bwd_reduce(dout, out, y1, p1, relu)
+    r2 = P.bn_bwd_reduce(dout, out, y2, p2, relu) if y2 is not None else None
+    acc1 = _bn_acc(bn1)
+    acc2 = _bn_acc(bn2) if bn2 is not None else None
+    red = P.stats_collapse(r1, r2, None, acc1, acc2)     # local sums; gamma/beta grads += local
+    c1 = y1.shape[-1]
+    grads = [None, None, None, None]
+    if acc1 is None:
+        grads[0], grads[1] = red[c1:2 * c1], red[:c1]
+    else:
+        _ready(bn1.bias, bn1.weight)
+    if y2 is not None:
+        c2 = y2.shape[-1]
+        if acc2 is None:
+            grads[2], grads[3] = red[2 * c1 + c2:], red[2 * c1:2 * c1 + c2]
+        else:
+            _ready(bn2.bias, bn2.weight)
+    if training:
+        if sync is not None:
+            red = red.clone()
+            sync.all_reduce_(red)
+        dy1, dzm = P.bn_bwd_elemt(dout, out, y1, p1, bn1.weight, red[:2 * c1].view(2, c1), count,
+                                  relu, want_dzm=want_dzm)
+        dy2 = None
+        if y2 is not None:
+            dy2, _ = P.bn_bwd_elemt(dout, out, y2, p2, bn2.weight, red[2 * c1:].view(2, -1), count,
+                                    relu)
+    else:
+        dy1, dzm = P.bn_bwd_elemt_eval(dout, out, p1, relu, want_dzm=want_dzm)
+        dy2 = P.bn_bwd_elemt_eval(dout, out, p2, relu)[0] if y2 is not None else None
+    return dy1, dy2, dzm, grads
+
+
 # ---------------------------------------------------------------------- conv
 class _ConvFn(torch.autograd.Function):
     @staticmethod
@@ -69,7 +192,7 @@ class _ConvFn(torch.autograd.Function):
         wpack = P.conv_weight(w, x.dtype, x.shape[-1], x.requires_grad)
         y, stats = P.conv_fwd(x, wpack, stride, pad, want_stats)
         ctx.save_for_backward(x, *wpack)
-        ctx.conf = (stride, pad, tuple(w.shape))
+        ctx.conf = (stride, pad, w)
         if stats is None:
             stats = _empty(x.device)
         ctx.mark_non_differentiable(stats)
@@ -78,25 +201,21 @@ class _ConvFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dstats):
         x, *wpack = ctx.saved_tensors
-        stride, pad, wshape = ctx.conf
+        stride, pad, w = ctx.conf
         P = prims_for(x)
         dy = dy.contiguous()
-        dx = dw = None
+        dx = None
         if ctx.needs_input_grad[0]:
             dx = P.conv_dgrad(dy, wpack, tuple(x.shape), stride, pad)
-        if ctx.needs_input_grad[1]:
-            dwk = P.conv_wgrad(dy, x, tuple(wpack[0].shape), stride, pad)   # fp32 [K,R,S,Cx]
-            c = wshape[1]
-            if dwk.shape[-1] != c:
-                dwk = dwk[..., :c].contiguous()
-            dw = dwk.permute(0, 3, 1, 2)          # [K,C,R,S], channels_last strides
+        dw = _wgrad(P, dy, x, wpack, stride, pad, w) if ctx.needs_input_grad[1] else None
         return dx, dw, None, None, None
 
 
 def conv(x, conv_mod, want_stats=None):
-    """Returns ``(y, stats)``; ``stats`` = fp32 [2, K] (sum, sum^2) of y."""
+    """Returns ``(y, stats)``; ``stats`` = per-channel (sum, sum^2) of y in the
+    backend's layout (consumed by :func:`bn_add_act`)."""
     if want_stats is None:
-        want_stats = torch.is_grad_enabled() or conv_mod.training
+        want_stats = conv_mod.training
     return _ConvFn.apply(x, conv_mod.weight, conv_mod.stride, conv_mod.padding, bool(want_stats))
 
 
@@ -109,81 +228,28 @@ class _BNActFn(torch.autograd.Function):
         bn1, bn2, relu, training = cfg
         P = prims_for(y1)
         sync = _state["bn_sync"] if training else None
-        c1 = y1.shape[-1]
-        m_local = y1.numel() // c1
         two = y2 is not None
-        if training:
-            # local (sum, sum^2) of both branches + element count in ONE buffer
-            # -> one all-reduce per BN site (both BNs of a projection block share it)
-            buf = P.stats_collapse(s1, s2 if two else None, float(m_local))
-            if sync is not None:
-                sync.all_reduce_(buf)
-            count = buf[-1:]
-            gs1 = buf[: 2 * c1].view(2, c1)
-            p1 = P.bn_finalize(gs1, count, g1, b1, bn1.eps, bn1.running_mean, bn1.running_var,
-                               bn1.momentum, bn1.num_batches_tracked)
-            if two:
-                c2 = y2.shape[-1]
-                gs2 = buf[2 * c1: 2 * c1 + 2 * c2].view(2, c2)
-                p2 = P.bn_finalize(gs2, count, g2, b2, bn2.eps, bn2.running_mean,
-                                   bn2.running_var, bn2.momentum, bn2.num_batches_tracked)
-        else:
-            count = None
-            p1 = P.bn_eval_params(bn1.running_mean, bn1.running_var, g1, b1, bn1.eps)
-            if two:
-                p2 = P.bn_eval_params(bn2.running_mean, bn2.running_var, g2, b2, bn2.eps)
-        out = P.bn_apply(y1, p1, res, y2, p2 if two else None, relu)
-        ctx.cfg = (relu, training, two, res is not None, sync)
-        saved = [y1, out, p1, g1]
-        if two:
-            saved += [y2, p2, g2]
-        if count is not None:
-            saved.append(count)
-        ctx.save_for_backward(*saved)
+        p1, p2, count = _bn_forward_params(P, y1, s1, bn1, training, sync, y2, s2,
+                                           bn2 if two else None)
+        out = P.bn_apply(y1, p1, res, y2, p2, relu)
+        ctx.cfg = (bn1, bn2 if two else None, relu, training, res is not None, sync, count)
+        ctx.save_for_backward(y1, out, p1, *([y2, p2] if two else []))
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        relu, training, two, has_res, sync = ctx.cfg
-        sv = list(ctx.saved_tensors)
-        y1, out, p1, g1 = sv[:4]
-        if two:
-            y2, p2, g2 = sv[4:7]
-        count = sv[-1] if training else None
+        bn1, bn2, relu, training, has_res, sync, count = ctx.cfg
+        sv = ctx.saved_tensors
+        y1, out, p1 = sv[:3]
+        y2, p2 = (sv[3], sv[4]) if bn2 is not None else (None, None)
         P = prims_for(y1)
-        dout = dout.contiguous()
-        d_y1 = d_g1 = d_b1 = d_res = d_y2 = d_g2 = d_b2 = None
-        r1 = P.bn_bwd_reduce(dout, out, y1, p1, relu)
-        r2 = P.bn_bwd_reduce(dout, out, y2, p2, relu) if two else None
-        red = P.stats_collapse(r1, r2, None)            # flat [2C1 (+2C2)], local sums
-        c1 = y1.shape[-1]
-        # gamma/beta grads use the LOCAL sums (DDP averages them), like torch SyncBN
-        d_b1, d_g1 = red[:c1], red[c1:2 * c1]
-        if two:
-            c2 = y2.shape[-1]
-            d_b2, d_g2 = red[2 * c1:2 * c1 + c2], red[2 * c1 + c2:]
-        if training:
-            if sync is not None:
-                red = red.clone()
-                sync.all_reduce_(red)
-            red1 = red[:2 * c1].view(2, c1)
-            red2 = red[2 * c1:].view(2, -1) if two else None
-            d_y1, dzm = P.bn_bwd_elemt(dout, out, y1, p1, g1, red1, count, relu,
-                                       want_dzm=has_res)
-            if two:
-                d_y2, _ = P.bn_bwd_elemt(dout, out, y2, p2, g2, red2, count, relu)
-        else:
-            d_y1, dzm = P.bn_bwd_elemt_eval(dout, out, p1, relu, want_dzm=has_res)
-            if two:
-                d_y2, _ = P.bn_bwd_elemt_eval(dout, out, p2, relu)
-        if has_res:
-            d_res = dzm
-        return None, d_y1, None, d_g1, d_b1, d_res, d_y2, None, d_g2, d_b2
+        dy1, dy2, dzm, g = _bn_backward(P, dout.contiguous(), out, relu, training, sync, count,
+                                        y1, p1, bn1, y2, p2, bn2, want_dzm=has_res)
+        return None, dy1, None, g[0], g[1], (dzm if has_res else None), dy2, None, g[2], g[3]
 
 
 def bn_add_act(y, stats, bn, residual=None, res_y=None, res_stats=None, res_bn=None, relu=True):
-    training = bn.training
-    cfg = (bn, res_bn, relu, training)
+    cfg = (bn, res_bn, relu, bn.training)
     if res_y is not None:
         return _BNActFn.apply(cfg, y, stats, bn.weight, bn.bias, None,
                               res_y, res_stats, res_bn.weight, res_bn.bias)
@@ -193,6 +259,131 @@ def bn_add_act(y, stats, bn, residual=None, res_y=None, res_stats=None, res_bn=N
 def conv_bn_act(x, conv_mod, bn, relu=True):
     y, s = conv(x, conv_mod, want_stats=bn.training)
     return bn_add_act(y, s, bn, relu=relu)
+
+
+# ------------------------------------------------------------ residual block
+class _ResidualBlockFn(torch.autograd.Function):
+    """A whole ResNet block as one autograd node.
+
+    stages   : [(conv, bn)]*  conv -> BN -> ReLU  (Bottleneck: 1x1, 3x3; Basic: 3x3)
+    final    : (conv, bn)     conv -> BN, then + shortcut, ReLU
+    shortcut : None (identity) or (conv, bn) projection on the block input
+    """
+
+    @staticmethod
+    def forward(ctx, cfg, x, *params):
+        stages, final, shortcut, training = cfg
+        P = prims_for(x)
+        sync = _state["bn_sync"] if training else None
+        h = x
+        recs = []
+        for conv_m, bn in stages:
+            wp = P.conv_weight(conv_m.weight, x.dtype, h.shape[-1], True)
+            y, st = P.conv_fwd(h, wp, conv_m.stride, conv_m.padding, training)
+            p, _, count = _bn_forward_params(P, y, st, bn, training, sync)
+            z = P.bn_apply(y, p, relu=True)
+            recs.append((h, wp, y, p, z, count))
+            h = z
+        fconv, fbn = final
+        wpf = P.conv_weight(fconv.weight, x.dtype, h.shape[-1], True)
+        yf, stf = P.conv_fwd(h, wpf, fconv.stride, fconv.padding, training)
+        if shortcut is not None:
+            sconv, sbn = shortcut
+            wps = P.conv_weight(sconv.weight, x.dtype, x.shape[-1], x.requires_grad)
+            ys, sts = P.conv_fwd(x, wps, sconv.stride, sconv.padding, training)
+            pf, ps, countf = _bn_forward_params(P, yf, stf, fbn, training, sync, ys, sts, sbn)
+            out = P.bn_apply(yf, pf, None, ys, ps, relu=True)
+        else:
+            wps = None
+            pf, _, countf = _bn_forward_params(P, yf, stf, fbn, training, sync)
+            out = P.bn_apply(yf, pf, x, relu=True)
+        ctx.cfg = (cfg, sync, [r[5] for r in recs], countf, len(wpf),
+                   0 if wps is None else len(wps), [len(r[1]) for r in recs])
+        flat = [x, out, yf, pf, h, *wpf]
+        for (hin, wp, y, p, z, _) in recs:
+            flat += [hin, y, p, z, *wp]
+        if shortcut is not None:
+            flat += [ys, ps, *wps]
+        ctx.save_for_backward(*flat)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        cfg, sync, counts, countf, nwf, nws, nwst = ctx.cfg
+        stages, final, shortcut, training = cfg
+        nst = len(stages)
+        sv = list(ctx.saved_tensors)
+        x, out, yf, pf, hlast = sv[:5]
+        i = 5
+        wpf = tuple(sv[i:i + nwf])
+        i += nwf
+        recs = []
+        for k in range(nst):
+            hin, y, p, z = sv[i:i + 4]
+            i += 4
+            recs.append((hin, tuple(sv[i:i + nwst[k]]), y, p, z))
+            i += nwst[k]
+        P = prims_for(x)
+        dout = dout.contiguous()
+        fconv, fbn = final
+        grads = {}
+
+        def put(p, g):
+            if g is not None:
+                grads[id(p)] = g
+
+        # --- final BN (+ projection BN) and the residual ReLU
+        if shortcut is not None:
+            sconv, sbn = shortcut
+            ys, ps = sv[i], sv[i + 1]
+            wps = tuple(sv[i + 2:i + 2 + nws])
+            dyf, dys, _, g = _bn_backward(P, dout, out, True, training, sync, countf,
+                                          yf, pf, fbn, ys, ps, sbn)
+            put(sbn.weight, g[2])
+            put(sbn.bias, g[3])
+            dres = None
+        else:
+            dyf, _, dres, g = _bn_backward(P, dout, out, True, training, sync, countf,
+                                           yf, pf, fbn, want_dzm=True)
+        put(fbn.weight, g[0])
+        put(fbn.bias, g[1])
+        # --- final conv
+        dh = P.conv_dgrad(dyf, wpf, tuple(hlast.shape), fconv.stride, fconv.padding)
+        put(fconv.weight, _wgrad(P, dyf, hlast, wpf, fconv.stride, fconv.padding, fconv.weight))
+        dx = None
+        # --- conv->BN->ReLU stages in reverse; the block-input gradient of the
+        #     residual/projection path is added in the first stage's dgrad epilogue
+        for k in range(nst - 1, -1, -1):
+            conv_m, bn = stages[k]
+            hin, wp, y, p, z = recs[k]
+            dy, _, _, g = _bn_backward(P, dh, z, True, training, sync, counts[k], y, p, bn)
+            put(bn.weight, g[0])
+            put(bn.bias, g[1])
+            if k > 0:
+                dh = P.conv_dgrad(dy, wp, tuple(hin.shape), conv_m.stride, conv_m.padding)
+            elif ctx.needs_input_grad[1]:
+                addend = dres
+                if shortcut is not None:
+                    addend = P.conv_dgrad(dys, wps, tuple(x.shape), sconv.stride, sconv.padding)
+                dx = P.conv_dgrad(dy, wp, tuple(x.shape), conv_m.stride, conv_m.padding, addend)
+            put(conv_m.weight, _wgrad(P, dy, hin, wp, conv_m.stride, conv_m.padding,
+                                      conv_m.weight))
+        if shortcut is not None:
+            put(sconv.weight, _wgrad(P, dys, x, wps, sconv.stride, sconv.padding, sconv.weight))
+        return (None, dx, *[grads.get(id(p)) for p in _block_params(stages, final, shortcut)])
+
+
+def _block_params(stages, final, shortcut):
+    ps = []
+    for conv_m, bn in [*stages, final] + ([shortcut] if shortcut is not None else []):
+        ps += [conv_m.weight, bn.weight, bn.bias]
+    return ps
+
+
+def residual_block(x, stages, final, shortcut, training):
+    """Run a ResNet block (see :class:`_ResidualBlockFn`) as one autograd node."""
+    cfg = (tuple(stages), final, shortcut, training)
+    return _ResidualBlockFn.apply(cfg, x, *_block_params(stages, final, shortcut))
 
 
 # --------------------------------------------------------------------- pools
@@ -220,7 +411,6 @@ class _AvgPoolFn(torch.autograd.Function):
     def forward(ctx, x):
         ctx.xshape = tuple(x.shape)
         ctx.dtype = x.dtype
-        ctx.is_cuda = x.is_cuda
         return prims_for(x).avgpool_fwd(x)
 
     @staticmethod
@@ -229,7 +419,7 @@ class _AvgPoolFn(torch.autograd.Function):
 
 
 def global_avg_pool(x):
-    """[N,H,W,C] -> [N,C] fp32."""
+    """[N,H,W,C] -> [N,C] (fp32 accumulation)."""
     return _AvgPoolFn.apply(x)
 
 
@@ -250,7 +440,7 @@ class _XentFn(torch.autograd.Function):
     def backward(ctx, gloss):
         logits, target, lse = ctx.saved_tensors
         P = prims_for(logits)
-        return P.xent_bwd(gloss.reshape(1).float(), logits, target, lse), None
+        return P.xent_bwd(gloss.reshape(1).to(logits.dtype), logits, target, lse), None
 
 
 def cross_entropy(logits, target):

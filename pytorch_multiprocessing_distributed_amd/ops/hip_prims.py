@@ -3,12 +3,35 @@
 Same contracts as :mod:`.torch_prims` (NHWC bf16 activations, fp32
 statistics, BN params packed [4, C]).  There is deliberately no fallback:
 importing this module on a GPU box without the built extension raises.
+
+Statistics buffers: conv epilogues and BN-backward reductions accumulate into
+``[kStatSlots=64, 2, C]`` fp32 slot buffers (spreads atomics).  They come
+from a small per-(device, C) pool of *already zeroed* buffers; the collapse
+kernels read-and-clear them, after which they go back to the pool -- so the
+hot loop issues no memset launches for statistics.  All of this is ordered by
+the current HIP stream.
 """
 from __future__ import annotations
 
 import torch
 
 from .native import C as _C
+
+SLOTS = 64
+_POOL: dict = {}
+
+
+def _acquire(c, dev):
+    lst = _POOL.get((dev, c))
+    if lst:
+        return lst.pop()
+    return torch.zeros(SLOTS, 2, c, dtype=torch.float32, device=dev)
+
+
+def _release(*bufs):
+    for b in bufs:
+        if b is not None:
+            _POOL.setdefault((b.device, b.shape[-1]), []).append(b)
 
 
 # --------------------------------------------------------------------- conv
@@ -19,18 +42,23 @@ def conv_weight(w, dtype, cin, want_t=True):
 
 
 def conv_fwd(x, wpack, stride, pad, want_stats):
-    r = _C.conv_fwd(x, wpack[0], int(stride), int(pad), bool(want_stats))
-    return (r[0], r[1]) if want_stats else (r[0], None)
+    if want_stats:
+        buf = _acquire(wpack[0].shape[0], x.device)
+        y, st = _C.conv_fwd(x, wpack[0], int(stride), int(pad), True, buf)
+        return y, st
+    return _C.conv_fwd(x, wpack[0], int(stride), int(pad), False, None)[0], None
 
 
-def conv_dgrad(dy, wpack, x_shape, stride, pad):
+def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None):
     if len(wpack) < 2:
         raise RuntimeError("dgrad image was not prepared (input did not require grad)")
-    return _C.conv_dgrad(dy, wpack[1], int(x_shape[1]), int(x_shape[2]), int(stride), int(pad))
+    return _C.conv_dgrad(dy, wpack[1], int(x_shape[1]), int(x_shape[2]), int(stride), int(pad),
+                         addend)
 
 
-def conv_wgrad(dy, x, wk_shape, stride, pad):
-    return _C.conv_wgrad(dy, x, int(wk_shape[1]), int(wk_shape[2]), int(stride), int(pad))
+def conv_wgrad(dy, x, wk_shape, stride, pad, out=None):
+    """fp32 [K,R,S,C]; with ``out`` the gradient is accumulated into it."""
+    return _C.conv_wgrad(dy, x, int(wk_shape[1]), int(wk_shape[2]), int(stride), int(pad), out)
 
 
 # ----------------------------------------------------------------------- BN
@@ -40,14 +68,29 @@ def bn_finalize(sums, count, gamma, beta, eps, running_mean=None, running_var=No
                           running_var, float(momentum), num_batches_tracked, False)
 
 
+def stats_finalize_local(slots, count, gamma, beta, eps, running_mean=None, running_var=None,
+                         momentum=0.1, num_batches_tracked=None):
+    p = _C.stats_finalize_local(slots, float(count), gamma.detach(), beta.detach(), float(eps),
+                                running_mean, running_var, float(momentum), num_batches_tracked)
+    _release(slots)
+    return p
+
+
 def bn_eval_params(running_mean, running_var, gamma, beta, eps):
     return _C.bn_finalize(None, None, gamma.detach(), beta.detach(), float(eps), running_mean,
                           running_var, 0.0, None, True)
 
 
-def stats_collapse(a, b=None, count=None):
-    """[S,2,Ca] (+[S,2,Cb]) slot statistics -> flat [2Ca (+2Cb) (+1 count)]."""
-    return _C.stats_collapse(a, b, None if count is None else float(count))
+def stats_collapse(a, b=None, count=None, acc_a=None, acc_b=None):
+    """[S,2,Ca] (+[S,2,Cb]) slot statistics -> flat [2Ca (+2Cb) (+1 count)];
+    the slot buffers are cleared and recycled.  ``acc_*`` = (d_beta, d_gamma)
+    fp32 targets that receive += the local sums."""
+    aa = acc_a or (None, None)
+    ab = acc_b or (None, None)
+    out = _C.stats_collapse(a, b, None if count is None else float(count), True,
+                            aa[0], aa[1], ab[0], ab[1])
+    _release(a, b)
+    return out
 
 
 def bn_apply(y1, p1, res=None, y2=None, p2=None, relu=True):
@@ -55,17 +98,22 @@ def bn_apply(y1, p1, res=None, y2=None, p2=None, relu=True):
 
 
 def bn_bwd_reduce(dout, out, y, p, relu):
-    return _C.bn_bwd_reduce(dout, out, y, p, bool(relu))
+    buf = _acquire(y.shape[-1], y.device)
+    return _C.bn_bwd_reduce(dout, out, y, p, bool(relu), buf)
 
 
 def bn_bwd_elemt(dout, out, y, p, gamma, red, count, relu, want_dzm=False):
-    r = _C.bn_bwd_elemt(dout, out, y, p, gamma.detach(), red, count, bool(relu), bool(want_dzm),
-                        False)
+    if torch.is_tensor(count):
+        r = _C.bn_bwd_elemt(dout, out, y, p, gamma.detach(), red, count, 0.0, bool(relu),
+                            bool(want_dzm), False)
+    else:
+        r = _C.bn_bwd_elemt(dout, out, y, p, gamma.detach(), red, None, float(count), bool(relu),
+                            bool(want_dzm), False)
     return (r[0], r[1]) if want_dzm else (r[0], None)
 
 
 def bn_bwd_elemt_eval(dout, out, p, relu, want_dzm=False):
-    r = _C.bn_bwd_elemt(dout, out, out, p, p[2], None, None, bool(relu), bool(want_dzm), True)
+    r = _C.bn_bwd_elemt(dout, out, out, p, p[2], None, None, 1.0, bool(relu), bool(want_dzm), True)
     return (r[0], r[1]) if want_dzm else (r[0], None)
 
 

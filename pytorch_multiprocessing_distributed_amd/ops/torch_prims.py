@@ -46,19 +46,27 @@ def conv_fwd(x, wpack, stride, pad, want_stats):
     return y, stats
 
 
-def conv_dgrad(dy, wpack, x_shape, stride, pad):
+def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None):
     wk = wpack[0]
     n, h, w, c = x_shape
     dx = torch.nn.grad.conv2d_input((n, c, h, w), _f(wk.permute(0, 3, 1, 2)),
                                     _f(_nchw(dy)), stride=stride, padding=pad)
-    return _nhwc(dx).to(dy.dtype)
+    dx = _nhwc(dx)
+    if addend is not None:
+        dx = dx + _f(addend)
+    return dx.to(dy.dtype)
 
 
-def conv_wgrad(dy, x, wk_shape, stride, pad):
+def conv_wgrad(dy, x, wk_shape, stride, pad, out=None):
+    """fp32 [K,R,S,C]; with ``out`` the gradient is accumulated into it."""
     k, r, s, c = wk_shape
     dw = torch.nn.grad.conv2d_weight(_f(_nchw(x)), (k, c, r, s), _f(_nchw(dy)),
                                      stride=stride, padding=pad)
-    return dw.permute(0, 2, 3, 1).contiguous()          # fp32 [K,R,S,C]
+    dw = dw.permute(0, 2, 3, 1)
+    if out is not None:
+        out.add_(dw.to(out.dtype))
+        return out
+    return dw.contiguous()          # fp32 [K,R,S,C]
 
 
 # ----------------------------------------------------------------------- BN
@@ -84,6 +92,13 @@ def bn_finalize(sums, count, gamma, beta, eps, running_mean=None, running_var=No
     return torch.stack([mean, invstd, scale, shift])
 
 
+def stats_finalize_local(stats, count, gamma, beta, eps, running_mean=None, running_var=None,
+                         momentum=0.1, num_batches_tracked=None):
+    cnt = torch.full((1,), float(count), dtype=stats.dtype, device=stats.device)
+    return bn_finalize(stats, cnt, gamma, beta, eps, running_mean, running_var, momentum,
+                       num_batches_tracked)
+
+
 def bn_eval_params(running_mean, running_var, gamma, beta, eps):
     mean = _f(running_mean)
     invstd = torch.rsqrt(_f(running_var) + eps)
@@ -92,8 +107,14 @@ def bn_eval_params(running_mean, running_var, gamma, beta, eps):
     return torch.stack([mean, invstd, scale, shift])
 
 
-def stats_collapse(a, b=None, count=None):
-    """Per-channel stat blocks -> one flat buffer [2Ca (+2Cb) (+1 count)]."""
+def stats_collapse(a, b=None, count=None, acc_a=None, acc_b=None):
+    """Per-channel stat blocks -> one flat buffer [2Ca (+2Cb) (+1 count)];
+    ``acc_*`` = (d_beta, d_gamma) targets that receive += the sums."""
+    for st, acc in ((a, acc_a), (b, acc_b)):
+        if acc is not None and st is not None:
+            for row, tgt in enumerate(acc):
+                if tgt is not None:
+                    tgt.add_(st[row].to(tgt.dtype))
     parts = [a.reshape(-1)]
     if b is not None:
         parts.append(b.reshape(-1))
@@ -131,7 +152,7 @@ def bn_bwd_reduce(dout, out, y, p, relu):
 def bn_bwd_elemt(dout, out, y, p, gamma, red, count, relu, want_dzm=False):
     d = _dzm(dout, out, relu)
     xhat = (_f(y) - p[0]) * p[1]
-    cnt = _f(count)
+    cnt = _f(count) if torch.is_tensor(count) else float(count)
     mdy = red[0] / cnt
     mdyx = red[1] / cnt
     dy = ((d - mdy - xhat * mdyx) * (_f(gamma.detach()) * p[1])).to(y.dtype)

@@ -68,10 +68,15 @@ class DataParallel(nn.Module):
             self._sync_module_states()
         self._sync_enabled = True
         self._callback_queued = False
+        self._marked = [False] * len(self.flat.params)
         self._hooks = []
         if comm is not None:
             for i, p in enumerate(self.flat.params):
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+                h = self._make_hook(i)
+                # AccumulateGrad path (params whose grad is returned to autograd) ...
+                self._hooks.append(p.register_post_accumulate_grad_hook(h))
+                # ... and the direct path (fused ops that wrote into the arena call this)
+                p._pmd_ready = h
         self.iteration = 0
 
     # ------------------------------------------------------------ buckets
@@ -121,9 +126,13 @@ class DataParallel(nn.Module):
 
     # --------------------------------------------------------------- hooks
     def _make_hook(self, i):
+        # Called by the AccumulateGrad post-hook and/or by fused ops that wrote the
+        # gradient into the arena directly (autograd may still run the post-hook
+        # for those with an undefined grad) -> idempotent per iteration.
         def hook(_p):
-            if not self._sync_enabled:
+            if not self._sync_enabled or self._marked[i]:
                 return
+            self._marked[i] = True
             if not self._callback_queued:
                 self._callback_queued = True
                 torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
@@ -154,6 +163,7 @@ class DataParallel(nn.Module):
             b.work = None
             b.fired = 0
             b.pending = len(b.params)
+        self._marked = [False] * len(self.flat.params)
         self._callback_queued = False
         self.iteration += 1
 

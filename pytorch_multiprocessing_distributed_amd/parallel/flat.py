@@ -59,6 +59,8 @@ class FlatParams:
                 pv.copy_(p.detach())
                 p.data = pv
                 p.grad = self._view(self.grad_arena, p, o)
+                # fused ops may accumulate this param's gradient straight into the arena
+                p._pmd_direct = True
 
     @staticmethod
     def _view(arena, p, off):
