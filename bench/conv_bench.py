@@ -52,13 +52,17 @@ def main():
     ap.add_argument("--iters", type=int, default=15)
     ap.add_argument("--json", default="")
     ap.add_argument("--only", default="")
+    ap.add_argument("--impls", default="1", help="conv operand-staging impls to time (0 reg, 1 DMA)")
+    ap.add_argument("--no-miopen", action="store_true")
     a = ap.parse_args()
     torch.backends.cudnn.benchmark = True
     dev = "cuda"
     rows = []
     tot = {"ours": 0.0, "miopen": 0.0}
+    from pytorch_multiprocessing_distributed_amd.ops.native import C as _C
+    impls = [int(v) for v in a.impls.split(",")]
     print(f"{'shape':>24} | {'fwd ours':>9} {'miopen':>7} | {'dgrad':>9} {'miopen':>7} | "
-          f"{'wgrad':>9} {'miopen':>7}   (TFLOP/s)")
+          f"{'wgrad':>9} {'miopen':>7}   (TFLOP/s; ours per impl {impls})")
     for (C, H, K, R, st, cnt) in SHAPES:
         name = f"C{C}_H{H}_K{K}_R{R}_s{st}"
         if a.only and a.only not in name:
@@ -73,26 +77,42 @@ def main():
         P = y.shape[1]
         dy = torch.randn_like(y)
         flops = 2.0 * N * P * P * K * C * R * R
-        t_f = timeit(lambda: HP.conv_fwd(x, wp, st, pad, True), a.iters)
-        t_d = timeit(lambda: HP.conv_dgrad(dy, wp, tuple(x.shape), st, pad), a.iters) if C != 8 else 0.0
-        t_w = timeit(lambda: HP.conv_wgrad(dy, x, tuple(wp[0].shape), st, pad), a.iters)
+
+        def fwd():
+            yy, ss = HP.conv_fwd(x, wp, st, pad, True)
+            HP._release(ss)          # recycle without clearing: timing only
+        per = {}
+        for im in impls:
+            _C.conv_set_impl(im)
+            per[im] = (timeit(fwd, a.iters),
+                       timeit(lambda: HP.conv_dgrad(dy, wp, tuple(x.shape), st, pad), a.iters)
+                       if C != 8 else 0.0,
+                       timeit(lambda: HP.conv_wgrad(dy, x, tuple(wp[0].shape), st, pad), a.iters))
+        t_f, t_d, t_w = per[impls[-1]]
         # MIOpen (NCHW-shaped channels_last views of the same data)
         xn = x.permute(0, 3, 1, 2)
         wn = w.to(torch.bfloat16)
         dyn = dy.permute(0, 3, 1, 2)
-        m_f = timeit(lambda: F.conv2d(xn, wn, stride=st, padding=pad), a.iters)
-        m_d = timeit(lambda: torch.nn.grad.conv2d_input(xn.shape, wn, dyn, stride=st, padding=pad),
-                     a.iters) if C != 8 else 0.0
-        m_w = timeit(lambda: torch.nn.grad.conv2d_weight(xn, wn.shape, dyn, stride=st, padding=pad),
-                     a.iters)
+        if a.no_miopen:
+            m_f = m_d = m_w = 0.0
+        else:
+            m_f = timeit(lambda: F.conv2d(xn, wn, stride=st, padding=pad), a.iters)
+            m_d = timeit(lambda: torch.nn.grad.conv2d_input(xn.shape, wn, dyn, stride=st,
+                                                            padding=pad), a.iters) if C != 8 else 0.0
+            m_w = timeit(lambda: torch.nn.grad.conv2d_weight(xn, wn.shape, dyn, stride=st,
+                                                             padding=pad), a.iters)
 
         def tf(t):
             return flops / t / 1e9 if t > 0 else 0.0
-        print(f"{name:>24} | {tf(t_f):9.0f} {tf(m_f):7.0f} | {tf(t_d):9.0f} {tf(m_d):7.0f} | "
-              f"{tf(t_w):9.0f} {tf(m_w):7.0f}", flush=True)
+
+        def cell(k, m):
+            ours = "/".join(f"{tf(per[im][k]):.0f}" for im in impls)
+            return f"{ours:>9} {tf(m):7.0f}"
+        print(f"{name:>24} | {cell(0, m_f)} | {cell(1, m_d)} | {cell(2, m_w)}", flush=True)
         tot["ours"] += cnt * (t_f + t_d + t_w)
         tot["miopen"] += cnt * (m_f + m_d + m_w)
         rows.append(dict(shape=name, count=cnt, ms=dict(fwd=t_f, dgrad=t_d, wgrad=t_w),
+                         ms_by_impl={str(k): v for k, v in per.items()},
                          miopen_ms=dict(fwd=m_f, dgrad=m_d, wgrad=m_w), gflop=flops / 1e9))
     print(f"R50 conv total (count-weighted): ours {tot['ours']:.2f} ms, MIOpen {tot['miopen']:.2f} ms")
     if a.json:

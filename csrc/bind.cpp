@@ -411,6 +411,7 @@ Tensor cifar_augment(Tensor data, Tensor idx, int64_t Cp, bool train, int64_t pa
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) kernels for pytorch_multiprocessing_distributed_amd";
   m.def("conv_weight_prep", &conv_weight_prep);
+  m.def("conv_set_impl", &pmd::conv_set_impl, "0: register-staged operands, 1: LDS-DMA operands");
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);

@@ -23,6 +23,7 @@
 // atomic per channel per block), then the tile is staged through LDS and
 // written with coalesced 16-byte row stores.
 #include "common.h"
+#include <stdlib.h>
 
 namespace pmd {
 
@@ -41,14 +42,23 @@ struct ConvArgs {
 constexpr int BK = 64;
 constexpr int LDA = BK + 8;  // padded LDS row (elements)
 
-template <int BM, int BN, bool DGRAD, bool STATS>
+// 16 zero bytes: the LDS-DMA source for padded / out-of-range im2col chunks
+__device__ __attribute__((aligned(16))) unsigned char g_zero16[64];
+
+// DMA=true : operands are copied global->LDS by LDS-DMA (global_load_lds_dwordx4,
+//            no VGPR round trip, no ds_write), unpadded 128-B rows with the 16-B
+//            chunk XOR-swizzled by (row & 7) -- the swizzle is applied to the
+//            per-lane SOURCE address because the DMA writes lane-linearly.
+// DMA=false: register staging into 144-B padded rows (the original kernel).
+template <int BM, int BN, bool DGRAD, bool STATS, bool DMA>
 __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
   constexpr int PA = BM / 32;        // A rows per thread
   constexpr int PB = BN / 32;        // B rows per thread
   constexpr int MI = BM / 32;        // 16-row MFMA tiles per wave (wave covers BM/2)
   constexpr int NI = BN / 32;        // 16-col MFMA tiles per wave
-  constexpr int A_ELEMS = BM * LDA;
-  constexpr int B_ELEMS = BN * LDA;
+  constexpr int LDR = DMA ? BK : LDA;  // LDS row length (elements)
+  constexpr int A_ELEMS = BM * LDR;
+  constexpr int B_ELEMS = BN * LDR;
   constexpr int STAGE = A_ELEMS + B_ELEMS;
   constexpr int LDC = BN + 8;
   constexpr int SMEM_MAIN = 2 * STAGE * 2;
@@ -90,14 +100,19 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
   if (m0 >= Mp) return;  // uniform per block, before any barrier
 
   // ---- per-thread A-row precompute
-  const int chunk = tid & 7;
+  // register staging: thread -> (row rsub + 32 i, chunk tid & 7)
+  // DMA: wave w, instruction i, lane l -> row w*(BM/4) + 8 i + l/8, LDS chunk l&7
+  //      holding logical chunk (l&7) ^ ((l/8)&7)
+  const int chunk = DMA ? ((lane & 7) ^ ((lane >> 3) & 7)) : (tid & 7);
   const int rsub = tid >> 3;  // 0..31
+  auto a_row_of = [&](int i) { return DMA ? wid * (BM / 4) + 8 * i + (lane >> 3) : rsub + 32 * i; };
+  auto b_row_of = [&](int i) { return DMA ? wid * (BN / 4) + 8 * i + (lane >> 3) : rsub + 32 * i; };
   int a_base[PA], a_h[PA], a_w[PA];
   bool a_ok[PA];
   const int ohw = OHp * OWp;
 #pragma unroll
   for (int i = 0; i < PA; ++i) {
-    const int m = m0 + rsub + 32 * i;
+    const int m = m0 + a_row_of(i);
     a_ok[i] = m < Mp;
     const int mm = a_ok[i] ? m : 0;
     const int n = mm / ohw;
@@ -117,7 +132,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
   bool b_ok[PB];
 #pragma unroll
   for (int i = 0; i < PB; ++i) {
-    const int nn = n0 + rsub + 32 * i;
+    const int nn = n0 + b_row_of(i);
     b_ok[i] = nn < a.Nout;
     b_row[i] = a.wt + (size_t)(b_ok[i] ? nn : 0) * a.Kg;
   }
@@ -125,7 +140,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
   uint4 ra[PA], rb[PB];
   const int nk = (Kgp + BK - 1) / BK;
 
-  auto load_tile = [&](int kt) {
+  auto load_tile = [&](int kt, int dbuf) {
     const int k0 = kt * BK + chunk * 8;
     const bool kok = k0 < Kgp;
     const int tap = k0 >> a.log2Cs;
@@ -148,18 +163,33 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
         iw = a_w[i] + s;
       }
       ok = ok && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (ok) {
-        const size_t pix = (size_t)(a_base[i] + ih * a.W + iw);
-        v = *reinterpret_cast<const uint4*>(a.src + (pix << a.log2Cs) + c);
+      if constexpr (DMA) {
+        const void* src = g_zero16;
+        if (ok) src = a.src + (((size_t)(a_base[i] + ih * a.W + iw)) << a.log2Cs) + c;
+        bf16_t* dst = lds + dbuf * STAGE + (wid * (BM / 4) + 8 * i) * LDR;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      } else {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (ok) {
+          const size_t pix = (size_t)(a_base[i] + ih * a.W + iw);
+          v = *reinterpret_cast<const uint4*>(a.src + (pix << a.log2Cs) + c);
+        }
+        ra[i] = v;
       }
-      ra[i] = v;
     }
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (b_ok[i] && kok) v = *reinterpret_cast<const uint4*>(b_row[i] + boff);
-      rb[i] = v;
+      if constexpr (DMA) {
+        const void* src = (b_ok[i] && kok) ? (const void*)(b_row[i] + boff) : (const void*)g_zero16;
+        bf16_t* dst = lds + dbuf * STAGE + A_ELEMS + (wid * (BN / 4) + 8 * i) * LDR;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      } else {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (b_ok[i] && kok) v = *reinterpret_cast<const uint4*>(b_row[i] + boff);
+        rb[i] = v;
+      }
     }
   };
   auto store_tile = [&](int buf) {
@@ -179,36 +209,68 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nk > 0) {
-    load_tile(0);
-    store_tile(0);
-  }
-  __syncthreads();
-
   const int frow = lane & 15;
   const int fk = (lane >> 4) * 8;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) load_tile(kt + 1);
-    const bf16_t* As = lds + buf * STAGE + (wm * (BM / 2)) * LDA;
-    const bf16_t* Bs = lds + buf * STAGE + A_ELEMS + (wn * (BN / 2)) * LDA;
+  // fragment read: row r, logical 16-B chunk q of the current K-step
+  auto frag = [&](const bf16_t* base, int r, int q) {
+    if constexpr (DMA)
+      return *reinterpret_cast<const bf16x8*>(base + r * LDR + ((q ^ (r & 7)) << 3));
+    else
+      return *reinterpret_cast<const bf16x8*>(base + r * LDR + (q << 3));
+  };
+  auto compute = [&](int buf) {
+    const bf16_t* As = lds + buf * STAGE;
+    const bf16_t* Bs = lds + buf * STAGE + A_ELEMS;
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       bf16x8 af[MI], bfg[NI];
+      const int q = ks * 4 + (lane >> 4);
 #pragma unroll
-      for (int i = 0; i < MI; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(As + (i * 16 + frow) * LDA + ks * 32 + fk);
+      for (int i = 0; i < MI; ++i) af[i] = frag(As, wm * (BM / 2) + i * 16 + frow, q);
 #pragma unroll
-      for (int j = 0; j < NI; ++j)
-        bfg[j] = *reinterpret_cast<const bf16x8*>(Bs + (j * 16 + frow) * LDA + ks * 32 + fk);
+      for (int j = 0; j < NI; ++j) bfg[j] = frag(Bs, wn * (BN / 2) + j * 16 + frow, q);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) store_tile(buf ^ 1);
+  };
+  (void)fk;
+
+  if constexpr (DMA) {
+    // one barrier-protected DMA stage in flight while the other is consumed:
+    //   issue(kt+1) ; wait own DMAs of kt (vmcnt = #DMAs of kt+1) ; barrier ; MFMA(kt) ; barrier
+    if (nk > 0) load_tile(0, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) {
+        load_tile(kt + 1, (kt + 1) & 1);
+        if constexpr (PA + PB == 8)
+          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if constexpr (PA + PB == 6)
+          asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      asm volatile("s_barrier" ::: "memory");
+      compute(kt & 1);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+  } else {
+    if (nk > 0) {
+      load_tile(0, 0);
+      store_tile(0);
+    }
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      if (kt + 1 < nk) load_tile(kt + 1, buf ^ 1);
+      compute(buf);
+      if (kt + 1 < nk) store_tile(buf ^ 1);
+      __syncthreads();
+    }
   }
 
   // ---- epilogue
@@ -309,14 +371,30 @@ static int ilog2(int v) {
   return l;
 }
 
+static int g_conv_impl = -1;  // 0 = register staging, 1 = LDS-DMA (default)
+
+void conv_set_impl(int impl) { g_conv_impl = impl; }
+
+static bool use_dma() {
+  if (g_conv_impl < 0) {
+    const char* e = getenv("PMD_CONV_IMPL");
+    g_conv_impl = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_conv_impl == 1;
+}
+
 template <int BM, int BN, bool DGRAD, bool STATS>
 static void launch_t(const ConvArgs& a, hipStream_t st) {
   const bool ph2 = DGRAD && a.stride == 2;
   const int Mgrid = ph2 ? a.N * ((a.OH + 1) >> 1) * ((a.OW + 1) >> 1) : a.M;
   const int tiles = ((Mgrid + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
   const int phases = ph2 ? 4 : 1;
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, DGRAD, STATS>), dim3(tiles, phases), dim3(256), 0, st,
-                     a);
+  if (use_dma())
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, DGRAD, STATS, true>), dim3(tiles, phases), dim3(256), 0,
+                       st, a);
+  else
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, DGRAD, STATS, false>), dim3(tiles, phases), dim3(256),
+                       0, st, a);
 }
 
 template <bool DGRAD, bool STATS>

@@ -166,6 +166,7 @@ class ResNet(nn.Module):
             raise ValueError(f"unknown stem {stem!r}")
         self.impl = impl
         self.stem = stem
+        self.nchw_input = False   # True: accept reference-style NCHW input and transpose it
         self.in_planes = 64
         if stem == "cifar":
             self.conv1 = _conv(impl, 3, 64, 3, 1, 1)
@@ -194,6 +195,8 @@ class ResNet(nn.Module):
             out = self.layer4(self.layer3(self.layer2(self.layer1(out))))
             out = F.adaptive_avg_pool2d(out, 1).flatten(1)
             return self.linear(out)
+        if self.nchw_input and x.dim() == 4 and x.shape[1] in (3, 8) and x.shape[-1] not in (3, 8):
+            x = x.permute(0, 2, 3, 1).contiguous()
         out = OF.conv_bn_act(x, self.conv1, self.bn1, relu=True)
         if self.stem == "imagenet":
             out = OF.max_pool3x3s2(out)
