@@ -129,8 +129,13 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int64_t R, int64_t S, int64_t stride, int
   } else {
     dw = torch::zeros({K, R, S, C}, x.options().dtype(torch::kFloat32));
   }
-  const int rc = pmd::conv_wgrad_launch(bfp(dy), bfp(x), dw.data_ptr<float>(), N, H, W, C, P, Q, K,
-                                        (int)R, (int)S, (int)stride, (int)pad, cur_stream());
+  const int splits = pmd::conv_wgrad_splits(N, H, W, C, P, Q, K, (int)R, (int)S, (int)stride,
+                                            (int)pad);
+  Tensor ws;
+  if (splits > 1) ws = torch::empty({splits, K, R * S * C}, x.options().dtype(torch::kFloat32));
+  const int rc = pmd::conv_wgrad_launch(bfp(dy), bfp(x), dw.data_ptr<float>(),
+                                        splits > 1 ? ws.data_ptr<float>() : nullptr, N, H, W, C, P, Q,
+                                        K, (int)R, (int)S, (int)stride, (int)pad, cur_stream());
   CHECK_RC(rc, "conv_wgrad");
   return dw;
 }
@@ -213,8 +218,9 @@ Tensor stats_finalize_local(Tensor slots, double count, Tensor gamma, Tensor bet
   return params;
 }
 
-Tensor bn_apply(Tensor y1, Tensor p1, c10::optional<Tensor> res, c10::optional<Tensor> y2,
-                c10::optional<Tensor> p2, bool relu) {
+// returns {out} or {out, relu_bitmask} (one uint8 per 8-channel chunk) when relu && want_mask
+std::vector<Tensor> bn_apply(Tensor y1, Tensor p1, c10::optional<Tensor> res, c10::optional<Tensor> y2,
+                             c10::optional<Tensor> p2, bool relu, bool want_mask) {
   CHECK_DEV(y1); CHECK_BF16(y1); CHECK_CONT(y1);
   const int C = y1.size(-1);
   const long long M = y1.numel() / C;
@@ -237,16 +243,28 @@ Tensor bn_apply(Tensor y1, Tensor p1, c10::optional<Tensor> res, c10::optional<T
   }
   c10::DeviceGuard g(y1.device());
   Tensor out = torch::empty_like(y1);
-  const int rc = pmd::bn_apply_launch(bfp(y1), p1.data_ptr<float>(), r, pp2, bfp_mut(out), M, C, mode,
-                                      relu, cur_stream());
+  Tensor mask;
+  const bool wm = relu && want_mask;
+  if (wm) mask = torch::empty({M * (C / 8)}, y1.options().dtype(torch::kUInt8));
+  const int rc = pmd::bn_apply_launch(bfp(y1), p1.data_ptr<float>(), r, pp2, bfp_mut(out),
+                                      wm ? mask.data_ptr<uint8_t>() : nullptr, M, C, mode, relu,
+                                      cur_stream());
   CHECK_RC(rc, "bn_apply");
-  return out;
+  if (wm) return {out, mask};
+  return {out};
 }
 
-Tensor bn_bwd_reduce(Tensor dout, Tensor out, Tensor y, Tensor params, bool relu,
+const uint8_t* mask_ptr(const c10::optional<Tensor>& mask, long long chunks, bool relu) {
+  if (!relu) return nullptr;
+  TORCH_CHECK(mask && mask->defined() && mask->scalar_type() == torch::kUInt8 && mask->is_cuda() &&
+              mask->is_contiguous() && mask->numel() == chunks, "relu backward needs the uint8 bitmask");
+  return mask->data_ptr<uint8_t>();
+}
+
+Tensor bn_bwd_reduce(Tensor dout, c10::optional<Tensor> mask, Tensor y, Tensor params, bool relu,
                      c10::optional<Tensor> red_buf) {
   CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONT(dout);
-  CHECK_BF16(out); CHECK_CONT(out); CHECK_BF16(y); CHECK_CONT(y);
+  CHECK_BF16(y); CHECK_CONT(y);
   const int C = y.size(-1);
   const long long M = y.numel() / C;
   TORCH_CHECK(M < (1ll << 31), "too many rows");
@@ -259,18 +277,19 @@ Tensor bn_bwd_reduce(Tensor dout, Tensor out, Tensor y, Tensor params, bool relu
   } else {
     red = torch::zeros({pmd_slots(), 2, C}, y.options().dtype(torch::kFloat32));
   }
-  const int rc = pmd::bn_bwd_reduce_launch(bfp(dout), bfp(out), bfp(y), params.data_ptr<float>(),
-                                           red.data_ptr<float>(), (int)M, C, relu, cur_stream());
+  const int rc = pmd::bn_bwd_reduce_launch(bfp(dout), mask_ptr(mask, M * (C / 8), relu), bfp(y),
+                                           params.data_ptr<float>(), red.data_ptr<float>(), (int)M, C,
+                                           relu, cur_stream());
   CHECK_RC(rc, "bn_bwd_reduce");
   return red;
 }
 
 // count: device scalar (SyncBN global count) or, if absent, count_h from the host
-std::vector<Tensor> bn_bwd_elemt(Tensor dout, Tensor out, Tensor y, Tensor params, Tensor gamma,
-                                 c10::optional<Tensor> red, c10::optional<Tensor> count,
-                                 double count_h, bool relu, bool want_dzm, bool eval_mode) {
+std::vector<Tensor> bn_bwd_elemt(Tensor dout, c10::optional<Tensor> mask, Tensor y, Tensor params,
+                                 Tensor gamma, c10::optional<Tensor> red,
+                                 c10::optional<Tensor> count, double count_h, bool relu,
+                                 bool want_dzm, bool eval_mode) {
   CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONT(dout);
-  CHECK_BF16(out); CHECK_CONT(out);
   const int C = dout.size(-1);
   const long long M = dout.numel() / C;
   c10::DeviceGuard g(dout.device());
@@ -285,7 +304,7 @@ std::vector<Tensor> bn_bwd_elemt(Tensor dout, Tensor out, Tensor y, Tensor param
     if (count && count->defined()) cc = count->contiguous();
   }
   const int rc = pmd::bn_bwd_elemt_launch(
-      bfp(dout), bfp(out), eval_mode ? nullptr : bfp(y), params.data_ptr<float>(), gm.data_ptr<float>(),
+      bfp(dout), mask_ptr(mask, M * (C / 8), relu), eval_mode ? nullptr : bfp(y), params.data_ptr<float>(), gm.data_ptr<float>(),
       eval_mode ? nullptr : rr.data_ptr<float>(),
       (eval_mode || !cc.defined()) ? nullptr : cc.data_ptr<float>(), (float)count_h, bfp_mut(dy), want_dzm ? bfp_mut(dzm) : nullptr, M, C, relu, eval_mode, cur_stream());
   CHECK_RC(rc, "bn_bwd_elemt");

@@ -65,8 +65,9 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
                                                        const float* __restrict__ p1,
                                                        const bf16_t* __restrict__ r,
                                                        const float* __restrict__ p2,
-                                                       bf16_t* __restrict__ out, long long nchunk,
-                                                       int C) {
+                                                       bf16_t* __restrict__ out,
+                                                       uint8_t* __restrict__ mask_out,
+                                                       long long nchunk, int C) {
   const int C8 = C >> 3;
   const long long start = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long step = (long long)gridDim.x * blockDim.x;
@@ -82,22 +83,27 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
     float v[8], w[8];
     unpack8(reinterpret_cast<const uint4*>(y1)[i], v);
     if (MODE >= 1) unpack8(reinterpret_cast<const uint4*>(r)[i], w);
+    uint32_t bits = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float o = v[k] * s1[k] + b1[k];
       if (MODE == 1) o += w[k];
       if (MODE == 2) o += w[k] * s2[k] + b2[k];
-      if (RELU) o = fmaxf(o, 0.f);
+      if (RELU) {
+        bits |= (uint32_t)(o > 0.f) << k;
+        o = fmaxf(o, 0.f);
+      }
       v[k] = o;
     }
     reinterpret_cast<uint4*>(out)[i] = pack8(v);
+    if (RELU && mask_out) mask_out[i] = (uint8_t)bits;
   }
 }
 
 // red out: [2][C] += (sum dzm, sum dzm*xhat); TPR = C/8 threads per row (<= 256)
 template <bool RELU>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __restrict__ dout,
-                                                            const bf16_t* __restrict__ out,
+                                                            const uint8_t* __restrict__ mask,
                                                             const bf16_t* __restrict__ y,
                                                             const float* __restrict__ params,
                                                             float* __restrict__ red, int M, int C) {
@@ -115,13 +121,13 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
   for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
   for (int row = blockIdx.x * rpi + tid / C8; row < M; row += gridDim.x * rpi) {
     const long long i = (long long)row * C8 + cc;
-    float d[8], o[8], v[8];
+    float d[8], v[8];
     unpack8(reinterpret_cast<const uint4*>(dout)[i], d);
-    if (RELU) unpack8(reinterpret_cast<const uint4*>(out)[i], o);
+    const uint32_t mb = RELU ? mask[i] : 0xffu;
     unpack8(reinterpret_cast<const uint4*>(y)[i], v);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const float dz = (RELU && !(o[k] > 0.f)) ? 0.f : d[k];
+      const float dz = ((mb >> k) & 1u) ? d[k] : 0.f;
       s1[k] += dz;
       s2[k] += dz * (v[k] - mean[k]) * inv[k];
     }
@@ -157,7 +163,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
 //                        eval : a = scale, b = c = 0
 template <bool RELU, bool DZM, bool EVAL>
 __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(
-    const bf16_t* __restrict__ dout, const bf16_t* __restrict__ out, const bf16_t* __restrict__ y,
+    const bf16_t* __restrict__ dout, const uint8_t* __restrict__ mask, const bf16_t* __restrict__ y,
     const float* __restrict__ params, const float* __restrict__ gamma,
     const float* __restrict__ red, const float* __restrict__ count, float count_h,
     bf16_t* __restrict__ dy, bf16_t* __restrict__ dzm_out, long long nchunk, int C) {
@@ -190,11 +196,11 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(
   for (long long i = start; i < nchunk; i += step) {
     float d[8], o[8], v[8];
     unpack8(reinterpret_cast<const uint4*>(dout)[i], d);
-    if (RELU) unpack8(reinterpret_cast<const uint4*>(out)[i], o);
+    const uint32_t mb = RELU ? mask[i] : 0xffu;
     if (!EVAL) unpack8(reinterpret_cast<const uint4*>(y)[i], v);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const float dz = (RELU && !(o[k] > 0.f)) ? 0.f : d[k];
+      const float dz = ((mb >> k) & 1u) ? d[k] : 0.f;
       d[k] = dz;
       o[k] = EVAL ? ca[k] * dz : ca[k] * dz + cb[k] * v[k] + cc[k];
     }
@@ -304,12 +310,13 @@ int bn_finalize_launch(const float* sums, const float* count, const float* gamma
 }
 
 int bn_apply_launch(const bf16_t* y1, const float* p1, const bf16_t* r, const float* p2, bf16_t* out,
-                    long long M, int C, int mode, bool relu, hipStream_t st) {
+                    uint8_t* mask, long long M, int C, int mode, bool relu, hipStream_t st) {
   if (C % 8 || (C >> 3) > 256 || ((C >> 3) & ((C >> 3) - 1))) return 1;
   const long long nchunk = M * (C / 8);
   const int g = ew_grid(nchunk, C / 8);
 #define APPLY(MD, RL) \
-  hipLaunchKernelGGL((bn_apply_kernel<MD, RL>), dim3(g), dim3(256), 0, st, y1, p1, r, p2, out, nchunk, C)
+  hipLaunchKernelGGL((bn_apply_kernel<MD, RL>), dim3(g), dim3(256), 0, st, y1, p1, r, p2, out, mask, \
+                     nchunk, C)
   if (relu) {
     if (mode == 0) APPLY(0, true); else if (mode == 1) APPLY(1, true); else APPLY(2, true);
   } else {
@@ -319,23 +326,23 @@ int bn_apply_launch(const bf16_t* y1, const float* p1, const bf16_t* r, const fl
   return 0;
 }
 
-int bn_bwd_reduce_launch(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const float* params,
-                         float* red, int M, int C, bool relu, hipStream_t st) {
+int bn_bwd_reduce_launch(const bf16_t* dout, const uint8_t* mask, const bf16_t* y,
+                         const float* params, float* red, int M, int C, bool relu, hipStream_t st) {
   const int C8 = C / 8;
   if (C % 8 || C8 > 256 || (C8 & (C8 - 1))) return 1;
   const int rpi = 256 / C8;
   long long b = ((long long)M + rpi - 1) / rpi;
   if (b > 1024) b = 1024;
   if (relu)
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true>), dim3((int)b), dim3(256), 0, st, dout, out, y,
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true>), dim3((int)b), dim3(256), 0, st, dout, mask, y,
                        params, red, M, C);
   else
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false>), dim3((int)b), dim3(256), 0, st, dout, out, y,
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false>), dim3((int)b), dim3(256), 0, st, dout, mask, y,
                        params, red, M, C);
   return 0;
 }
 
-int bn_bwd_elemt_launch(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const float* params,
+int bn_bwd_elemt_launch(const bf16_t* dout, const uint8_t* mask, const bf16_t* y, const float* params,
                         const float* gamma, const float* red, const float* count, float count_h,
                         bf16_t* dy, bf16_t* dzm, long long M, int C, bool relu, bool eval_mode,
                         hipStream_t st) {
@@ -343,7 +350,7 @@ int bn_bwd_elemt_launch(const bf16_t* dout, const bf16_t* out, const bf16_t* y, 
   const long long nchunk = M * (C / 8);
   const int g = ew_grid(nchunk, C / 8);
 #define EL(RL, DZ, EV)                                                                            \
-  hipLaunchKernelGGL((bn_bwd_elemt_kernel<RL, DZ, EV>), dim3(g), dim3(256), 0, st, dout, out, y, \
+  hipLaunchKernelGGL((bn_bwd_elemt_kernel<RL, DZ, EV>), dim3(g), dim3(256), 0, st, dout, mask, y, \
                      params, gamma, red, count, count_h, dy, dzm, nchunk, C)
   const bool dz = dzm != nullptr;
   if (eval_mode) {

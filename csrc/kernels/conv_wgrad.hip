@@ -12,8 +12,11 @@
 // distinct bank windows.
 //
 // The m axis is split over blocks (enough blocks to fill the 256 CUs); each
-// block reduces its range in registers and adds its fp32 tile into dW with
-// one atomic per element.  Each thread's im2col column (r, s, c) is fixed for
+// block reduces its range in registers and writes its fp32 partial tile with
+// plain stores into a [split][K][Kg] workspace; wgrad_reduce then adds the
+// splits into dW in a fixed order (deterministic, and plain stores run ~4-5x
+// the chip's fp32-atomic byte rate).  With a single split the block adds its
+// tile into dW directly.  Each thread's im2col column (r, s, c) is fixed for
 // the whole kernel and the per-row (n, p, q) coordinates advance by
 // single-carry increments, so the gather costs no integer divisions in the
 // main loop.
@@ -24,7 +27,8 @@ namespace pmd {
 struct WgradArgs {
   const bf16_t* dy;  // [M][K]
   const bf16_t* x;   // NHWC [N, H, W, C]
-  float* dw;         // [K][Kg] fp32, pre-zeroed
+  float* dw;         // [K][Kg] fp32 accumulation target
+  float* ws;         // [splits][K][Kg] partials, or nullptr when splits == 1
   int N, H, W, C, log2C;
   int P, Q, K, R, S, stride, pad;
   int M, Kg;
@@ -191,7 +195,8 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
     __syncthreads();
   }
 
-  // epilogue: fp32 atomics into dW[k][kg]
+  // epilogue: partial tile -> workspace slice of this split (or += dW when unsplit)
+  float* dst = a.ws ? a.ws + (size_t)split * a.K * a.Kg : a.dw;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -200,8 +205,50 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
       for (int e = 0; e < 4; ++e) {
         const int k = k0 + wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + e;
         const int gg = g0 + wn * (BN / 2) + j * 16 + (lane & 15);
-        if (k < a.K && gg < a.Kg) atomicAdd(a.dw + (size_t)k * a.Kg + gg, acc[i][j][e]);
+        if (k < a.K && gg < a.Kg) {
+          float* p = dst + (size_t)k * a.Kg + gg;
+          if (a.ws)
+            *p = acc[i][j][e];
+          else
+            *p += acc[i][j][e];
+        }
       }
+}
+
+// dW[i] += sum_s ws[s][i].  blockIdx.y = split group of <= kSplitGroup slices:
+// one group -> plain read-modify-write in fixed order (deterministic); several
+// groups (tiny outputs with hundreds of splits) -> one fp32 atomic per group.
+constexpr int kSplitGroup = 32;
+__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw, int splits,
+                                    long long n4) {
+  const int s0 = blockIdx.y * kSplitGroup;
+  const int s1 = s0 + kSplitGroup < splits ? s0 + kSplitGroup : splits;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
+       i += (long long)gridDim.x * blockDim.x) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+    for (int s = s0; s < s1; ++s) {
+      const float4 v = reinterpret_cast<const float4*>(ws)[(long long)s * n4 + i];
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+    if (gridDim.y == 1) {
+      float4 d = reinterpret_cast<float4*>(dw)[i];
+      d.x += acc.x;
+      d.y += acc.y;
+      d.z += acc.z;
+      d.w += acc.w;
+      reinterpret_cast<float4*>(dw)[i] = d;
+    } else {
+      float* p = dw + 4 * i;
+      atomicAdd(p, acc.x);
+      atomicAdd(p + 1, acc.y);
+      atomicAdd(p + 2, acc.z);
+      atomicAdd(p + 3, acc.w);
+    }
+  }
 }
 
 static int ilog2w(int v) {
@@ -210,29 +257,25 @@ static int ilog2w(int v) {
   return l;
 }
 
-template <int BM, int BN>
-static void launch_w(WgradArgs a, hipStream_t st) {
+template <int BM>
+static void plan(const WgradArgs& a, int* splits_out, int* cps_out) {
+  constexpr int BN = 128;
   const int tiles = ((a.K + BM - 1) / BM) * ((a.Kg + BN - 1) / BN);
   const int chunks = (a.M + BR - 1) / BR;
   int splits = (1024 + tiles - 1) / tiles;
   const int max_splits = (chunks + 3) / 4;
   if (splits > max_splits) splits = max_splits;
+  // keep the partial workspace bounded (<= 96 MiB)
+  const long long per = (long long)a.K * a.Kg * 4;
+  while (splits > 1 && per * splits > (96ll << 20)) --splits;
   if (splits < 1) splits = 1;
-  a.chunks_per_split = (chunks + splits - 1) / splits;
-  splits = (chunks + a.chunks_per_split - 1) / a.chunks_per_split;
-  hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN>), dim3(tiles * splits), dim3(256), 0, st, a);
+  const int cps = (chunks + splits - 1) / splits;
+  *cps_out = cps;
+  *splits_out = (chunks + cps - 1) / cps;
 }
 
-int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, int N, int H, int W, int C, int P,
-                      int Q, int K, int R, int S, int stride, int pad, hipStream_t st) {
-  if (C % 8 != 0 || (C & (C - 1)) != 0) return 1;
-  if (K % 64 != 0) return 2;
-  const long long M = (long long)N * P * Q;
-  if (M >= (1ll << 31)) return 4;
-  WgradArgs a;
-  a.dy = dy;
-  a.x = x;
-  a.dw = dw;
+static void fill_args(WgradArgs& a, int N, int H, int W, int C, int P, int Q, int K, int R, int S,
+                      int stride, int pad) {
   a.N = N;
   a.H = H;
   a.W = W;
@@ -245,13 +288,53 @@ int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, int N, int H
   a.S = S;
   a.stride = stride;
   a.pad = pad;
-  a.M = (int)M;
+  a.M = (int)((long long)N * P * Q);
   a.Kg = R * S * C;
-  a.chunks_per_split = 1;
+}
+
+int conv_wgrad_splits(int N, int H, int W, int C, int P, int Q, int K, int R, int S, int stride,
+                      int pad) {
+  WgradArgs a;
+  fill_args(a, N, H, W, C, P, Q, K, R, S, stride, pad);
+  int splits, cps;
   if (K == 64)
-    launch_w<64, 128>(a, st);
+    plan<64>(a, &splits, &cps);
   else
-    launch_w<128, 128>(a, st);
+    plan<128>(a, &splits, &cps);
+  return splits;
+}
+
+int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, float* ws, int N, int H, int W,
+                      int C, int P, int Q, int K, int R, int S, int stride, int pad, hipStream_t st) {
+  if (C % 8 != 0 || (C & (C - 1)) != 0) return 1;
+  if (K % 64 != 0) return 2;
+  if ((long long)N * P * Q >= (1ll << 31)) return 4;
+  WgradArgs a;
+  a.dy = dy;
+  a.x = x;
+  a.dw = dw;
+  fill_args(a, N, H, W, C, P, Q, K, R, S, stride, pad);
+  int splits, cps;
+  if (K == 64)
+    plan<64>(a, &splits, &cps);
+  else
+    plan<128>(a, &splits, &cps);
+  a.chunks_per_split = cps;
+  a.ws = splits > 1 ? ws : nullptr;
+  if (splits > 1 && !ws) return 5;
+  const int BM = K == 64 ? 64 : 128;
+  const int tiles = ((a.K + BM - 1) / BM) * ((a.Kg + 127) / 128);
+  if (K == 64)
+    hipLaunchKernelGGL((conv_wgrad_kernel<64, 128>), dim3(tiles * splits), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), dim3(tiles * splits), dim3(256), 0, st, a);
+  if (splits > 1) {
+    const long long n4 = (long long)a.K * a.Kg / 4;
+    const int groups = (splits + kSplitGroup - 1) / kSplitGroup;
+    long long b = (n4 + 255) / 256;
+    if (b > 4096) b = 4096;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)b, groups), dim3(256), 0, st, ws, dw, splits, n4);
+  }
   return 0;
 }
 

@@ -12,8 +12,12 @@ int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* s
 void conv_set_impl(int impl);  // 0 register staging, 1 LDS-DMA
 void conv_weight_prep_launch(const float* w, bf16_t* wk, bf16_t* wkt, int K, int RS, int C, int Cp,
                              hipStream_t st);
-int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, int N, int H, int W, int C, int P,
-                      int Q, int K, int R, int S, int stride, int pad, hipStream_t st);
+// split-K plan: number of partial slices the workspace must hold ([splits][K][R*S*C] fp32)
+int conv_wgrad_splits(int N, int H, int W, int C, int P, int Q, int K, int R, int S, int stride,
+                      int pad);
+// dw += dW (dw must be initialised: zeros or an accumulation target)
+int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, float* ws, int N, int H, int W,
+                      int C, int P, int Q, int K, int R, int S, int stride, int pad, hipStream_t st);
 
 int bn_finalize_launch(const float* sums, const float* count, const float* gamma, const float* beta,
                        float* params, float* rm, float* rv, long long* nbt, int C, float eps,
@@ -24,11 +28,12 @@ int stats_collapse_launch(float* a, int Ca, float* b, int Cb, float count, float
 int stats_finalize_local_launch(float* slots, float count, const float* gamma, const float* beta,
                                 float* params, float* rm, float* rv, long long* nbt, int C, float eps,
                                 float momentum, hipStream_t st);
+// mask: ReLU bitmask, one byte per 8-channel chunk (bit k = element k of the chunk > 0)
 int bn_apply_launch(const bf16_t* y1, const float* p1, const bf16_t* r, const float* p2, bf16_t* out,
-                    long long M, int C, int mode, bool relu, hipStream_t st);
-int bn_bwd_reduce_launch(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const float* params,
-                         float* red, int M, int C, bool relu, hipStream_t st);
-int bn_bwd_elemt_launch(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const float* params,
+                    uint8_t* mask, long long M, int C, int mode, bool relu, hipStream_t st);
+int bn_bwd_reduce_launch(const bf16_t* dout, const uint8_t* mask, const bf16_t* y,
+                         const float* params, float* red, int M, int C, bool relu, hipStream_t st);
+int bn_bwd_elemt_launch(const bf16_t* dout, const uint8_t* mask, const bf16_t* y, const float* params,
                         const float* gamma, const float* red, const float* count, float count_h,
                         bf16_t* dy, bf16_t* dzm, long long M, int C, bool relu, bool eval_mode,
                         hipStream_t st);

@@ -147,12 +147,12 @@ def _bn_forward_params(P, y, st, bn, training, sync, y2=None, st2=None, bn2=None
     return p1, p2, count
 
 
-def _bn_backward(P, dout, out, relu, training, sync, count, y1, p1, bn1, y2=None, p2=None,
+def _bn_backward(P, dout, mask, relu, training, sync, count, y1, p1, bn1, y2=None, p2=None,
                  bn2=None, want_dzm=False):
     """BN(+second BN)(+ReLU) backward. Returns (dy1, dy2, dzm, grads) with
     grads = [d_g1, d_b1, d_g2, d_b2] for params that were NOT written directly."""
-    r1 = P.bn_bwd_reduce(dout, out, y1, p1, relu)
-    r2 = P.bn_bwd_reduce(dout, out, y2, p2, relu) if y2 is not None else None
+    r1 = P.bn_bwd_reduce(dout, mask, y1, p1, relu)
+    r2 = P.bn_bwd_reduce(dout, mask, y2, p2, relu) if y2 is not None else None
     acc1 = _bn_acc(bn1)
     acc2 = _bn_acc(bn2) if bn2 is not None else None
     red = P.stats_collapse(r1, r2, None, acc1, acc2)     # local sums; gamma/beta grads += local
@@ -172,15 +172,15 @@ def _bn_backward(P, dout, out, relu, training, sync, count, y1, p1, bn1, y2=None
         if sync is not None:
             red = red.clone()
             sync.all_reduce_(red)
-        dy1, dzm = P.bn_bwd_elemt(dout, out, y1, p1, bn1.weight, red[:2 * c1].view(2, c1), count,
+        dy1, dzm = P.bn_bwd_elemt(dout, mask, y1, p1, bn1.weight, red[:2 * c1].view(2, c1), count,
                                   relu, want_dzm=want_dzm)
         dy2 = None
         if y2 is not None:
-            dy2, _ = P.bn_bwd_elemt(dout, out, y2, p2, bn2.weight, red[2 * c1:].view(2, -1), count,
+            dy2, _ = P.bn_bwd_elemt(dout, mask, y2, p2, bn2.weight, red[2 * c1:].view(2, -1), count,
                                     relu)
     else:
-        dy1, dzm = P.bn_bwd_elemt_eval(dout, out, p1, relu, want_dzm=want_dzm)
-        dy2 = P.bn_bwd_elemt_eval(dout, out, p2, relu)[0] if y2 is not None else None
+        dy1, dzm = P.bn_bwd_elemt_eval(dout, mask, p1, relu, want_dzm=want_dzm)
+        dy2 = P.bn_bwd_elemt_eval(dout, mask, p2, relu)[0] if y2 is not None else None
     return dy1, dy2, dzm, grads
 
 
@@ -231,19 +231,20 @@ class _BNActFn(torch.autograd.Function):
         two = y2 is not None
         p1, p2, count = _bn_forward_params(P, y1, s1, bn1, training, sync, y2, s2,
                                            bn2 if two else None)
-        out = P.bn_apply(y1, p1, res, y2, p2, relu)
+        out, mask = P.bn_apply(y1, p1, res, y2, p2, relu)
         ctx.cfg = (bn1, bn2 if two else None, relu, training, res is not None, sync, count)
-        ctx.save_for_backward(y1, out, p1, *([y2, p2] if two else []))
+        ctx.save_for_backward(y1, mask if relu else _empty(y1.device), p1,
+                              *([y2, p2] if two else []))
         return out
 
     @staticmethod
     def backward(ctx, dout):
         bn1, bn2, relu, training, has_res, sync, count = ctx.cfg
         sv = ctx.saved_tensors
-        y1, out, p1 = sv[:3]
+        y1, mask, p1 = sv[:3]
         y2, p2 = (sv[3], sv[4]) if bn2 is not None else (None, None)
         P = prims_for(y1)
-        dy1, dy2, dzm, g = _bn_backward(P, dout.contiguous(), out, relu, training, sync, count,
+        dy1, dy2, dzm, g = _bn_backward(P, dout.contiguous(), mask, relu, training, sync, count,
                                         y1, p1, bn1, y2, p2, bn2, want_dzm=has_res)
         return None, dy1, None, g[0], g[1], (dzm if has_res else None), dy2, None, g[2], g[3]
 
@@ -281,8 +282,8 @@ class _ResidualBlockFn(torch.autograd.Function):
             wp = P.conv_weight(conv_m.weight, x.dtype, h.shape[-1], True)
             y, st = P.conv_fwd(h, wp, conv_m.stride, conv_m.padding, training)
             p, _, count = _bn_forward_params(P, y, st, bn, training, sync)
-            z = P.bn_apply(y, p, relu=True)
-            recs.append((h, wp, y, p, z, count))
+            z, zmask = P.bn_apply(y, p, relu=True)
+            recs.append((h, wp, y, p, zmask, count))
             h = z
         fconv, fbn = final
         wpf = P.conv_weight(fconv.weight, x.dtype, h.shape[-1], True)
@@ -292,16 +293,17 @@ class _ResidualBlockFn(torch.autograd.Function):
             wps = P.conv_weight(sconv.weight, x.dtype, x.shape[-1], x.requires_grad)
             ys, sts = P.conv_fwd(x, wps, sconv.stride, sconv.padding, training)
             pf, ps, countf = _bn_forward_params(P, yf, stf, fbn, training, sync, ys, sts, sbn)
-            out = P.bn_apply(yf, pf, None, ys, ps, relu=True)
+            out, omask = P.bn_apply(yf, pf, None, ys, ps, relu=True)
         else:
             wps = None
             pf, _, countf = _bn_forward_params(P, yf, stf, fbn, training, sync)
-            out = P.bn_apply(yf, pf, x, relu=True)
+            out, omask = P.bn_apply(yf, pf, x, relu=True)
         ctx.cfg = (cfg, sync, [r[5] for r in recs], countf, len(wpf),
                    0 if wps is None else len(wps), [len(r[1]) for r in recs])
-        flat = [x, out, yf, pf, h, *wpf]
-        for (hin, wp, y, p, z, _) in recs:
-            flat += [hin, y, p, z, *wp]
+        # saved: the ReLU bitmasks (not the activations they came from) + conv inputs
+        flat = [x, omask, yf, pf, h, *wpf]
+        for (hin, wp, y, p, zmask, _) in recs:
+            flat += [hin, y, p, zmask, *wp]
         if shortcut is not None:
             flat += [ys, ps, *wps]
         ctx.save_for_backward(*flat)
@@ -313,7 +315,7 @@ class _ResidualBlockFn(torch.autograd.Function):
         stages, final, shortcut, training = cfg
         nst = len(stages)
         sv = list(ctx.saved_tensors)
-        x, out, yf, pf, hlast = sv[:5]
+        x, omask, yf, pf, hlast = sv[:5]
         i = 5
         wpf = tuple(sv[i:i + nwf])
         i += nwf
@@ -337,13 +339,13 @@ class _ResidualBlockFn(torch.autograd.Function):
             sconv, sbn = shortcut
             ys, ps = sv[i], sv[i + 1]
             wps = tuple(sv[i + 2:i + 2 + nws])
-            dyf, dys, _, g = _bn_backward(P, dout, out, True, training, sync, countf,
+            dyf, dys, _, g = _bn_backward(P, dout, omask, True, training, sync, countf,
                                           yf, pf, fbn, ys, ps, sbn)
             put(sbn.weight, g[2])
             put(sbn.bias, g[3])
             dres = None
         else:
-            dyf, _, dres, g = _bn_backward(P, dout, out, True, training, sync, countf,
+            dyf, _, dres, g = _bn_backward(P, dout, omask, True, training, sync, countf,
                                            yf, pf, fbn, want_dzm=True)
         put(fbn.weight, g[0])
         put(fbn.bias, g[1])
@@ -355,8 +357,8 @@ class _ResidualBlockFn(torch.autograd.Function):
         #     residual/projection path is added in the first stage's dgrad epilogue
         for k in range(nst - 1, -1, -1):
             conv_m, bn = stages[k]
-            hin, wp, y, p, z = recs[k]
-            dy, _, _, g = _bn_backward(P, dh, z, True, training, sync, counts[k], y, p, bn)
+            hin, wp, y, p, zmask = recs[k]
+            dy, _, _, g = _bn_backward(P, dh, zmask, True, training, sync, counts[k], y, p, bn)
             put(bn.weight, g[0])
             put(bn.bias, g[1])
             if k > 0:

@@ -94,26 +94,30 @@ def stats_collapse(a, b=None, count=None, acc_a=None, acc_b=None):
 
 
 def bn_apply(y1, p1, res=None, y2=None, p2=None, relu=True):
-    return _C.bn_apply(y1, p1, res, y2, p2, bool(relu))
+    """-> (out, mask): mask is the ReLU bitmask (uint8 per 8-channel chunk) the
+    backward reads instead of re-reading ``out`` (1/16 of the bytes)."""
+    r = _C.bn_apply(y1, p1, res, y2, p2, bool(relu), True)
+    return (r[0], r[1]) if relu else (r[0], None)
 
 
-def bn_bwd_reduce(dout, out, y, p, relu):
+def bn_bwd_reduce(dout, mask, y, p, relu):
     buf = _acquire(y.shape[-1], y.device)
-    return _C.bn_bwd_reduce(dout, out, y, p, bool(relu), buf)
+    return _C.bn_bwd_reduce(dout, mask, y, p, bool(relu), buf)
 
 
-def bn_bwd_elemt(dout, out, y, p, gamma, red, count, relu, want_dzm=False):
+def bn_bwd_elemt(dout, mask, y, p, gamma, red, count, relu, want_dzm=False):
     if torch.is_tensor(count):
-        r = _C.bn_bwd_elemt(dout, out, y, p, gamma.detach(), red, count, 0.0, bool(relu),
+        r = _C.bn_bwd_elemt(dout, mask, y, p, gamma.detach(), red, count, 0.0, bool(relu),
                             bool(want_dzm), False)
     else:
-        r = _C.bn_bwd_elemt(dout, out, y, p, gamma.detach(), red, None, float(count), bool(relu),
+        r = _C.bn_bwd_elemt(dout, mask, y, p, gamma.detach(), red, None, float(count), bool(relu),
                             bool(want_dzm), False)
     return (r[0], r[1]) if want_dzm else (r[0], None)
 
 
-def bn_bwd_elemt_eval(dout, out, p, relu, want_dzm=False):
-    r = _C.bn_bwd_elemt(dout, out, out, p, p[2], None, None, 1.0, bool(relu), bool(want_dzm), True)
+def bn_bwd_elemt_eval(dout, mask, p, relu, want_dzm=False):
+    r = _C.bn_bwd_elemt(dout, mask, dout, p, p[2], None, None, 1.0, bool(relu), bool(want_dzm),
+                        True)
     return (r[0], r[1]) if want_dzm else (r[0], None)
 
 

@@ -124,33 +124,36 @@ def stats_collapse(a, b=None, count=None, acc_a=None, acc_b=None):
 
 
 def bn_apply(y1, p1, res=None, y2=None, p2=None, relu=True):
+    """-> (out, mask); mask = ReLU mask (bool, same shape) or None."""
     o = _f(y1) * p1[2] + p1[3]
     if y2 is not None:
         o = o + _f(y2) * p2[2] + p2[3]
     elif res is not None:
         o = o + _f(res)
+    mask = None
     if relu:
+        mask = o > 0
         o = o.clamp_min(0.0)
-    return o.to(y1.dtype)
+    return o.to(y1.dtype), mask
 
 
-def _dzm(dout, out, relu):
+def _dzm(dout, mask, relu):
     d = _f(dout)
     if relu:
-        d = d * (out > 0)
+        d = d * mask
     return d
 
 
-def bn_bwd_reduce(dout, out, y, p, relu):
+def bn_bwd_reduce(dout, mask, y, p, relu):
     """-> fp32 [2, C]: (sum dzm, sum dzm*xhat), dzm = dout * relu_mask."""
     c = y.shape[-1]
-    d = _dzm(dout, out, relu).reshape(-1, c)
+    d = _dzm(dout, mask, relu).reshape(-1, c)
     xhat = (_f(y).reshape(-1, c) - p[0]) * p[1]
     return torch.stack([d.sum(0), (d * xhat).sum(0)])
 
 
-def bn_bwd_elemt(dout, out, y, p, gamma, red, count, relu, want_dzm=False):
-    d = _dzm(dout, out, relu)
+def bn_bwd_elemt(dout, mask, y, p, gamma, red, count, relu, want_dzm=False):
+    d = _dzm(dout, mask, relu)
     xhat = (_f(y) - p[0]) * p[1]
     cnt = _f(count) if torch.is_tensor(count) else float(count)
     mdy = red[0] / cnt
@@ -159,8 +162,8 @@ def bn_bwd_elemt(dout, out, y, p, gamma, red, count, relu, want_dzm=False):
     return dy, (d.to(y.dtype) if want_dzm else None)
 
 
-def bn_bwd_elemt_eval(dout, out, p, relu, want_dzm=False):
-    d = _dzm(dout, out, relu)
+def bn_bwd_elemt_eval(dout, mask, p, relu, want_dzm=False):
+    d = _dzm(dout, mask, relu)
     dy = (d * p[2]).to(dout.dtype)
     return dy, (d.to(dout.dtype) if want_dzm else None)
 

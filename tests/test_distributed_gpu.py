@@ -64,10 +64,14 @@ def _worker(rank, world, port, out):
     model = build_model("res").cuda()
     x, y = _data()
     per = x.shape[0] // world
-    dp, losses = _steps(model, x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per], comm)
+    dp, losses = _steps(model, x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per], comm,
+                        n=1)
     comm.all_reduce_(losses)
     if rank == 0:
-        torch.save({"state": {k: v.cpu() for k, v in dp.module.state_dict().items()},
+        torch.save({"grads": {n: p.grad.detach().float().cpu() for n, p in
+                              dp.module.named_parameters()},
+                    "buffers": {k: v.cpu() for k, v in dp.module.state_dict().items()
+                                if "running" in k or "num_batches" in k},
                     "loss": (losses / world).cpu()}, out)
     OF.set_bn_sync(None)
     dist.destroy_process_group()
@@ -81,14 +85,21 @@ def test_two_ranks_on_one_gpu_match_single_process(tmp_path):
     torch.manual_seed(0)
     model = build_model("res").cuda()
     x, y = _data()
-    dp, losses = _steps(model, x, y, None)
-    torch.testing.assert_close(got["loss"], losses.cpu(), rtol=2e-2, atol=2e-2)
-    ref = dp.module.state_dict()
-    for k, v in ref.items():
-        g = got["state"][k].float()
-        v = v.float().cpu()
-        if k.endswith("num_batches_tracked"):
-            assert torch.equal(g, v), k
-            continue
-        err = (g - v).abs().max() / v.abs().max().clamp_min(1e-6)
-        assert err < 5e-2, (k, err.item())
+    dp, losses = _steps(model, x, y, None, n=1)
+    torch.testing.assert_close(got["loss"], losses.cpu(), rtol=1e-2, atol=1e-2)
+    # all-reduced (averaged) gradients of the 2-rank step == single-process gradients
+    errs = {}
+    for n, p in dp.module.named_parameters():
+        g, v = got["grads"][n], p.grad.detach().float().cpu()
+        errs[n] = ((g - v).norm() / v.norm().clamp_min(1e-12)).item()
+    bad = {n: e for n, e in errs.items() if e >= 3e-2}
+    assert not bad, f"grad mismatch {bad} (all: {errs})"
+    # SyncBN running statistics are the global-batch ones
+    for k, v in dp.module.state_dict().items():
+        if k in got["buffers"]:
+            g = got["buffers"][k].float()
+            v = v.float().cpu()
+            if k.endswith("num_batches_tracked"):
+                assert torch.equal(g, v), k
+            else:
+                assert (g - v).abs().max() <= 1e-2 * v.abs().max().clamp_min(1e-3), k

@@ -41,6 +41,15 @@ def _close(a, b, rel):
     assert err < rel, f"max rel err {err.item():.3e} >= {rel}"
 
 
+def _close_norm(a, b, rel):
+    """Relative Frobenius error: robust to the handful of elements whose ReLU
+    mask flips between two bf16 roundings of a near-zero pre-activation."""
+    a = a.float()
+    b = b.float()
+    err = (a - b).norm() / b.norm().clamp_min(1e-12)
+    assert err < rel, f"relative L2 err {err.item():.3e} >= {rel}"
+
+
 def _batch_for(h):
     return 2 if h >= 112 else (4 if h >= 28 else 8)
 
@@ -102,19 +111,22 @@ def test_bn_family(mode, C):
         kw = dict(res=res)
     if mode == "two":
         kw = dict(y2=y2, p2=pr)
-    out = HP.bn_apply(y1, p, relu=relu, **kw)
-    outr = TP.bn_apply(y1, pr, relu=relu, **kw)
+    out, mask = HP.bn_apply(y1, p, relu=relu, **kw)
+    outr, maskr = TP.bn_apply(y1, pr, relu=relu, **kw)
     _close(out, outr, 1e-2)
+    if relu:   # bitmask bit k of byte i == element 8i+k > 0
+        bits = (mask.view(-1, 1).int() >> torch.arange(8, device=DEV).view(1, 8)) & 1
+        assert torch.equal(bits.view(M, C).bool(), maskr), "relu bitmask mismatch"
     dout = torch.randn(M, C, device=DEV).to(torch.bfloat16)
-    red = HP.stats_collapse(HP.bn_bwd_reduce(dout, outr, y1, pr, relu)).view(2, C)
-    redr = TP.bn_bwd_reduce(dout, outr, y1, pr, relu)
+    red = HP.stats_collapse(HP.bn_bwd_reduce(dout, mask, y1, pr, relu)).view(2, C)
+    redr = TP.bn_bwd_reduce(dout, maskr, y1, pr, relu)
     _close(red, redr, 1e-3)
-    dy, dzm = HP.bn_bwd_elemt(dout, outr, y1, pr, g, redr, count, relu, want_dzm=True)
-    dyr, dzmr = TP.bn_bwd_elemt(dout, outr, y1, pr, g, redr, count, relu, want_dzm=True)
+    dy, dzm = HP.bn_bwd_elemt(dout, mask, y1, pr, g, redr, count, relu, want_dzm=True)
+    dyr, dzmr = TP.bn_bwd_elemt(dout, maskr, y1, pr, g, redr, count, relu, want_dzm=True)
     _close(dy, dyr, 1e-2)
     _close(dzm, dzmr, 1e-2)
-    dye, _ = HP.bn_bwd_elemt_eval(dout, outr, pr, relu)
-    dyer, _ = TP.bn_bwd_elemt_eval(dout, outr, pr, relu)
+    dye, _ = HP.bn_bwd_elemt_eval(dout, mask, pr, relu)
+    dyer, _ = TP.bn_bwd_elemt_eval(dout, maskr, pr, relu)
     _close(dye, dyer, 1e-2)
     pe = HP.bn_eval_params(rm2, rv2, g, b, 1e-5)
     per = TP.bn_eval_params(rm2, rv2, g, b, 1e-5)
@@ -238,9 +250,9 @@ def test_residual_block_hip_matches_torch_prims(kind):
                      {k: v.clone() for k, v in blk.state_dict().items() if "running" in k})
     h, t = res["hip"], res["torch"]
     _close(h[0], t[0], 2e-2)
-    _close(h[1], t[1], 3e-2)
+    _close_norm(h[1], t[1], 2e-2)
     for k, g in t[2].items():
-        _close(h[2][k], g, 3e-2)
+        _close_norm(h[2][k], g, 2e-2)
     for k, v in t[3].items():
         _close(h[3][k], v, 1e-2)
 
