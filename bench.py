@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--bucket_mb", type=float, default=25.0)
     ap.add_argument("--first_bucket_mb", type=float, default=1.0)
     ap.add_argument("--profile", default="", help="write a torch.profiler table here (rank 0)")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the whole training step (fwd+bwd+SGD) in a HIP graph and replay it "
+                         "(single GPU); each replay is a full step on a freshly generated batch")
     return ap.parse_args()
 
 
@@ -83,6 +86,34 @@ def bench_rank(rank, world, a):
         opt.step()
         return loss
 
+    if a.graph and world == 1:
+        opt.graph_safe()
+        sx, sy = data.batch_at(0)
+
+        def static_step():
+            out = model(sx)
+            loss = OF.cross_entropy(out, sy)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            return loss
+
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(max(a.warmup, 2)):
+                static_step()
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            static_loss = static_step()
+
+        def step(i):
+            x, y = data.batch_at(i)          # fresh on-device batch, copied into the graph inputs
+            sx.copy_(x)
+            sy.copy_(y)
+            graph.replay()
+            return static_loss
     for i in range(a.warmup):
         step(i)
     torch.cuda.synchronize()
@@ -113,7 +144,7 @@ def bench_rank(rank, world, a):
             "config": {"model": "ResNet-50", "global_batch": a.batch * world, "seq_len": None,
                        "image_size": a.image, "per_gpu_batch": a.batch,
                        "parallelism": f"dp{world}", "sync_bn": a.sync_bn == "on" and world > 1,
-                       "bucket_mb": a.bucket_mb},
+                       "bucket_mb": a.bucket_mb, "hip_graph": bool(a.graph and world == 1)},
             "vs_stock_pytorch_rocm": round(ips / (STOCK_IPS_PER_GPU * world), 3),
             "final_loss": round(final_loss, 4),
         }

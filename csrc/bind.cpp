@@ -384,7 +384,7 @@ Tensor xent_bwd(Tensor logits, Tensor target, Tensor lse, Tensor gloss) {
 
 // ------------------------------------------------------------------ optim
 void sgd_(Tensor p, Tensor g, Tensor buf, double lr, double momentum, double wd, double damp,
-          bool nesterov, bool first) {
+          bool nesterov, bool first, c10::optional<Tensor> lr_dev) {
   CHECK_DEV(p); CHECK_F32(p); CHECK_CONT(p);
   CHECK_F32(g); CHECK_CONT(g); CHECK_F32(buf); CHECK_CONT(buf);
   TORCH_CHECK(p.numel() == g.numel() && p.numel() == buf.numel(), "arena sizes differ");
@@ -393,7 +393,8 @@ void sgd_(Tensor p, Tensor g, Tensor buf, double lr, double momentum, double wd,
               reinterpret_cast<uintptr_t>(buf.data_ptr()) % 16 == 0, "arenas must be 16-B aligned");
   c10::DeviceGuard gd(p.device());
   pmd::sgd_launch(p.data_ptr<float>(), g.data_ptr<float>(), buf.data_ptr<float>(), p.numel(), (float)lr,
-                  (float)momentum, (float)wd, (float)damp, nesterov, first, cur_stream());
+                  opt_f32(lr_dev, "lr_dev"), (float)momentum, (float)wd, (float)damp, nesterov, first,
+                  cur_stream());
 }
 
 // ------------------------------------------------------------------- data

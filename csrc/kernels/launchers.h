@@ -48,8 +48,8 @@ int xent_fwd_launch(const float* logits, const long long* target, float* loss, f
                     long long* correct, int N, int V, hipStream_t st);
 int xent_bwd_launch(const float* logits, const long long* target, const float* lse, const float* gloss,
                     float* grad, int N, int V, hipStream_t st);
-int sgd_launch(float* p, const float* g, float* buf, long long n, float lr, float momentum, float wd,
-               float damp, bool nesterov, bool first, hipStream_t st);
+int sgd_launch(float* p, const float* g, float* buf, long long n, float lr, const float* lr_dev,
+               float momentum, float wd, float damp, bool nesterov, bool first, hipStream_t st);
 
 int synth_images_launch(bf16_t* x, long long* labels, int N, int H, int W, int Cp, int Creal,
                         int classes, unsigned long long seed, hipStream_t st);

@@ -207,9 +207,12 @@ __global__ void xent_bwd_kernel(const float* __restrict__ logits, const long lon
 // --------------------------------------------------------------------- sgd
 // torch.optim.SGD: g += wd*p; buf = first ? g : m*buf + (1-damp)*g; g = nesterov ? g + m*buf : buf;
 // p -= lr*g.  One launch over the whole flat arena (vectorised float4 + scalar tail).
+// lr_dev (optional): learning rate read from device memory, so a captured HIP
+// graph of the training step picks up scheduler changes without re-capture.
 __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
-                           long long n, float lr, float momentum, float wd, float damp, int nesterov,
-                           int first) {
+                           long long n, float lr_host, const float* __restrict__ lr_dev,
+                           float momentum, float wd, float damp, int nesterov, int first) {
+  const float lr = lr_dev ? lr_dev[0] : lr_host;
   const long long n4 = n >> 2;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4 + 4; i += stride) {
@@ -293,9 +296,10 @@ int xent_bwd_launch(const float* logits, const long long* target, const float* l
                      target, lse, gloss, grad, N, V);
   return 0;
 }
-int sgd_launch(float* p, const float* g, float* buf, long long n, float lr, float momentum, float wd,
-               float damp, bool nesterov, bool first, hipStream_t st) {
+int sgd_launch(float* p, const float* g, float* buf, long long n, float lr, const float* lr_dev,
+               float momentum, float wd, float damp, bool nesterov, bool first, hipStream_t st) {
   hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n / 4 + 4, 8192)), dim3(256), 0, st, p, g, buf, n, lr,
+                     lr_dev,
                      momentum, wd, damp, nesterov ? 1 : 0, first ? 1 : 0);
   return 0;
 }

@@ -33,17 +33,37 @@ class FusedSGD(torch.optim.Optimizer):
         super().__init__(self.flat.params, defaults)
         self.momentum_arena = torch.zeros_like(self.flat.param_arena)
         self.steps = 0
+        # device-resident learning rate: the SGD kernel reads it, so a captured
+        # HIP graph of the step follows scheduler updates (see graph_safe())
+        self.lr_dev = None
+        self._lr_cached = None
 
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
         g = self.param_groups[0]
         P = prims_for(self.flat.param_arena)
+        if self.lr_dev is not None and not torch.cuda.is_current_stream_capturing():
+            self.sync_lr()
         P.sgd_nesterov_(self.flat.param_arena, self.flat.grad_arena, self.momentum_arena,
                         g["lr"], g["momentum"], g["weight_decay"], g["nesterov"],
-                        self.steps == 0, g["dampening"])
+                        self.steps == 0, g["dampening"], self.lr_dev)
         self.steps += 1
         return loss
+
+    def graph_safe(self):
+        """Switch to the device-resident LR (call before capturing a step)."""
+        if self.lr_dev is None:
+            self.lr_dev = torch.zeros(1, dtype=torch.float32, device=self.flat.device)
+            self._lr_cached = None
+            self.sync_lr()
+        return self
+
+    def sync_lr(self):
+        lr = float(self.param_groups[0]["lr"])
+        if lr != self._lr_cached:
+            self.lr_dev.fill_(lr)
+            self._lr_cached = lr
 
     def zero_grad(self, set_to_none: bool = False):
         # grads are views into the arena: always zero in place

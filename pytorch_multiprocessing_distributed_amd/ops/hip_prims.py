@@ -156,6 +156,6 @@ def correct_count(logits, target):
 
 # -------------------------------------------------------------------- optim
 def sgd_nesterov_(params, grads, bufs, lr, momentum, weight_decay, nesterov, first_step,
-                  dampening=0.0):
+                  dampening=0.0, lr_dev=None):
     _C.sgd_(params, grads, bufs, float(lr), float(momentum), float(weight_decay),
-            float(dampening), bool(nesterov), bool(first_step))
+            float(dampening), bool(nesterov), bool(first_step), lr_dev)

@@ -216,8 +216,10 @@ def correct_count(logits, target):
 
 # -------------------------------------------------------------------- optim
 def sgd_nesterov_(params, grads, bufs, lr, momentum, weight_decay, nesterov, first_step,
-                  dampening=0.0):
+                  dampening=0.0, lr_dev=None):
     """In-place SGD over flat fp32 arenas (torch.optim.SGD semantics)."""
+    if lr_dev is not None:
+        lr = float(lr_dev.item())
     g = grads
     if weight_decay != 0:
         g = g.add(params, alpha=weight_decay)
