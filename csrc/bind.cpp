@@ -428,8 +428,11 @@ Tensor cifar_augment(Tensor data, Tensor idx, int64_t Cp, bool train, int64_t pa
 
 }  // namespace
 
+namespace pmd { void register_runtime(pybind11::module& m); }
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) kernels for pytorch_multiprocessing_distributed_amd";
+  pmd::register_runtime(m);
   m.def("conv_weight_prep", &conv_weight_prep);
   m.def("conv_set_impl", &pmd::conv_set_impl, "0: register-staged operands, 1: LDS-DMA operands");
   m.def("conv_fwd", &conv_fwd);

@@ -66,15 +66,19 @@ def build(force=False, jobs=None, debug=False, verbose=True):
         objs.append(obj)
         if force or _newer([src, *headers], obj):
             jobs_.append(common + ["-c", src, "-o", obj, f"-I{os.path.join(CSRC, 'kernels')}"])
-    bind_src = os.path.join(CSRC, "bind.cpp")
-    bind_obj = os.path.join(BUILD, "bind.cpp.o")
-    objs.append(bind_obj)
-    if force or _newer([bind_src, *headers], bind_obj):
-        jobs_.append(common + [
-            "-x", "hip", "-c", bind_src, "-o", bind_obj, f"-I{CSRC}",
-            *[f"-I{p}" for p in inc], f"-I{sysconfig.get_paths()['include']}",
-            "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
-            f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-Wno-unused-result", "-Wno-deprecated-declarations"])
+    # host TUs that include torch headers: the binding layer + native runtime
+    # (reducer, comm bootstrap); they are host-only C++ compiled by hipcc
+    torch_tus = [os.path.join(CSRC, "bind.cpp")] + sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+    rt_headers = glob.glob(os.path.join(CSRC, "runtime", "*.h"))
+    for src in torch_tus:
+        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if force or _newer([src, *headers, *rt_headers], obj):
+            jobs_.append(common + [
+                "-x", "hip", "-c", src, "-o", obj, f"-I{CSRC}",
+                *[f"-I{p}" for p in inc], f"-I{sysconfig.get_paths()['include']}",
+                "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
+                f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-Wno-unused-result", "-Wno-deprecated-declarations"])
     if jobs_:
         n = jobs or min(len(jobs_), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16)
         if verbose:

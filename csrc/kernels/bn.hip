@@ -100,18 +100,25 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
   }
 }
 
-// red out: [2][C] += (sum dzm, sum dzm*xhat); TPR = C/8 threads per row (<= 256)
+// red out: [slot][2][C] += (sum dzm, sum dzm*xhat).
+// Grid: x = row blocks, y = channel tiles of CT8 = min(C/8, 32) 16-B chunks
+// (256 channels).  A block covers its channel tile for 256/CT8 rows per
+// iteration, two rows in flight per thread; the row-block count is sized so
+// each thread streams ~32 rows -- few enough blocks that the per-block
+// partials (one atomic per channel per block, spread over kStatSlots slot
+// copies) stay far below the streaming cost even at 7x7x2048.
 template <bool RELU>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __restrict__ dout,
                                                             const uint8_t* __restrict__ mask,
                                                             const bf16_t* __restrict__ y,
                                                             const float* __restrict__ params,
-                                                            float* __restrict__ red, int M, int C) {
+                                                            float* __restrict__ red, int M, int C,
+                                                            int CT8) {
   __shared__ float part[256 * 17];
   const int C8 = C >> 3;
   const int tid = threadIdx.x;
-  const int cc = tid % C8;
-  const int rpi = 256 / C8;
+  const int cc = blockIdx.y * CT8 + tid % CT8;
+  const int rpi = 256 / CT8;
   const int c0 = cc * 8;
   float mean[8], inv[8];
   load8f(params + c0, mean);
@@ -119,7 +126,36 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
   float s1[8], s2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
-  for (int row = blockIdx.x * rpi + tid / C8; row < M; row += gridDim.x * rpi) {
+  const int stride = gridDim.x * rpi;
+  int row = blockIdx.x * rpi + tid / CT8;
+  for (; row + stride < M; row += 2 * stride) {
+    const long long i0 = (long long)row * C8 + cc;
+    const long long i1 = i0 + (long long)stride * C8;
+    const uint4 d0 = reinterpret_cast<const uint4*>(dout)[i0];
+    const uint4 d1 = reinterpret_cast<const uint4*>(dout)[i1];
+    const uint4 y0 = reinterpret_cast<const uint4*>(y)[i0];
+    const uint4 y1 = reinterpret_cast<const uint4*>(y)[i1];
+    const uint32_t m0 = RELU ? mask[i0] : 0xffu;
+    const uint32_t m1 = RELU ? mask[i1] : 0xffu;
+    float d[8], v[8];
+    unpack8(d0, d);
+    unpack8(y0, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float dz = ((m0 >> k) & 1u) ? d[k] : 0.f;
+      s1[k] += dz;
+      s2[k] += dz * (v[k] - mean[k]) * inv[k];
+    }
+    unpack8(d1, d);
+    unpack8(y1, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float dz = ((m1 >> k) & 1u) ? d[k] : 0.f;
+      s1[k] += dz;
+      s2[k] += dz * (v[k] - mean[k]) * inv[k];
+    }
+  }
+  if (row < M) {
     const long long i = (long long)row * C8 + cc;
     float d[8], v[8];
     unpack8(reinterpret_cast<const uint4*>(dout)[i], d);
@@ -138,24 +174,14 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
     part[tid * 17 + 8 + k] = s2[k];
   }
   __syncthreads();
-  if (tid < C8) {
-    float a1[8], a2[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) a1[k] = a2[k] = 0.f;
-    for (int rr = 0; rr < rpi; ++rr) {
-      const int t = rr * C8 + tid;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        a1[k] += part[t * 17 + k];
-        a2[k] += part[t * 17 + 8 + k];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float* slot = red + (size_t)(blockIdx.x % kStatSlots) * 2 * C;
-      atomicAdd(slot + c0 + k, a1[k]);
-      atomicAdd(slot + C + c0 + k, a2[k]);
-    }
+  // 16 values per chunk column: thread (col, k) sums one of them over the rpi rows
+  for (int e = tid; e < CT8 * 16; e += 256) {
+    const int col = e >> 4, k = e & 15;
+    float a = 0.f;
+    for (int rr = 0; rr < rpi; ++rr) a += part[(rr * CT8 + col) * 17 + k];
+    const int c = (blockIdx.y * CT8 + col) * 8 + (k & 7);
+    float* slot = red + (size_t)(blockIdx.x % kStatSlots) * 2 * C;
+    atomicAdd(slot + (k < 8 ? 0 : C) + c, a);
   }
 }
 
@@ -330,15 +356,20 @@ int bn_bwd_reduce_launch(const bf16_t* dout, const uint8_t* mask, const bf16_t* 
                          const float* params, float* red, int M, int C, bool relu, hipStream_t st) {
   const int C8 = C / 8;
   if (C % 8 || C8 > 256 || (C8 & (C8 - 1))) return 1;
-  const int rpi = 256 / C8;
-  long long b = ((long long)M + rpi - 1) / rpi;
-  if (b > 1024) b = 1024;
+  const int CT8 = C8 < 32 ? C8 : 32;
+  const int ctiles = C8 / CT8;
+  const int rpi = 256 / CT8;
+  long long b = ((long long)M + rpi * 32 - 1) / (rpi * 32);  // ~32 rows per thread
+  const long long bmax = 1024 / ctiles;
+  if (b > bmax) b = bmax;
+  if (b < 1) b = 1;
+  const dim3 grid((unsigned)b, (unsigned)ctiles);
   if (relu)
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true>), dim3((int)b), dim3(256), 0, st, dout, mask, y,
-                       params, red, M, C);
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true>), grid, dim3(256), 0, st, dout, mask, y, params, red,
+                       M, C, CT8);
   else
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false>), dim3((int)b), dim3(256), 0, st, dout, mask, y,
-                       params, red, M, C);
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false>), grid, dim3(256), 0, st, dout, mask, y, params,
+                       red, M, C, CT8);
   return 0;
 }
 

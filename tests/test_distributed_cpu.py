@@ -24,11 +24,12 @@ def _free_port():
     return p
 
 
-def _run_steps(model, x, y, steps, dp_comm=None, bucket_mb=0.05):
+def _run_steps(model, x, y, steps, dp_comm=None, bucket_mb=0.05, reducer="native", compress="none"):
     from pytorch_multiprocessing_distributed_amd.engine.optim import FusedSGD
     from pytorch_multiprocessing_distributed_amd.ops import functional as OF
     from pytorch_multiprocessing_distributed_amd.parallel.dp import DataParallel
-    dp = DataParallel(model, dp_comm, bucket_mb=bucket_mb, first_bucket_mb=0.01)
+    dp = DataParallel(model, dp_comm, bucket_mb=bucket_mb, first_bucket_mb=0.01, reducer=reducer,
+                      compress=compress)
     opt = FusedSGD(dp, lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
     losses = []
     for _ in range(steps):
@@ -47,7 +48,7 @@ def _data(seed=3):
     return x, y
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, reducer="native", compress="none"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -65,8 +66,9 @@ def _worker(rank, world, port, out_path):
     x, y = _data()
     per = x.shape[0] // world
     dp, losses = _run_steps(model, x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per],
-                            2, comm)
+                            2, comm, reducer=reducer, compress=compress)
     assert len(dp.buckets) > 1
+    assert dp.num_iterations == 2
     gl = [torch.stack(losses)]
     comm.all_reduce_(gl[0])
     if rank == 0:
@@ -77,10 +79,13 @@ def _worker(rank, world, port, out_path):
 
 
 @pytest.mark.slow
-def test_two_rank_step_equals_single_process(tmp_path):
+@pytest.mark.parametrize("reducer", ["native", "python"])
+def test_two_rank_step_equals_single_process(tmp_path, reducer):
+    """Both reducers (C++ ``_C.Reducer`` and the Python one) give the exact
+    global-batch step."""
     from pytorch_multiprocessing_distributed_amd.models import build_model
     out = str(tmp_path / "r0.pt")
-    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), out, reducer), nprocs=2, join=True)
     got = torch.load(out, weights_only=True)
     torch.manual_seed(0)
     ref_model = build_model("res").double()
@@ -92,6 +97,54 @@ def test_two_rank_step_equals_single_process(tmp_path):
     # per-rank mean loss averaged over ranks == global-batch loss
     torch.testing.assert_close(got["loss"], torch.stack(losses), rtol=1e-9, atol=1e-9)
     torch.testing.assert_close(got["grad"], dp.flat.grad_arena, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.slow
+def test_two_rank_bf16_wire_compression(tmp_path):
+    """compress="bf16": buckets travel in bf16, the fp32/fp64 arena receives
+    the average -- equal to the exact step up to bf16 rounding."""
+    from pytorch_multiprocessing_distributed_amd.models import build_model
+    out = str(tmp_path / "r0.pt")
+    mp.spawn(_worker, args=(2, _free_port(), out, "native", "bf16"), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    torch.manual_seed(0)
+    ref_model = build_model("res").double()
+    x, y = _data()
+    dp, _ = _run_steps(ref_model, x, y, 2, None)
+    g, r = got["grad"], dp.flat.grad_arena
+    assert ((g - r).norm() / r.norm()).item() < 5e-2   # 2 steps of bf16-rounded averages
+
+
+def _no_sync_worker(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    from pytorch_multiprocessing_distributed_amd.models import build_model
+    from pytorch_multiprocessing_distributed_amd.ops import functional as OF
+    from pytorch_multiprocessing_distributed_amd.parallel.comm import get_comm
+    from pytorch_multiprocessing_distributed_amd.parallel.dp import DataParallel
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = get_comm()
+    torch.manual_seed(0)
+    dp = DataParallel(build_model("res").double(), comm, bucket_mb=0.05, first_bucket_mb=0.01)
+    x, y = _data(seed=10 + rank)
+    dp.zero_grad()
+    with dp.no_sync():
+        OF.cross_entropy(dp(x[:4]), y[:4]).backward()
+    assert dp.num_iterations == 0                       # nothing was communicated
+    local = dp.flat.grad_arena.clone()
+    other = comm.all_gather(local)
+    assert not torch.equal(other[0], other[1])          # grads still rank-local
+    OF.cross_entropy(dp(x[4:]), y[4:]).backward()       # accumulates, then averages
+    assert dp.num_iterations == 1
+    allg = comm.all_gather(dp.flat.grad_arena.clone())
+    assert torch.equal(allg[0], allg[1])
+    dist.destroy_process_group()
+
+
+@pytest.mark.slow
+def test_no_sync_gradient_accumulation():
+    mp.spawn(_no_sync_worker, args=(2, _free_port()), nprocs=2, join=True)
 
 
 def _fault_worker(rank, world, port):

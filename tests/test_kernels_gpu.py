@@ -259,14 +259,20 @@ def test_residual_block_hip_matches_torch_prims(kind):
 
 def test_resnet50_trains_on_gpu():
     """End-to-end: the fused ResNet-50 (ImageNet stem) on the gfx950 kernels
-    overfits a fixed batch -- loss must drop well below its initial value."""
+    overfits a fixed batch -- loss must drop well below its initial value.
+
+    lr 0.01: at lr >= 0.02 this batch-16 / 64x64 setup is unstable for ANY bf16
+    implementation (bench/dbg_r50.py: the torch reference prims in bf16 and in
+    fp32 spike and stall the same way), and first-step gradients of bf16 vs
+    fp32 torch prims agree only to cosine ~0.2 here -- the net at random init is
+    that sensitive to rounding, so convergence is the meaningful check."""
     from pytorch_multiprocessing_distributed_amd.engine.optim import FusedSGD
     from pytorch_multiprocessing_distributed_amd.models import ResNet50
     from pytorch_multiprocessing_distributed_amd.ops import functional as OF
     from pytorch_multiprocessing_distributed_amd.ops.native import C
     torch.manual_seed(0)
     m = ResNet50(num_classes=10, stem="imagenet").to(DEV)
-    opt = FusedSGD(m, lr=0.05, momentum=0.9, weight_decay=0.0, nesterov=True)
+    opt = FusedSGD(m, lr=0.01, momentum=0.9, weight_decay=0.0, nesterov=True)
     x, _ = C.synth_images(16, 64, 64, 8, 3, 10, 5, 0)
     y = torch.arange(16, device=DEV) % 10
     losses = []
@@ -277,4 +283,4 @@ def test_resnet50_trains_on_gpu():
         opt.step()
         losses.append(loss.item())
     assert all(map(lambda v: v == v, losses)), losses
-    assert losses[-1] < 0.3 * losses[0], losses
+    assert losses[-1] < 0.1 * losses[0], losses
