@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--sync_bn", default="on", choices=["on", "off"])
     ap.add_argument("--bucket_mb", type=float, default=25.0)
     ap.add_argument("--first_bucket_mb", type=float, default=1.0)
+    ap.add_argument("--syncbn_comm", default="auto", choices=["auto", "xgmi", "rccl"],
+                    help="SyncBN statistics transport (auto: one-shot xGMI kernel when W>1)")
+    ap.add_argument("--grad_compress", default="none", choices=["none", "bf16"])
     ap.add_argument("--profile", default="", help="write a torch.profiler table here (rank 0)")
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole training step (fwd+bwd+SGD) in a HIP graph and replay it "
@@ -56,6 +59,7 @@ def parse():
 def bench_rank(rank, world, a):
     from pytorch_multiprocessing_distributed_amd import launch
     from pytorch_multiprocessing_distributed_amd.data.loader import SyntheticImageNet
+    from pytorch_multiprocessing_distributed_amd.engine.train import setup_syncbn
     from pytorch_multiprocessing_distributed_amd.engine.optim import FusedSGD
     from pytorch_multiprocessing_distributed_amd.models import build_model
     from pytorch_multiprocessing_distributed_amd.ops import functional as OF
@@ -70,8 +74,9 @@ def bench_rank(rank, world, a):
     torch.manual_seed(0)
     model = build_model(a.model, num_classes=a.classes, stem="imagenet").to(dev)
     comm = get_comm()
-    OF.set_bn_sync(comm if (comm is not None and a.sync_bn == "on") else None)
-    model = DataParallel(model, comm, bucket_mb=a.bucket_mb, first_bucket_mb=a.first_bucket_mb)
+    setup_syncbn(comm, a.sync_bn, a.syncbn_comm, True)
+    model = DataParallel(model, comm, bucket_mb=a.bucket_mb, first_bucket_mb=a.first_bucket_mb,
+                         compress=a.grad_compress)
     opt = FusedSGD(model, lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
     data = SyntheticImageNet(a.batch, a.image, a.classes, steps=a.warmup + a.steps, device=dev,
                              dtype=torch.bfloat16, cpad=8, seed=rank)
@@ -133,6 +138,8 @@ def bench_rank(rank, world, a):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
     final_loss = float(loss.item())
+    if comm is not None and comm.xgmi is not None:
+        comm.xgmi.check()         # raises if any statistics exchange timed out
     if rank == 0:
         ips = a.batch * world * a.steps / dt
         rec = {
@@ -144,7 +151,10 @@ def bench_rank(rank, world, a):
             "config": {"model": "ResNet-50", "global_batch": a.batch * world, "seq_len": None,
                        "image_size": a.image, "per_gpu_batch": a.batch,
                        "parallelism": f"dp{world}", "sync_bn": a.sync_bn == "on" and world > 1,
-                       "bucket_mb": a.bucket_mb, "hip_graph": bool(a.graph and world == 1)},
+                       "bucket_mb": a.bucket_mb, "hip_graph": bool(a.graph and world == 1),
+                       "syncbn_comm": ("xgmi" if comm is not None and comm.xgmi is not None
+                                       else "rccl" if world > 1 else None),
+                       "grad_compress": a.grad_compress},
             "vs_stock_pytorch_rocm": round(ips / (STOCK_IPS_PER_GPU * world), 3),
             "final_loss": round(final_loss, 4),
         }

@@ -56,4 +56,16 @@ int synth_images_launch(bf16_t* x, long long* labels, int N, int H, int W, int C
 int cifar_augment_launch(const uint8_t* data, const long long* idx, void* out, bool out_bf16, int B,
                          int Cp, bool train, int pad, unsigned long long seed, long long epoch,
                          hipStream_t st);
+
+// One-shot xGMI all-reduce (kernels/xgmi.hip).  Receive-buffer layout per rank:
+// flags [kXgmiMaxRanks][kXgmiMaxBlocks] uint32 (kXgmiFlagBytes), then data
+// [2 parities][world][kXgmiCap] fp32.
+constexpr int kXgmiMaxRanks = 16;
+constexpr int kXgmiChunk = 2048;       // floats per block
+constexpr int kXgmiMaxBlocks = 16;
+constexpr int kXgmiCap = kXgmiChunk * kXgmiMaxBlocks;  // max floats per call
+constexpr int kXgmiFlagBytes = 4096;
+int xgmi_allreduce_launch(float* const* data, uint32_t* const* flags, float* x, int n, int rank,
+                          int world, uint32_t* epochs, uint32_t* err, long long spin_limit,
+                          hipStream_t st);
 }  // namespace pmd

@@ -1,0 +1,102 @@
+// One-shot xGMI all-reduce for small, latency-bound messages (K21).
+//
+// SyncBN issues one tiny all-reduce per BN site per pass (2C+1 floats fwd,
+// 2C bwd; 53+53 per ResNet-50 step, reference main.py:43 ->
+// torch:nn/modules/_functions.py:65-83,155-165), all on the critical path.
+// A ring collective needs 2(W-1) dependent hops; this needs ONE: every rank
+// pushes its vector straight into a slot of every peer's receive buffer
+// over the point-to-point xGMI links, raises a per-peer flag, waits for all
+// W flags of its own buffer, and sums the W slots locally in rank order (so
+// every rank produces bit-identical results).
+//
+// Receive buffers are IPC-mapped, uncached device memory (coherent across
+// the fabric without cache maintenance).  Flags carry a per-block epoch that
+// only increases; slots are double-buffered by epoch parity, which is
+// enough because a rank can run at most one call ahead of any peer (it
+// cannot finish call e+1 before every peer has *started* e+1, i.e. finished
+// reading call e).  Spins are bounded: on timeout the kernel records an
+// error and returns garbage instead of hanging the GPU; the host checks the
+// error word (XgmiComm.check()).
+#include "common.h"
+
+namespace pmd {
+
+struct XgmiPeers {
+  float* data[kXgmiMaxRanks];
+  uint32_t* flags[kXgmiMaxRanks];
+};
+
+__global__ __launch_bounds__(256) void xgmi_allreduce_kernel(XgmiPeers peers, float* __restrict__ x,
+                                                            int n, int rank, int world,
+                                                            uint32_t* __restrict__ epochs,
+                                                            uint32_t* __restrict__ err,
+                                                            long long spin_limit) {
+  __shared__ uint32_t e_sh;
+  const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x;
+  if (tid == 0) {
+    e_sh = epochs[b] + 1;
+    epochs[b] = e_sh;
+  }
+  __syncthreads();
+  const uint32_t e = e_sh;
+  const int p = e & 1;
+  const int lo = b * kXgmiChunk;
+  const int len = min(kXgmiChunk, n - lo);
+  // 1) push my chunk into slot [p][rank] of every rank's receive buffer
+  const size_t my_slot = ((size_t)p * world + rank) * kXgmiCap + lo;
+  const bool vec = ((len & 3) == 0) && ((reinterpret_cast<uintptr_t>(x + lo) & 15) == 0);
+  for (int r = 0; r < world; ++r) {
+    float* dst = peers.data[r] + my_slot;
+    if (vec) {
+      for (int i = tid; i < (len >> 2); i += 256)
+        reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(x + lo)[i];
+    } else {
+      for (int i = tid; i < len; i += 256) dst[i] = x[lo + i];
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  // 2) raise my flag (block b) in every rank's buffer
+  if (tid < world)
+    __hip_atomic_store(peers.flags[tid] + rank * kXgmiMaxBlocks + b, e, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  // 3) wait until every rank's chunk for epoch e has landed in MY buffer
+  if (tid < world) {
+    const uint32_t* f = peers.flags[rank] + tid * kXgmiMaxBlocks + b;
+    long long it = 0;
+    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+      if (++it > spin_limit) {
+        atomicOr(err, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  // 4) sum the W slots in rank order (identical on every rank)
+  const float* mine = peers.data[rank] + (size_t)p * world * kXgmiCap + lo;
+  for (int i = tid; i < len; i += 256) {
+    float s = 0.f;
+    for (int r = 0; r < world; ++r) s += mine[(size_t)r * kXgmiCap + i];
+    x[lo + i] = s;
+  }
+  (void)nb;
+}
+
+int xgmi_allreduce_launch(float* const* data, uint32_t* const* flags, float* x, int n, int rank,
+                          int world, uint32_t* epochs, uint32_t* err, long long spin_limit,
+                          hipStream_t st) {
+  if (world < 1 || world > kXgmiMaxRanks || n < 0 || n > kXgmiCap) return 1;
+  if (n == 0) return 0;
+  XgmiPeers p{};
+  for (int r = 0; r < world; ++r) {
+    p.data[r] = data[r];
+    p.flags[r] = flags[r];
+  }
+  const int nb = (n + kXgmiChunk - 1) / kXgmiChunk;
+  hipLaunchKernelGGL(xgmi_allreduce_kernel, dim3(nb), dim3(256), 0, st, p, x, n, rank, world, epochs,
+                     err, spin_limit);
+  return 0;
+}
+
+}  // namespace pmd

@@ -1,0 +1,135 @@
+// Host side of the one-shot xGMI all-reduce (kernels/xgmi.hip, K21).
+//
+// Each rank owns one receive buffer in uncached device memory
+// (hipExtMallocWithFlags(hipDeviceMallocUncached): peers write it over xGMI
+// and the owner polls it, with no cache maintenance).  Buffers are exported
+// with hipIpcGetMemHandle; the 64-byte handles are exchanged by the Python
+// wrapper through the c10d store (parallel/xgmi.py) and opened here with
+// hipIpcOpenMemHandle, giving every rank the pointer table the kernel writes
+// through.  Everything runs on the caller's current HIP stream; nothing
+// blocks the host except check().
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/core/DeviceGuard.h>
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "kernels/launchers.h"
+
+namespace pmd {
+
+#define HIP_OK(x)                                                                        \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    TORCH_CHECK(e_ == hipSuccess, #x " failed: ", hipGetErrorString(e_));                 \
+  } while (0)
+
+class XgmiComm {
+ public:
+  XgmiComm(int64_t rank, int64_t world, int64_t device, double timeout_s)
+      : rank_(rank), world_(world), device_(device) {
+    TORCH_CHECK(world >= 1 && world <= kXgmiMaxRanks, "xgmi: world size must be 1..", kXgmiMaxRanks);
+    TORCH_CHECK(rank >= 0 && rank < world, "xgmi: bad rank");
+    c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, device));
+    bytes_ = (size_t)kXgmiFlagBytes + sizeof(float) * 2 * (size_t)world * kXgmiCap;
+    HIP_OK(hipExtMallocWithFlags(&buf_, bytes_, hipDeviceMallocUncached));
+    HIP_OK(hipMemset(buf_, 0, bytes_));
+    HIP_OK(hipMalloc(reinterpret_cast<void**>(&epochs_), sizeof(uint32_t) * (kXgmiMaxBlocks + 1)));
+    HIP_OK(hipMemset(epochs_, 0, sizeof(uint32_t) * (kXgmiMaxBlocks + 1)));
+    err_ = epochs_ + kXgmiMaxBlocks;
+    HIP_OK(hipDeviceSynchronize());
+    peers_.assign(world, nullptr);
+    peers_[rank] = buf_;
+    // ~timeout_s at roughly 64 polls per microsecond-ish s_sleep(1) granularity
+    spin_limit_ = static_cast<long long>(timeout_s * 1.0e6);
+  }
+
+  ~XgmiComm() {
+    c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, device_));
+    for (int r = 0; r < world_; ++r)
+      if (r != rank_ && peers_[r]) (void)hipIpcCloseMemHandle(peers_[r]);
+    if (buf_) (void)hipFree(buf_);
+    if (epochs_) (void)hipFree(epochs_);
+  }
+
+  pybind11::bytes handle() {
+    c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, device_));
+    hipIpcMemHandle_t h;
+    HIP_OK(hipIpcGetMemHandle(&h, buf_));
+    return pybind11::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+  }
+
+  void open(const std::vector<std::string>& handles) {
+    TORCH_CHECK(static_cast<int64_t>(handles.size()) == world_, "xgmi: need one handle per rank");
+    c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, device_));
+    for (int r = 0; r < world_; ++r) {
+      if (r == rank_) continue;
+      TORCH_CHECK(handles[r].size() == sizeof(hipIpcMemHandle_t), "xgmi: bad handle size");
+      hipIpcMemHandle_t h;
+      std::memcpy(&h, handles[r].data(), sizeof(h));
+      HIP_OK(hipIpcOpenMemHandle(&peers_[r], h, hipIpcMemLazyEnablePeerAccess));
+    }
+    opened_ = true;
+  }
+
+  // in-place SUM over ranks of a contiguous fp32 GPU tensor (<= capacity())
+  at::Tensor all_reduce_(at::Tensor x) {
+    TORCH_CHECK(opened_ || world_ == 1, "xgmi: open() the peer handles first");
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous(),
+                "xgmi: expects a contiguous fp32 GPU tensor");
+    TORCH_CHECK(x.get_device() == device_, "xgmi: tensor on the wrong device");
+    TORCH_CHECK(x.numel() <= kXgmiCap, "xgmi: message of ", x.numel(), " floats exceeds capacity ",
+                kXgmiCap);
+    float* data[kXgmiMaxRanks];
+    uint32_t* flags[kXgmiMaxRanks];
+    for (int r = 0; r < world_; ++r) {
+      flags[r] = reinterpret_cast<uint32_t*>(peers_[r]);
+      data[r] = reinterpret_cast<float*>(static_cast<char*>(peers_[r]) + kXgmiFlagBytes);
+    }
+    c10::DeviceGuard g(x.device());
+    const int rc = xgmi_allreduce_launch(data, flags, x.data_ptr<float>(), static_cast<int>(x.numel()),
+                                         rank_, world_, epochs_, err_, spin_limit_,
+                                         c10::hip::getCurrentHIPStream().stream());
+    TORCH_CHECK(rc == 0, "xgmi: launch rejected");
+    calls_++;
+    return x;
+  }
+
+  // host-blocking: did any call time out waiting for a peer?
+  bool check() {
+    c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, device_));
+    uint32_t e = 0;
+    HIP_OK(hipMemcpy(&e, err_, sizeof(e), hipMemcpyDeviceToHost));
+    return e == 0;
+  }
+
+  int64_t capacity() const { return kXgmiCap; }
+  int64_t calls() const { return calls_; }
+
+ private:
+  int rank_, world_, device_;
+  size_t bytes_ = 0;
+  void* buf_ = nullptr;
+  uint32_t* epochs_ = nullptr;
+  uint32_t* err_ = nullptr;
+  std::vector<void*> peers_;
+  long long spin_limit_ = 0;
+  bool opened_ = false;
+  int64_t calls_ = 0;
+};
+
+void register_xgmi(pybind11::module& m) {
+  namespace py = pybind11;
+  py::class_<XgmiComm>(m, "XgmiComm")
+      .def(py::init<int64_t, int64_t, int64_t, double>(), py::arg("rank"), py::arg("world"),
+           py::arg("device"), py::arg("timeout_s") = 60.0)
+      .def("handle", &XgmiComm::handle)
+      .def("open", &XgmiComm::open)
+      .def("all_reduce_", &XgmiComm::all_reduce_)
+      .def("check", &XgmiComm::check)
+      .def_property_readonly("capacity", &XgmiComm::capacity)
+      .def_property_readonly("calls", &XgmiComm::calls);
+}
+
+}  // namespace pmd

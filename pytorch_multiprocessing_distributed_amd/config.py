@@ -58,6 +58,13 @@ def build_parser():
                    help="never advance the sampler epoch (reference never calls set_epoch)")
     p.add_argument("--no_plot", action="store_true")
     p.add_argument("--timeout_min", default=30, type=int, help="collective timeout (minutes)")
+    p.add_argument("--syncbn_comm", default="auto", choices=["auto", "xgmi", "rccl"],
+                   help="SyncBN statistics transport: one-shot xGMI IPC kernel or the process "
+                        "group (auto: xgmi on multi-GPU runs)")
+    p.add_argument("--reducer", default="native", choices=["native", "python"],
+                   help="gradient bucket reducer implementation")
+    p.add_argument("--grad_compress", default="none", choices=["none", "bf16"],
+                   help="wire dtype of the gradient all-reduce")
     return p
 
 

@@ -148,6 +148,20 @@ def run_rank(rank, world_size, args):
         launch.shutdown()
 
 
+def setup_syncbn(comm, sync_bn="on", transport="auto", on_gpu=True):
+    """Install the SyncBN communicator.  transport "xgmi" (or "auto" on GPU)
+    maps the one-shot IPC all-reduce for the statistics vectors."""
+    if comm is None or sync_bn != "on":
+        OF.set_bn_sync(None)
+        return None
+    if transport == "xgmi" or (transport == "auto" and on_gpu and comm.backend == "nccl"):
+        if not on_gpu:
+            raise ValueError("--syncbn_comm xgmi needs GPU ranks")
+        comm.enable_xgmi()
+    OF.set_bn_sync(comm)
+    return comm
+
+
 def _run(rank, world_size, args, dev):
     on_gpu = dev.type == "cuda"
     dtype = torch.bfloat16 if (args.dtype == "bf16" or (args.dtype == "auto" and on_gpu)) \
@@ -160,9 +174,11 @@ def _run(rank, world_size, args, dev):
         torch.manual_seed(args.seed)
     model = build_model(args.model, num_classes=args.num_classes, stem=args.stem).to(dev)
     comm = get_comm()
-    OF.set_bn_sync(comm if (comm is not None and args.sync_bn == "on") else None)
+    setup_syncbn(comm, args.sync_bn, getattr(args, "syncbn_comm", "auto"), on_gpu)
     model = DataParallel(model, comm, bucket_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb,
-                         broadcast_buffers=args.broadcast_buffers)
+                         broadcast_buffers=args.broadcast_buffers,
+                         reducer=getattr(args, "reducer", "native"),
+                         compress=getattr(args, "grad_compress", "none"))
     optimizer = FusedSGD(model, lr=args.lr, momentum=args.momentum, weight_decay=args.wd,
                          nesterov=True)
     scheduler = torch.optim.lr_scheduler.MultiStepLR(optimizer, milestones=args.milestone_list,

@@ -134,7 +134,7 @@ def _bn_forward_params(P, y, st, bn, training, sync, y2=None, st2=None, bn2=None
                                         bn2.num_batches_tracked)
         return p1, p2, float(m_local)
     buf = P.stats_collapse(st, st2, float(m_local))
-    sync.all_reduce_(buf)
+    sync.all_reduce_stats_(buf)
     count = buf[-1:]
     p1 = P.bn_finalize(buf[: 2 * c1].view(2, c1), count, bn.weight, bn.bias, bn.eps,
                        bn.running_mean, bn.running_var, bn.momentum, bn.num_batches_tracked)
@@ -171,7 +171,7 @@ def _bn_backward(P, dout, mask, relu, training, sync, count, y1, p1, bn1, y2=Non
     if training:
         if sync is not None:
             red = red.clone()
-            sync.all_reduce_(red)
+            sync.all_reduce_stats_(red)
         dy1, dzm = P.bn_bwd_elemt(dout, mask, y1, p1, bn1.weight, red[:2 * c1].view(2, c1), count,
                                   relu, want_dzm=want_dzm)
         dy2 = None

@@ -28,11 +28,27 @@ class Comm:
         self.backend = dist.get_backend(group)
         # RCCL implements ncclAvg; gloo does not -> pre-scale there
         self.supports_avg = self.backend == "nccl"
+        self.xgmi = None   # one-shot xGMI path for SyncBN statistics (enable_xgmi)
+
+    def enable_xgmi(self, timeout_s: float = 60.0):
+        """Route small fp32 GPU all-reduces (SyncBN statistics) through the
+        one-shot xGMI kernel (parallel/xgmi.py).  Collective: every rank calls it."""
+        from .xgmi import XgmiAllReduce
+        self.xgmi = XgmiAllReduce(self.group, timeout_s)
+        return self.xgmi
 
     # ------------------------------------------------------------ blocking
     def all_reduce_(self, t, op=dist.ReduceOp.SUM):
         dist.all_reduce(t, op=op, group=self.group)
         return t
+
+    def all_reduce_stats_(self, t):
+        """SUM all-reduce of a small statistics vector (SyncBN).  One-shot xGMI
+        kernel when enabled and the message fits, RCCL/gloo otherwise."""
+        x = self.xgmi
+        if x is not None and x.accepts(t):
+            return x.all_reduce_(t)
+        return self.all_reduce_(t)
 
     def broadcast_(self, t, src=0):
         dist.broadcast(t, src=src, group=self.group)

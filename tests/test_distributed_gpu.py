@@ -49,7 +49,7 @@ def _steps(model, x, y, comm, n=2):
     return dp, torch.stack(losses)
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, stats_comm="gloo"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -59,6 +59,8 @@ def _worker(rank, world, port, out):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     comm = get_comm()
+    if stats_comm == "xgmi":
+        comm.enable_xgmi(timeout_s=20.0)     # SyncBN statistics over the one-shot IPC kernel
     OF.set_bn_sync(comm)
     torch.manual_seed(0 if rank == 0 else 77)     # rank 1 starts different: broadcast must fix it
     model = build_model("res").cuda()
@@ -67,6 +69,9 @@ def _worker(rank, world, port, out):
     dp, losses = _steps(model, x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per], comm,
                         n=1)
     comm.all_reduce_(losses)
+    if comm.xgmi is not None:
+        comm.xgmi.check()
+        assert comm.xgmi.calls > 0
     if rank == 0:
         torch.save({"grads": {n: p.grad.detach().float().cpu() for n, p in
                               dp.module.named_parameters()},
@@ -77,10 +82,11 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_two_ranks_on_one_gpu_match_single_process(tmp_path):
+@pytest.mark.parametrize("stats_comm", ["gloo", "xgmi"])
+def test_two_ranks_on_one_gpu_match_single_process(tmp_path, stats_comm):
     from pytorch_multiprocessing_distributed_amd.models import build_model
     out = str(tmp_path / "r0.pt")
-    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), out, stats_comm), nprocs=2, join=True)
     got = torch.load(out, weights_only=True)
     torch.manual_seed(0)
     model = build_model("res").cuda()
