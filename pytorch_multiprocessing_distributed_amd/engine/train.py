@@ -20,6 +20,7 @@ from ..data.cifar import get_cifar10
 from ..data.loader import DeviceLoader, SyntheticImageNet
 from ..models import build_model
 from ..ops import functional as OF
+from ..utils.trace import region
 from ..parallel.comm import get_comm
 from ..parallel.dp import DataParallel
 from ..utils.checkpoint import load_resume, save_model, save_resume
@@ -68,11 +69,16 @@ def train_epoch(loader, model, optimizer, epoch, logger, args, rank, dev, comm=N
     for i, (inp, target) in enumerate(loader):
         data_time.update(time.time() - end)
         launch.maybe_inject_fault(rank, step_offset + i)
-        output = model(inp)
-        loss = OF.cross_entropy(output, target)
+        with region("fwd"):
+            output = model(inp)
+            loss = OF.cross_entropy(output, target)
         optimizer.zero_grad()
-        loss.backward()
-        optimizer.step()
+        with region("bwd"):
+            loss.backward()
+        with region("opt"):
+            optimizer.step()
+        if comm is not None and comm.order_check_every and (step_offset + i) % comm.order_check_every == 0:
+            comm.verify_order(model.collective_signature())
         bsz = inp.size(0)
         images += bsz
         correct = OF.correct_count(output.detach(), target)
@@ -144,6 +150,9 @@ def run_rank(rank, world_size, args):
                               args.master_port, args.timeout_min)
     try:
         _run(rank, world_size, args, dev)
+    except BaseException:
+        launch.abort()          # ncclCommAbort: peers blocked in a collective error out
+        raise
     finally:
         launch.shutdown()
 

@@ -10,6 +10,7 @@
   creates the process group: backend ``"nccl"`` (= RCCL on ROCm, over xGMI)
   with GPUs, ``"gloo"`` on CPU.
 * optional fault injection for tests: ``PMD_FAULT_RANK`` / ``PMD_FAULT_STEP``.
+* :func:`abort` -- communicator abort on a rank failure (peers unblock).
 """
 from __future__ import annotations
 
@@ -61,6 +62,19 @@ def init_process(rank, world_size, backend="auto", device="auto", master_addr=No
 def shutdown():
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()
+
+
+def abort():
+    """Abort the communicators of this rank (RCCL: ``ncclCommAbort``) after a
+    local failure, so peers blocked in a collective fail fast instead of
+    waiting out the collective timeout.  Best effort."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    try:
+        from torch.distributed.distributed_c10d import _abort_process_group
+        _abort_process_group()
+    except Exception:  # noqa: BLE001 -- already failing; never mask the original error
+        pass
 
 
 def run_model(main_fn, world_size, save_path=None, snapshot=None, args=()):

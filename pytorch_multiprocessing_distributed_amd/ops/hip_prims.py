@@ -159,3 +159,15 @@ def sgd_nesterov_(params, grads, bufs, lr, momentum, weight_decay, nesterov, fir
                   dampening=0.0, lr_dev=None):
     _C.sgd_(params, grads, bufs, float(lr), float(momentum), float(weight_decay),
             float(dampening), bool(nesterov), bool(first_step), lr_dev)
+
+
+# ------------------------------------------------------------------- debug
+def _install_sync_debug():
+    from ..utils.trace import sync_debug_enabled, wrap_sync_debug
+    if sync_debug_enabled():
+        names = [n for n, v in globals().items()
+                 if callable(v) and not n.startswith("_") and getattr(v, "__module__", "") == __name__]
+        wrap_sync_debug(globals(), names)
+
+
+_install_sync_debug()

@@ -13,6 +13,8 @@ C9 teardown (main.py:84).
 from __future__ import annotations
 
 import hashlib
+import os
+import zlib
 
 import torch
 import torch.distributed as dist
@@ -29,6 +31,24 @@ class Comm:
         # RCCL implements ncclAvg; gloo does not -> pre-scale there
         self.supports_avg = self.backend == "nccl"
         self.xgmi = None   # one-shot xGMI path for SyncBN statistics (enable_xgmi)
+        # collective-order checker: rolling hash of every collective
+        # issued through this object; verify_order() compares it across ranks
+        self.order_check_every = int(os.environ.get("PMD_CHECK_ORDER", "0"))
+        self._seq = 0
+        self._ncoll = 0
+
+    def _record(self, op, t):
+        key = f"{op}:{t.numel()}:{t.dtype}".encode()
+        self._seq = (self._seq * 1000003 + zlib.crc32(key)) & 0x7FFFFFFFFFFFFFF
+        self._ncoll += 1
+
+    def verify_order(self, extra=()):
+        """Collective: raise if ranks issued different collective sequences since
+        construction (op, size, dtype, in order) -- the classic silent-hang /
+        wrong-result bug of data-parallel code.  ``extra`` folds in sequences
+        issued outside this object (the native reducer's bucket launch order)."""
+        text = f"{self._seq}:{self._ncoll}:{list(extra)}"
+        self.check_same(text, "collective sequence")
 
     def enable_xgmi(self, timeout_s: float = 60.0):
         """Route small fp32 GPU all-reduces (SyncBN statistics) through the
@@ -39,6 +59,7 @@ class Comm:
 
     # ------------------------------------------------------------ blocking
     def all_reduce_(self, t, op=dist.ReduceOp.SUM):
+        self._record("all_reduce", t)
         dist.all_reduce(t, op=op, group=self.group)
         return t
 
@@ -47,14 +68,17 @@ class Comm:
         kernel when enabled and the message fits, RCCL/gloo otherwise."""
         x = self.xgmi
         if x is not None and x.accepts(t):
+            self._record("xgmi_all_reduce", t)
             return x.all_reduce_(t)
         return self.all_reduce_(t)
 
     def broadcast_(self, t, src=0):
+        self._record("broadcast", t)
         dist.broadcast(t, src=src, group=self.group)
         return t
 
     def all_gather(self, t):
+        self._record("all_gather", t)
         out = [torch.empty_like(t) for _ in range(self.world_size)]
         dist.all_gather(out, t, group=self.group)
         return out
@@ -68,6 +92,7 @@ class Comm:
     # --------------------------------------------------------------- async
     def all_reduce_mean_async(self, t):
         """Average ``t`` in place across ranks; returns a Work handle."""
+        self._record("all_reduce_mean", t)
         if self.supports_avg:
             return dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
         t.mul_(1.0 / self.world_size)

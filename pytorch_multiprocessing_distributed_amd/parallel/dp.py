@@ -208,6 +208,12 @@ class DataParallel(nn.Module):
         if self._native is not None:
             self._native.set_enabled(on)
 
+    def collective_signature(self):
+        """Bucket launch order of the last iteration (for Comm.verify_order)."""
+        if self._native is not None:
+            return self._native.last_launch_order()
+        return []
+
     @property
     def num_iterations(self):
         return self._native.iteration if self._native is not None else self.iteration

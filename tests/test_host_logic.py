@@ -175,3 +175,42 @@ def test_augment_reference_semantics():
     for i in range(3):
         if oy[i] < 8:
             assert torch.all(x[i, 0, :, :3] == -1.0)
+
+
+def test_collective_order_checker_detects_divergence():
+    """Comm.verify_order raises when ranks issued different collective sequences."""
+    import torch.multiprocessing as mp
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_order_worker, args=(2, port), nprocs=2, join=True)
+
+
+def _order_worker(rank, world, port):
+    import os
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pytorch_multiprocessing_distributed_amd.parallel.comm import get_comm
+    comm = get_comm()
+    comm.all_reduce_(torch.ones(4))
+    comm.verify_order()                         # identical so far
+    if rank == 1:   # rank 1 "issued" an extra collective (recorded only: a real mismatch hangs)
+        comm._record("all_reduce", torch.ones(5))
+    try:
+        comm.verify_order()
+        raised = False
+    except RuntimeError:
+        raised = True
+    assert raised, "divergent collective sequence not detected"
+    dist.destroy_process_group()
+
+
+def test_roctx_region_noop_without_env():
+    from pytorch_multiprocessing_distributed_amd.utils.trace import region
+    with region("x"):
+        pass
