@@ -52,7 +52,7 @@ def main():
     ap.add_argument("--iters", type=int, default=15)
     ap.add_argument("--json", default="")
     ap.add_argument("--only", default="")
-    ap.add_argument("--impls", default="1", help="conv operand-staging impls to time (0 reg, 1 DMA)")
+    ap.add_argument("--impls", default="5", help="conv staging/pipeline impls to time (see conv_igemm.hip; 5 = per-shape default)")
     ap.add_argument("--no-miopen", action="store_true")
     a = ap.parse_args()
     torch.backends.cudnn.benchmark = True

@@ -434,7 +434,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) kernels for pytorch_multiprocessing_distributed_amd";
   pmd::register_runtime(m);
   m.def("conv_weight_prep", &conv_weight_prep);
-  m.def("conv_set_impl", &pmd::conv_set_impl, "0: register-staged operands, 1: LDS-DMA operands");
+  m.def("conv_set_impl", &pmd::conv_set_impl, "conv staging/pipeline variant 0-4, 5 = per-shape default");
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);

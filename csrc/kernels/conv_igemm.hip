@@ -39,29 +39,51 @@ struct ConvArgs {
   int M, Kg;
 };
 
-constexpr int BK = 64;
-constexpr int LDA = BK + 8;  // padded LDS row (elements)
+constexpr int LDA_REG = 64 + 8;  // padded LDS row of the register-staged path (elements)
 
 // 16 zero bytes: the LDS-DMA source for padded / out-of-range im2col chunks
 __device__ __attribute__((aligned(16))) unsigned char g_zero16[64];
 
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // DMA=true : operands are copied global->LDS by LDS-DMA (global_load_lds_dwordx4,
-//            no VGPR round trip, no ds_write), unpadded 128-B rows with the 16-B
-//            chunk XOR-swizzled by (row & 7) -- the swizzle is applied to the
-//            per-lane SOURCE address because the DMA writes lane-linearly.
-// DMA=false: register staging into 144-B padded rows (the original kernel).
-template <int BM, int BN, bool DGRAD, bool STATS, bool DMA>
+//            no VGPR round trip, no ds_write) into unpadded BK-element rows.  The
+//            DMA writes lane-linearly (lane l -> LDS base + 16 l), so one wave
+//            instruction fills 64/(BK/8) whole rows; the 16-B chunk is
+//            XOR-swizzled on the per-lane SOURCE address so the fragment reads
+//            (ds_read_b128, 16 rows x one chunk per lane group) are conflict-free:
+//              BK=64 (8 chunks/row): phys = chunk ^ (row & 7)
+//              BK=32 (4 chunks/row): phys = chunk ^ ((row >> 2) & 2)
+//            NST-stage ring: NST-1 K-tiles of DMA in flight while one is consumed,
+//            ONE barrier per K-tile (it both publishes tile kt and retires the
+//            reads of the buffer the next DMA overwrites).
+// DMA=false: register staging into 144-B padded rows, 2 stages (BK=64 only).
+template <int BK>
+__device__ __forceinline__ int swz(int row) {
+  if constexpr (BK == 64) return row & 7;
+  else return (row >> 2) & 2;
+}
+
+template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA>
 __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
-  constexpr int PA = BM / 32;        // A rows per thread
-  constexpr int PB = BN / 32;        // B rows per thread
+  static_assert(DMA || (BK == 64 && NST == 2), "register staging: BK=64, 2 stages");
+  constexpr int CH = BK / 8;                      // 16-B chunks per LDS row
+  constexpr int RPI = DMA ? 64 / CH : 32;         // rows per load instruction (wave / block)
+  constexpr int PA = DMA ? BM / (4 * RPI) : BM / 32;  // A load instructions per thread per tile
+  constexpr int PB = DMA ? BN / (4 * RPI) : BN / 32;
+  static_assert(PA >= 1 && PB >= 1, "tile too small for this BK");
+  constexpr int LPT = PA + PB;
   constexpr int MI = BM / 32;        // 16-row MFMA tiles per wave (wave covers BM/2)
   constexpr int NI = BN / 32;        // 16-col MFMA tiles per wave
-  constexpr int LDR = DMA ? BK : LDA;  // LDS row length (elements)
+  constexpr int LDR = DMA ? BK : BK + 8;  // LDS row length (elements)
   constexpr int A_ELEMS = BM * LDR;
   constexpr int B_ELEMS = BN * LDR;
   constexpr int STAGE = A_ELEMS + B_ELEMS;
   constexpr int LDC = BN + 8;
-  constexpr int SMEM_MAIN = 2 * STAGE * 2;
+  constexpr int SMEM_MAIN = NST * STAGE * 2;
   constexpr int SMEM_EPI = BM * LDC * 2;
   constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
   __shared__ __attribute__((aligned(16))) char smem[SMEM + (STATS ? 2 * 2 * BN * 4 : 0)];
@@ -101,12 +123,12 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
 
   // ---- per-thread A-row precompute
   // register staging: thread -> (row rsub + 32 i, chunk tid & 7)
-  // DMA: wave w, instruction i, lane l -> row w*(BM/4) + 8 i + l/8, LDS chunk l&7
-  //      holding logical chunk (l&7) ^ ((l/8)&7)
-  const int chunk = DMA ? ((lane & 7) ^ ((lane >> 3) & 7)) : (tid & 7);
+  // DMA: wave w, instruction i, lane l -> row w*(BM/4) + RPI i + l/CH, LDS chunk l%CH
+  //      holding logical chunk (l%CH) ^ swz(row)
+  const int chunk = DMA ? ((lane % CH) ^ swz<BK>(lane / CH)) : (tid & 7);
   const int rsub = tid >> 3;  // 0..31
-  auto a_row_of = [&](int i) { return DMA ? wid * (BM / 4) + 8 * i + (lane >> 3) : rsub + 32 * i; };
-  auto b_row_of = [&](int i) { return DMA ? wid * (BN / 4) + 8 * i + (lane >> 3) : rsub + 32 * i; };
+  auto a_row_of = [&](int i) { return DMA ? wid * (BM / 4) + RPI * i + lane / CH : rsub + 32 * i; };
+  auto b_row_of = [&](int i) { return DMA ? wid * (BN / 4) + RPI * i + lane / CH : rsub + 32 * i; };
   int a_base[PA], a_h[PA], a_w[PA];
   bool a_ok[PA];
   const int ohw = OHp * OWp;
@@ -137,7 +159,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     b_row[i] = a.wt + (size_t)(b_ok[i] ? nn : 0) * a.Kg;
   }
 
-  uint4 ra[PA], rb[PB];
+  uint4 ra[DMA ? 1 : PA], rb[DMA ? 1 : PB];
   const int nk = (Kgp + BK - 1) / BK;
 
   auto load_tile = [&](int kt, int dbuf) {
@@ -166,7 +188,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
       if constexpr (DMA) {
         const void* src = g_zero16;
         if (ok) src = a.src + (((size_t)(a_base[i] + ih * a.W + iw)) << a.log2Cs) + c;
-        bf16_t* dst = lds + dbuf * STAGE + (wid * (BM / 4) + 8 * i) * LDR;
+        bf16_t* dst = lds + dbuf * STAGE + (wid * (BM / 4) + RPI * i) * LDR;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
       } else {
@@ -182,7 +204,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     for (int i = 0; i < PB; ++i) {
       if constexpr (DMA) {
         const void* src = (b_ok[i] && kok) ? (const void*)(b_row[i] + boff) : (const void*)g_zero16;
-        bf16_t* dst = lds + dbuf * STAGE + A_ELEMS + (wid * (BN / 4) + 8 * i) * LDR;
+        bf16_t* dst = lds + dbuf * STAGE + A_ELEMS + (wid * (BN / 4) + RPI * i) * LDR;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
       } else {
@@ -193,14 +215,16 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     }
   };
   auto store_tile = [&](int buf) {
-    bf16_t* As = lds + buf * STAGE;
-    bf16_t* Bs = As + A_ELEMS;
+    if constexpr (!DMA) {
+      bf16_t* As = lds + buf * STAGE;
+      bf16_t* Bs = As + A_ELEMS;
 #pragma unroll
-    for (int i = 0; i < PA; ++i)
-      *reinterpret_cast<uint4*>(As + (rsub + 32 * i) * LDA + chunk * 8) = ra[i];
+      for (int i = 0; i < PA; ++i)
+        *reinterpret_cast<uint4*>(As + (rsub + 32 * i) * LDA_REG + chunk * 8) = ra[i];
 #pragma unroll
-    for (int i = 0; i < PB; ++i)
-      *reinterpret_cast<uint4*>(Bs + (rsub + 32 * i) * LDA + chunk * 8) = rb[i];
+      for (int i = 0; i < PB; ++i)
+        *reinterpret_cast<uint4*>(Bs + (rsub + 32 * i) * LDA_REG + chunk * 8) = rb[i];
+    }
   };
 
   f32x4 acc[MI][NI];
@@ -210,11 +234,10 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int frow = lane & 15;
-  const int fk = (lane >> 4) * 8;
   // fragment read: row r, logical 16-B chunk q of the current K-step
   auto frag = [&](const bf16_t* base, int r, int q) {
     if constexpr (DMA)
-      return *reinterpret_cast<const bf16x8*>(base + r * LDR + ((q ^ (r & 7)) << 3));
+      return *reinterpret_cast<const bf16x8*>(base + r * LDR + ((q ^ swz<BK>(r)) << 3));
     else
       return *reinterpret_cast<const bf16x8*>(base + r * LDR + (q << 3));
   };
@@ -236,28 +259,32 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
     }
   };
-  (void)fk;
 
   if constexpr (DMA) {
-    // one barrier-protected DMA stage in flight while the other is consumed:
-    //   issue(kt+1) ; wait own DMAs of kt (vmcnt = #DMAs of kt+1) ; barrier ; MFMA(kt) ; barrier
-    if (nk > 0) load_tile(0, 0);
+    // prologue: tiles 0 .. NST-2 in flight
+#pragma unroll
+    for (int t = 0; t < NST - 1; ++t)
+      if (t < nk) load_tile(t, t);
     for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) {
-        load_tile(kt + 1, (kt + 1) & 1);
-        if constexpr (PA + PB == 8)
-          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if constexpr (PA + PB == 6)
-          asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // own DMAs of tile kt done; later tiles (at most NST-2 of them) may still fly
+      const int rem = min(NST - 2, nk - 1 - kt);
+      if constexpr (NST >= 4) {
+        if (rem >= 2) wait_vmcnt<2 * LPT>();
+        else if (rem == 1) wait_vmcnt<LPT>();
+        else wait_vmcnt<0>();
+      } else if constexpr (NST == 3) {
+        if (rem >= 1) wait_vmcnt<LPT>();
+        else wait_vmcnt<0>();
       } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        wait_vmcnt<0>();
       }
-      asm volatile("s_barrier" ::: "memory");
-      compute(kt & 1);
+      // publishes tile kt to all waves AND retires every wave's reads of tile kt-1,
+      // whose buffer the DMA below overwrites
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (kt + NST - 1 < nk) load_tile(kt + NST - 1, (kt + NST - 1) % NST);
+      compute(kt % NST);
     }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   } else {
     if (nk > 0) {
       load_tile(0, 0);
@@ -371,30 +398,47 @@ static int ilog2(int v) {
   return l;
 }
 
-static int g_conv_impl = -1;  // 0 = register staging, 1 = LDS-DMA (default)
+// Operand staging / pipeline variant (conv_set_impl or PMD_CONV_IMPL):
+//   0 register staging, BK=64, 2 stages
+//   1 LDS-DMA BK=64, 2 stages      2 LDS-DMA BK=32, 4 stages
+//   3 LDS-DMA BK=64, 3 stages      4 LDS-DMA BK=32, 3 stages
+//   5 (default) per shape: BK=32/3 stages for short reductions (Kg <= 512: the
+//     prologue/epilogue dominate, a shallower K-tile fills the pipe sooner),
+//     BK=64/2 stages otherwise (fewer barriers per MFMA) -- measured on all 23
+//     ResNet-50 layer shapes x {fwd, dgrad} (profiles/conv_bench_r01_v5_impls.txt).
+static int g_conv_impl = -1;
 
 void conv_set_impl(int impl) { g_conv_impl = impl; }
 
-static bool use_dma() {
+static int conv_impl() {
   if (g_conv_impl < 0) {
     const char* e = getenv("PMD_CONV_IMPL");
-    g_conv_impl = (e && e[0] == '0') ? 0 : 1;
+    g_conv_impl = (e && e[0] >= '0' && e[0] <= '5') ? e[0] - '0' : 5;
   }
-  return g_conv_impl == 1;
+  return g_conv_impl;
 }
 
-template <int BM, int BN, bool DGRAD, bool STATS>
-static void launch_t(const ConvArgs& a, hipStream_t st) {
+template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA>
+static void launch_k(const ConvArgs& a, hipStream_t st) {
   const bool ph2 = DGRAD && a.stride == 2;
   const int Mgrid = ph2 ? a.N * ((a.OH + 1) >> 1) * ((a.OW + 1) >> 1) : a.M;
   const int tiles = ((Mgrid + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
   const int phases = ph2 ? 4 : 1;
-  if (use_dma())
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, DGRAD, STATS, true>), dim3(tiles, phases), dim3(256), 0,
-                       st, a);
-  else
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, DGRAD, STATS, false>), dim3(tiles, phases), dim3(256),
-                       0, st, a);
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, NST, DGRAD, STATS, DMA>), dim3(tiles, phases),
+                     dim3(256), 0, st, a);
+}
+
+template <int BM, int BN, bool DGRAD, bool STATS>
+static void launch_t(const ConvArgs& a, hipStream_t st) {
+  int impl = conv_impl();
+  if (impl == 5) impl = a.Kg <= 512 ? 4 : 1;
+  switch (impl) {
+    case 0: launch_k<BM, BN, 64, 2, DGRAD, STATS, false>(a, st); break;
+    case 1: launch_k<BM, BN, 64, 2, DGRAD, STATS, true>(a, st); break;
+    case 2: launch_k<BM, BN, 32, 4, DGRAD, STATS, true>(a, st); break;
+    case 3: launch_k<BM, BN, 64, 3, DGRAD, STATS, true>(a, st); break;
+    default: launch_k<BM, BN, 32, 3, DGRAD, STATS, true>(a, st); break;
+  }
 }
 
 template <bool DGRAD, bool STATS>

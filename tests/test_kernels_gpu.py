@@ -81,6 +81,37 @@ def test_conv_fwd_dgrad_wgrad(shape):
     _close(dw, dwr, 2e-3)
 
 
+@pytest.mark.parametrize("impl", [0, 1, 3, 4])
+@pytest.mark.parametrize("shape", R50_SHAPES + CIFAR_SHAPES, ids=lambda s: "C%d_H%d_K%d_R%d_s%d" % s)
+def test_conv_pipeline_variants(shape, impl):
+    """Every operand-staging / pipeline variant of the implicit-GEMM kernel
+    (register staging; LDS-DMA with BK 64/32 and 2-4 stages) on fwd + dgrad."""
+    from pytorch_multiprocessing_distributed_amd.ops.native import C as _C
+    HP = _hp()
+    torch.manual_seed(1)
+    C, H, K, R, st = shape
+    pad = R // 2
+    N = _batch_for(H)
+    x = torch.randn(N, H, H, C, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(K, C, R, R, device=DEV) / (C * R * R) ** 0.5).contiguous(
+        memory_format=torch.channels_last)
+    wp = HP.conv_weight(w, torch.bfloat16, C, True)
+    wref = TP.conv_weight(w, torch.bfloat16, C)
+    yr, sr = TP.conv_fwd(x, wref, st, pad, True)
+    dy = torch.randn_like(yr)
+    dxr = TP.conv_dgrad(dy, wref, tuple(x.shape), st, pad)
+    _C.conv_set_impl(impl)
+    try:
+        y, st_ = HP.conv_fwd(x, wp, st, pad, True)
+        dx = HP.conv_dgrad(dy, wp, tuple(x.shape), st, pad)
+        torch.cuda.synchronize()
+    finally:
+        _C.conv_set_impl(5)
+    _close(y, yr, 2e-2)
+    _close(HP.stats_collapse(st_).view(2, -1), sr, 2e-2)
+    _close(dx, dxr, 2e-2)
+
+
 @pytest.mark.parametrize("mode", ["plain", "res", "two", "norelu"])
 @pytest.mark.parametrize("C", [64, 256, 2048])
 def test_bn_family(mode, C):
