@@ -77,7 +77,7 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor wk, int64_t stride, int64_t pad, b
   }
   const int rc = pmd::conv_igemm_launch(bfp(x), bfp(wk), bfp_mut(y),
                                         want_stats ? stats.data_ptr<float>() : nullptr, N, H, W, C, P,
-                                        Q, K, R, S, (int)stride, (int)pad, false, nullptr, cur_stream());
+                                        Q, K, R, S, (int)stride, (int)pad, false, nullptr, nullptr, cur_stream());
   CHECK_RC(rc, "conv_fwd");
   if (want_stats) return {y, stats};
   return {y};
@@ -85,8 +85,13 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor wk, int64_t stride, int64_t pad, b
 
 // dx[N,H,W,Cp] from dy[N,P,Q,K] and wkt[Cp,R,S,K]
 // addend: optional [N,H,W,Cp] bf16 added in the epilogue (dx = dgrad + addend)
+// bn_*: optional fused BN-backward reduce of the output (see pmd::BnReduceArgs);
+// bn_red* are [kStatSlots, 2, C] fp32 slot buffers that receive += the sums.
 Tensor conv_dgrad(Tensor dy, Tensor wkt, int64_t H, int64_t W, int64_t stride, int64_t pad,
-                  c10::optional<Tensor> addend) {
+                  c10::optional<Tensor> addend, c10::optional<Tensor> bn_mask,
+                  c10::optional<Tensor> bn_y0, c10::optional<Tensor> bn_p0,
+                  c10::optional<Tensor> bn_red0, c10::optional<Tensor> bn_y1,
+                  c10::optional<Tensor> bn_p1, c10::optional<Tensor> bn_red1) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONT(dy);
   CHECK_DEV(wkt); CHECK_BF16(wkt); CHECK_CONT(wkt);
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), K = dy.size(3);
@@ -102,10 +107,32 @@ Tensor conv_dgrad(Tensor dy, Tensor wkt, int64_t H, int64_t W, int64_t stride, i
     TORCH_CHECK(addend->sizes() == dx.sizes(), "addend shape");
     add = bfp(*addend);
   }
+  pmd::BnReduceArgs bnr{};
+  const bool fused = bn_red0 && bn_red0->defined();
+  if (fused) {
+    auto chk_set = [&](const c10::optional<Tensor>& y, const c10::optional<Tensor>& p,
+                       const c10::optional<Tensor>& r, int t) {
+      TORCH_CHECK(y && y->defined() && p && p->defined() && r && r->defined(), "bn reduce set incomplete");
+      CHECK_BF16(*y); CHECK_CONT(*y); CHECK_F32(*p); CHECK_F32(*r); CHECK_CONT(*r); CHECK_CONT(*p);
+      TORCH_CHECK(y->sizes() == dx.sizes(), "bn reduce: y must match dx");
+      TORCH_CHECK(p->numel() == 4 * Cp, "bn reduce: params must be [4, C]");
+      TORCH_CHECK(r->numel() == pmd_slots() * 2 * Cp, "bn reduce: red must be [slots, 2, C]");
+      bnr.y[t] = bfp(*y);
+      bnr.p[t] = p->data_ptr<float>();
+      bnr.red[t] = r->data_ptr<float>();
+    };
+    chk_set(bn_y0, bn_p0, bn_red0, 0);
+    if (bn_red1 && bn_red1->defined()) chk_set(bn_y1, bn_p1, bn_red1, 1);
+    if (bn_mask && bn_mask->defined()) {
+      TORCH_CHECK(bn_mask->scalar_type() == torch::kUInt8 && bn_mask->is_contiguous() &&
+                  bn_mask->numel() == dx.numel() / 8, "bn reduce: mask must be uint8 [M, C/8]");
+      bnr.mask = bn_mask->data_ptr<uint8_t>();
+    }
+  }
   // the gathered operand is dy (spatial P x Q, K channels); output spatial is H x W
   const int rc = pmd::conv_igemm_launch(bfp(dy), bfp(wkt), bfp_mut(dx), nullptr, N, P, Q, K, (int)H,
                                         (int)W, Cp, R, S, (int)stride, (int)pad, true, add,
-                                        cur_stream());
+                                        fused ? &bnr : nullptr, cur_stream());
   CHECK_RC(rc, "conv_dgrad");
   return dx;
 }

@@ -33,6 +33,15 @@ struct ConvArgs {
   bf16_t* out;        // [M][Nout]
   float* stats;       // [kStatSlots][2][Nout] or nullptr
   const bf16_t* addend;  // optional [M][Nout] tensor added to the output (grad accumulation)
+  // optional fused BatchNorm-backward reduce over the (final, bf16) output tile
+  // (dgrad of the conv that CONSUMED a BN+ReLU output): per channel n
+  //   red[slot][0][n] += sum dz,  red[slot][1][n] += sum dz * (y - mean) * invstd
+  // with dz = out * relu_bit(mask) -- for up to two BNs sharing the ReLU mask
+  // (block-final BN + projection-shortcut BN).  Replaces a bn_bwd_reduce pass.
+  const uint8_t* bn_mask;
+  const bf16_t* bn_y[2];
+  const float* bn_p[2];  // [4][Nout] (mean, invstd, scale, shift)
+  float* bn_red[2];      // [kStatSlots][2][Nout]
   int N, H, W, Cs, log2Cs;
   int OH, OW;
   int Nout, R, S, stride, log2stride, pad;
@@ -86,6 +95,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
   constexpr int SMEM_MAIN = NST * STAGE * 2;
   constexpr int SMEM_EPI = BM * LDC * 2;
   constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
+  static_assert(SMEM >= 256 * 33 * 4, "LDS too small for the fused BN-reduce partials");
   __shared__ __attribute__((aligned(16))) char smem[SMEM + (STATS ? 2 * 2 * BN * 4 : 0)];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
 
@@ -351,6 +361,29 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     }
   }
   constexpr int CPR = BN / 8;  // 16-B chunks per output row
+  // fused BN-backward reduce: each thread owns one 8-channel chunk column (256 % CPR == 0)
+  const int nbn = (DGRAD && a.bn_red[0]) ? (a.bn_red[1] ? 2 : 1) : 0;
+  float bsum[2][8], bdot[2][8], bmean[2][8], binv[2][8];
+  {
+    const int n = n0 + (tid % CPR) * 8;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        bsum[t][e] = bdot[t][e] = 0.f;
+        bmean[t][e] = binv[t][e] = 0.f;
+      }
+    if (nbn && n < a.Nout) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        if (t < nbn)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            bmean[t][e] = a.bn_p[t][n + e];
+            binv[t][e] = a.bn_p[t][a.Nout + n + e];
+          }
+    }
+  }
   for (int idx = tid; idx < BM * CPR; idx += 256) {
     const int row = idx / CPR, cc = idx % CPR;
     const int m = m0 + row, n = n0 + cc * 8;
@@ -371,6 +404,48 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
         v = pack8(f);
       }
       *reinterpret_cast<uint4*>(a.out + orow * a.Nout + n) = v;
+      if (nbn) {
+        float d[8];
+        unpack8(v, d);
+        const uint32_t mb = a.bn_mask ? a.bn_mask[orow * (a.Nout >> 3) + (n >> 3)] : 0xffu;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[e] = ((mb >> e) & 1u) ? d[e] : 0.f;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          if (t < nbn) {
+            float yv[8];
+            unpack8(*reinterpret_cast<const uint4*>(a.bn_y[t] + orow * a.Nout + n), yv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              bsum[t][e] += d[e];
+              bdot[t][e] += d[e] * (yv[e] - bmean[t][e]) * binv[t][e];
+            }
+          }
+        }
+      }
+    }
+  }
+  if (nbn) {
+    // block-level combine of the 256/CPR threads sharing a chunk column, then one
+    // fp32 atomic per channel per block into a kStatSlots slot (like conv_fwd stats)
+    __syncthreads();  // everyone is done reading Cs
+    float* part = reinterpret_cast<float*>(smem);  // [256][33]
+    for (int t = 0; t < nbn; ++t) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        part[tid * 33 + e] = bsum[t][e];
+        part[tid * 33 + 8 + e] = bdot[t][e];
+      }
+      __syncthreads();
+      for (int q = tid; q < CPR * 16; q += 256) {
+        const int col = q >> 4, k = q & 15;
+        float acc2 = 0.f;
+        for (int r = col; r < 256; r += CPR) acc2 += part[r * 33 + k];
+        const int n = n0 + col * 8 + (k & 7);
+        if (n < a.Nout)
+          atomicAdd(a.bn_red[t] + ((size_t)((m0 / BM) % kStatSlots) * 2 + (k >> 3)) * a.Nout + n, acc2);
+      }
+      __syncthreads();
     }
   }
 }
@@ -452,7 +527,7 @@ static void launch_sel(const ConvArgs& a, hipStream_t st) {
 // Returns 0 on success, nonzero on unsupported shape.
 int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* stats, int N, int H,
                       int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
-                      bool dgrad, const bf16_t* addend, hipStream_t st) {
+                      bool dgrad, const bf16_t* addend, const BnReduceArgs* bnr, hipStream_t st) {
   if (Cs % 8 != 0 || (Cs & (Cs - 1)) != 0) return 1;  // power-of-two channels (>= 8)
   if (Nout % 8 != 0) return 2;
   if (stride != 1 && stride != 2) return 3;
@@ -462,6 +537,21 @@ int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* s
   a.out = out;
   a.stats = stats;
   a.addend = addend;
+  a.bn_mask = nullptr;
+  for (int t = 0; t < 2; ++t) {
+    a.bn_y[t] = nullptr;
+    a.bn_p[t] = nullptr;
+    a.bn_red[t] = nullptr;
+  }
+  if (bnr) {
+    if (!dgrad || !bnr->y[0] || !bnr->p[0] || !bnr->red[0]) return 5;
+    a.bn_mask = bnr->mask;
+    for (int t = 0; t < 2; ++t) {
+      a.bn_y[t] = bnr->y[t];
+      a.bn_p[t] = bnr->p[t];
+      a.bn_red[t] = bnr->red[t];
+    }
+  }
   a.N = N;
   a.H = H;
   a.W = W;

@@ -6,9 +6,17 @@
 namespace pmd {
 typedef unsigned short bf16_t;
 
+// Fused BatchNorm-backward reduce in the dgrad epilogue (see ConvArgs in conv_igemm.hip):
+// mask = ReLU bitmask of the BN output (nullptr: no ReLU); one or two (y, params, red) sets.
+struct BnReduceArgs {
+  const uint8_t* mask;
+  const bf16_t* y[2];
+  const float* p[2];
+  float* red[2];
+};
 int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* stats, int N, int H,
                       int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
-                      bool dgrad, const bf16_t* addend, hipStream_t st);
+                      bool dgrad, const bf16_t* addend, const BnReduceArgs* bnr, hipStream_t st);
 void conv_set_impl(int impl);  // 0 register staging, 1 LDS-DMA
 void conv_weight_prep_launch(const float* w, bf16_t* wk, bf16_t* wkt, int K, int RS, int C, int Cp,
                              hipStream_t st);

@@ -40,7 +40,10 @@ import torch
 
 from . import torch_prims
 
-_state = {"bn_sync": None, "force_torch": os.environ.get("PMD_PRIMS", "") == "torch"}
+_state = {"bn_sync": None, "force_torch": os.environ.get("PMD_PRIMS", "") == "torch",
+          # fuse each BN-backward reduce into the dgrad epilogue that produces its input
+          "fuse_bnred": os.environ.get("PMD_FUSE_BNRED", "1") != "0",
+          "fused_site_hits": 0}
 
 
 def set_bn_sync(comm):
@@ -50,6 +53,11 @@ def set_bn_sync(comm):
 
 def get_bn_sync():
     return _state["bn_sync"]
+
+
+def set_fuse_bn_reduce(flag: bool):
+    """Fuse BN-backward reduces into the producing dgrad epilogues (default on)."""
+    _state["fuse_bnred"] = bool(flag)
 
 
 def force_torch_prims(flag: bool):
@@ -148,11 +156,17 @@ def _bn_forward_params(P, y, st, bn, training, sync, y2=None, st2=None, bn2=None
 
 
 def _bn_backward(P, dout, mask, relu, training, sync, count, y1, p1, bn1, y2=None, p2=None,
-                 bn2=None, want_dzm=False):
+                 bn2=None, want_dzm=False, pre=None):
     """BN(+second BN)(+ReLU) backward. Returns (dy1, dy2, dzm, grads) with
-    grads = [d_g1, d_b1, d_g2, d_b2] for params that were NOT written directly."""
-    r1 = P.bn_bwd_reduce(dout, mask, y1, p1, relu)
-    r2 = P.bn_bwd_reduce(dout, mask, y2, p2, relu) if y2 is not None else None
+    grads = [d_g1, d_b1, d_g2, d_b2] for params that were NOT written directly.
+    ``pre``: the reduce results already produced by the dgrad that computed
+    ``dout`` (fused epilogue), in the order (bn1[, bn2])."""
+    if pre is not None:
+        r1 = pre[0]
+        r2 = pre[1] if y2 is not None else None
+    else:
+        r1 = P.bn_bwd_reduce(dout, mask, y1, p1, relu)
+        r2 = P.bn_bwd_reduce(dout, mask, y2, p2, relu) if y2 is not None else None
     acc1 = _bn_acc(bn1)
     acc2 = _bn_acc(bn2) if bn2 is not None else None
     red = P.stats_collapse(r1, r2, None, acc1, acc2)     # local sums; gamma/beta grads += local
@@ -263,6 +277,41 @@ def conv_bn_act(x, conv_mod, bn, relu=True):
 
 
 # ------------------------------------------------------------ residual block
+class _BnSite:
+    """Hand-off between two consecutive residual blocks for the fused BN reduce:
+    block i (forward) records its final BN(s) (ReLU mask, [(y, params)]); block
+    i+1 (backward) computes d(out_i) with the reduce fused into the same dgrad
+    epilogue and deposits the partial sums; block i (backward) takes them iff
+    the gradient it received IS that tensor (otherwise -- e.g. the output had
+    another consumer and autograd summed gradients -- it recomputes)."""
+
+    __slots__ = ("mask", "sets", "red", "dx_ptr", "dx_shape")
+
+    def __init__(self, mask, sets):
+        self.mask = mask
+        self.sets = sets
+        self.red = None
+        self.dx_ptr = None
+        self.dx_shape = None
+
+    def put(self, dx, red):
+        self.red = red
+        self.dx_ptr = dx.data_ptr()
+        self.dx_shape = tuple(dx.shape)
+
+    def take(self, dout, P):
+        red, self.red = self.red, None
+        if red is None:
+            return None
+        if dout.data_ptr() == self.dx_ptr and tuple(dout.shape) == self.dx_shape:
+            _state["fused_site_hits"] += 1
+            return red
+        rel = getattr(P, "_release", None)
+        if rel is not None:
+            rel(*red)
+        return None
+
+
 class _ResidualBlockFn(torch.autograd.Function):
     """A whole ResNet block as one autograd node.
 
@@ -300,6 +349,15 @@ class _ResidualBlockFn(torch.autograd.Function):
             out, omask = P.bn_apply(yf, pf, x, relu=True)
         ctx.cfg = (cfg, sync, [r[5] for r in recs], countf, len(wpf),
                    0 if wps is None else len(wps), [len(r[1]) for r in recs])
+        # cross-block fusion: the NEXT block's first dgrad computes d(out) and can
+        # reduce this block's final BN(s) in its epilogue.  The site carries what
+        # it needs; the input's site (previous block) is remembered likewise.
+        fuse = _state["fuse_bnred"] and training
+        ctx.in_site = getattr(x, "_pmd_bnsite", None) if fuse else None
+        ctx.out_site = None
+        if fuse:
+            ctx.out_site = _BnSite(omask, [(yf, pf)] + ([(ys, ps)] if shortcut is not None else []))
+            out._pmd_bnsite = ctx.out_site
         # saved: the ReLU bitmasks (not the activations they came from) + conv inputs
         flat = [x, omask, yf, pf, h, *wpf]
         for (hin, wp, y, p, zmask, _) in recs:
@@ -334,23 +392,33 @@ class _ResidualBlockFn(torch.autograd.Function):
             if g is not None:
                 grads[id(p)] = g
 
+        # reduce of the final BN(s), if the next block's dgrad already produced it
+        pre = ctx.out_site.take(dout, P) if ctx.out_site is not None else None
         # --- final BN (+ projection BN) and the residual ReLU
         if shortcut is not None:
             sconv, sbn = shortcut
             ys, ps = sv[i], sv[i + 1]
             wps = tuple(sv[i + 2:i + 2 + nws])
             dyf, dys, _, g = _bn_backward(P, dout, omask, True, training, sync, countf,
-                                          yf, pf, fbn, ys, ps, sbn)
+                                          yf, pf, fbn, ys, ps, sbn, pre=pre)
             put(sbn.weight, g[2])
             put(sbn.bias, g[3])
             dres = None
         else:
             dyf, _, dres, g = _bn_backward(P, dout, omask, True, training, sync, countf,
-                                           yf, pf, fbn, want_dzm=True)
+                                           yf, pf, fbn, want_dzm=True, pre=pre)
         put(fbn.weight, g[0])
         put(fbn.bias, g[1])
+        fuse = _state["fuse_bnred"] and training
+
+        def dgrad_fused(dy_, wp_, shape, stride, pad, rec, addend=None):
+            # dgrad whose output feeds stage rec's BN+ReLU backward: fuse its reduce
+            if not fuse:
+                return P.conv_dgrad(dy_, wp_, shape, stride, pad, addend), None
+            _hin, _wp, y_, p_, z_ = rec
+            return P.conv_dgrad(dy_, wp_, shape, stride, pad, addend, bnred=(z_, [(y_, p_)]))
         # --- final conv
-        dh = P.conv_dgrad(dyf, wpf, tuple(hlast.shape), fconv.stride, fconv.padding)
+        dh, pre_k = dgrad_fused(dyf, wpf, tuple(hlast.shape), fconv.stride, fconv.padding, recs[-1])
         put(fconv.weight, _wgrad(P, dyf, hlast, wpf, fconv.stride, fconv.padding, fconv.weight))
         dx = None
         # --- conv->BN->ReLU stages in reverse; the block-input gradient of the
@@ -358,16 +426,25 @@ class _ResidualBlockFn(torch.autograd.Function):
         for k in range(nst - 1, -1, -1):
             conv_m, bn = stages[k]
             hin, wp, y, p, zmask = recs[k]
-            dy, _, _, g = _bn_backward(P, dh, zmask, True, training, sync, counts[k], y, p, bn)
+            dy, _, _, g = _bn_backward(P, dh, zmask, True, training, sync, counts[k], y, p, bn,
+                                       pre=pre_k)
             put(bn.weight, g[0])
             put(bn.bias, g[1])
             if k > 0:
-                dh = P.conv_dgrad(dy, wp, tuple(hin.shape), conv_m.stride, conv_m.padding)
+                dh, pre_k = dgrad_fused(dy, wp, tuple(hin.shape), conv_m.stride, conv_m.padding,
+                                        recs[k - 1])
             elif ctx.needs_input_grad[1]:
                 addend = dres
                 if shortcut is not None:
                     addend = P.conv_dgrad(dys, wps, tuple(x.shape), sconv.stride, sconv.padding)
-                dx = P.conv_dgrad(dy, wp, tuple(x.shape), conv_m.stride, conv_m.padding, addend)
+                site = ctx.in_site
+                if site is not None:
+                    # d(x) is the previous block's d(out): reduce ITS final BN(s) here
+                    dx, site_red = P.conv_dgrad(dy, wp, tuple(x.shape), conv_m.stride,
+                                                conv_m.padding, addend, bnred=(site.mask, site.sets))
+                    site.put(dx, site_red)
+                else:
+                    dx = P.conv_dgrad(dy, wp, tuple(x.shape), conv_m.stride, conv_m.padding, addend)
             put(conv_m.weight, _wgrad(P, dy, hin, wp, conv_m.stride, conv_m.padding,
                                       conv_m.weight))
         if shortcut is not None:

@@ -46,7 +46,10 @@ def conv_fwd(x, wpack, stride, pad, want_stats):
     return y, stats
 
 
-def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None):
+def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None, bnred=None):
+    """dX (+ addend).  With ``bnred = (mask, [(y, params), ...])`` also returns
+    the BN-backward reduce of the result for each set (the fused form of
+    ``bn_bwd_reduce(dx, mask, y, params, relu=mask is not None)``)."""
     wk = wpack[0]
     n, h, w, c = x_shape
     dx = torch.nn.grad.conv2d_input((n, c, h, w), _f(wk.permute(0, 3, 1, 2)),
@@ -54,7 +57,11 @@ def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None):
     dx = _nhwc(dx)
     if addend is not None:
         dx = dx + _f(addend)
-    return dx.to(dy.dtype)
+    dx = dx.to(dy.dtype)
+    if bnred is None:
+        return dx
+    mask, sets = bnred
+    return dx, [bn_bwd_reduce(dx, mask, y, p, mask is not None) for y, p in sets]
 
 
 def conv_wgrad(dy, x, wk_shape, stride, pad, out=None):

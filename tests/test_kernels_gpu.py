@@ -315,3 +315,38 @@ def test_resnet50_trains_on_gpu():
         losses.append(loss.item())
     assert all(map(lambda v: v == v, losses)), losses
     assert losses[-1] < 0.1 * losses[0], losses
+
+
+@pytest.mark.parametrize("shape", [(64, 56, 256, 1, 1), (128, 28, 128, 3, 1), (256, 28, 512, 1, 2),
+                                   (256, 28, 256, 3, 2), (512, 7, 2048, 1, 1)],
+                         ids=lambda s: "C%d_H%d_K%d_R%d_s%d" % s)
+@pytest.mark.parametrize("two", [False, True])
+def test_dgrad_fused_bn_reduce(shape, two):
+    """BN-backward reduce fused into the dgrad epilogue (one or two BN sets
+    sharing the ReLU mask, with a residual addend) == dgrad then bn_bwd_reduce."""
+    HP = _hp()
+    torch.manual_seed(3)
+    C, H, K, R, st = shape
+    pad = R // 2
+    N = _batch_for(H)
+    x = torch.randn(N, H, H, C, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(K, C, R, R, device=DEV) / (C * R * R) ** 0.5).contiguous(
+        memory_format=torch.channels_last)
+    wp = HP.conv_weight(w, torch.bfloat16, C, True)
+    yconv, _ = HP.conv_fwd(x, wp, st, pad, False)
+    dy = torch.randn_like(yconv)
+    add = torch.randn_like(x)
+    sets = []
+    for _ in range(2 if two else 1):
+        yb = torch.randn_like(x)
+        p = torch.stack([torch.randn(C, device=DEV) * 0.1, torch.rand(C, device=DEV) + 0.5,
+                         torch.rand(C, device=DEV), torch.randn(C, device=DEV)]).contiguous()
+        sets.append((yb, p))
+    _, mask = HP.bn_apply(sets[0][0], sets[0][1], relu=True)
+    dx_f, reds = HP.conv_dgrad(dy, wp, tuple(x.shape), st, pad, add, bnred=(mask, sets))
+    dx = HP.conv_dgrad(dy, wp, tuple(x.shape), st, pad, add)
+    assert torch.equal(dx_f, dx)
+    for (yb, p), r in zip(sets, reds):
+        got = HP.stats_collapse(r).view(2, C)
+        want = TP.bn_bwd_reduce(dx, mask, yb, p, True)
+        _close(got, want, 1e-3)

@@ -132,3 +132,30 @@ def test_flat_arena_views_and_grads():
     assert dp.buckets[0].start == 0 and dp.buckets[-1].end == fp.numel
     for a, b in zip(dp.buckets, dp.buckets[1:]):
         assert a.end == b.start
+
+
+@pytest.mark.parametrize("arch", ["res", "resnet50"])
+def test_fused_bn_reduce_matches_unfused(arch):
+    """BN-backward reduces fused into the dgrad epilogues (intra-block and across
+    blocks through the _BnSite hand-off) give the same gradients as the
+    separate bn_bwd_reduce passes (fp64 torch prims)."""
+    from pytorch_multiprocessing_distributed_amd.models import build_model
+    from pytorch_multiprocessing_distributed_amd.ops import functional as OF
+    grads = {}
+    for fuse in (False, True):
+        OF.set_fuse_bn_reduce(fuse)
+        torch.manual_seed(0)
+        stem = "cifar" if arch == "res" else "imagenet"
+        m = build_model(arch, num_classes=10, stem=stem).double()
+        g = torch.Generator().manual_seed(1)
+        hw = 32 if stem == "cifar" else 64
+        x = torch.randn(4, hw, hw, 3, generator=g, dtype=torch.float64)
+        y = torch.randint(0, 10, (4,), generator=g)
+        hits0 = OF._state["fused_site_hits"]
+        OF.cross_entropy(m(x), y).backward()
+        if fuse:
+            assert OF._state["fused_site_hits"] > hits0     # cross-block hand-off happened
+        grads[fuse] = {n: p.grad.clone() for n, p in m.named_parameters()}
+    OF.set_fuse_bn_reduce(True)
+    for n, g0 in grads[False].items():
+        torch.testing.assert_close(grads[True][n], g0, rtol=1e-9, atol=1e-12, msg=n)
