@@ -453,6 +453,82 @@ Tensor cifar_augment(Tensor data, Tensor idx, int64_t Cp, bool train, int64_t pa
   return out;
 }
 
+// ------------------------------------------------------------------ fp8 (e4m3)
+#define CHECK_U8(t) TORCH_CHECK((t).scalar_type() == torch::kUInt8, #t " must be uint8 (e4m3 bytes)")
+
+Tensor quant_bf16_fp8(Tensor x, Tensor scale, c10::optional<Tensor> amax) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONT(x); CHECK_F32(scale);
+  TORCH_CHECK(x.numel() % 16 == 0, "quant: numel must be a multiple of 16");
+  c10::DeviceGuard g(x.device());
+  Tensor q = torch::empty(x.sizes(), x.options().dtype(torch::kUInt8));
+  float* am = (amax && amax->defined()) ? amax->data_ptr<float>() : nullptr;
+  CHECK_RC(pmd::quant_bf16_fp8_launch(bfp(x), q.data_ptr<uint8_t>(), scale.data_ptr<float>(), am,
+                                      x.numel(), cur_stream()), "quant_bf16_fp8");
+  return q;
+}
+
+Tensor quant_weight_fp8(Tensor w, int64_t cp, Tensor scale, c10::optional<Tensor> amax) {
+  CHECK_DEV(w); CHECK_F32(w); CHECK_F32(scale);
+  TORCH_CHECK(w.dim() == 4, "weight must be [K,C,R,S]");
+  const int K = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(cp >= C && cp % 16 == 0, "fp8 weight: padded channels must be >= C and a multiple of 16");
+  c10::DeviceGuard g(w.device());
+  Tensor wphys = w.permute({0, 2, 3, 1}).contiguous();
+  Tensor q = torch::empty({K, R, S, cp}, w.options().dtype(torch::kUInt8));
+  float* am = (amax && amax->defined()) ? amax->data_ptr<float>() : nullptr;
+  CHECK_RC(pmd::quant_weight_fp8_launch(wphys.data_ptr<float>(), q.data_ptr<uint8_t>(),
+                                        scale.data_ptr<float>(), am, K, R * S, C, (int)cp, cur_stream()),
+           "quant_weight_fp8");
+  return q;
+}
+
+Tensor dequant_fp8(Tensor q, c10::optional<Tensor> inv_scale) {
+  CHECK_DEV(q); CHECK_U8(q); CHECK_CONT(q);
+  c10::DeviceGuard g(q.device());
+  Tensor out = torch::empty(q.sizes(), q.options().dtype(torch::kFloat32));
+  CHECK_RC(pmd::dequant_fp8_launch(q.data_ptr<uint8_t>(), out.data_ptr<float>(),
+                                   (inv_scale && inv_scale->defined()) ? inv_scale->data_ptr<float>() : nullptr,
+                                   q.numel(), cur_stream()), "dequant_fp8");
+  return out;
+}
+
+Tensor fp8_mfma_probe(Tensor A, Tensor Bt) {
+  CHECK_DEV(A); CHECK_U8(A); CHECK_CONT(A); CHECK_U8(Bt); CHECK_CONT(Bt);
+  TORCH_CHECK(A.numel() == 16 * 128 && Bt.numel() == 16 * 128, "probe: A, Bt must be [16,128]");
+  c10::DeviceGuard g(A.device());
+  Tensor C = torch::empty({16, 16}, A.options().dtype(torch::kFloat32));
+  CHECK_RC(pmd::fp8_mfma_probe_launch(A.data_ptr<uint8_t>(), Bt.data_ptr<uint8_t>(), C.data_ptr<float>(),
+                                      cur_stream()), "fp8_mfma_probe");
+  return C;
+}
+
+std::vector<Tensor> conv_fp8_fwd(Tensor xq, Tensor wq, Tensor descale, int64_t stride, int64_t pad,
+                                 bool want_stats, c10::optional<Tensor> stats_buf) {
+  CHECK_DEV(xq); CHECK_U8(xq); CHECK_CONT(xq); CHECK_U8(wq); CHECK_CONT(wq); CHECK_F32(descale);
+  TORCH_CHECK(xq.dim() == 4 && wq.dim() == 4, "fp8 conv: NHWC input and KRSC weight");
+  const int N = xq.size(0), H = xq.size(1), W = xq.size(2), C = xq.size(3);
+  const int K = wq.size(0), R = wq.size(1), S = wq.size(2);
+  TORCH_CHECK(wq.size(3) == C, "fp8 conv: weight channels must match the (padded) input");
+  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
+  c10::DeviceGuard g(xq.device());
+  Tensor y = torch::empty({N, P, Q, K}, xq.options().dtype(torch::kBFloat16));
+  Tensor stats;
+  if (want_stats) {
+    if (stats_buf && stats_buf->defined()) {
+      stats = *stats_buf;
+      TORCH_CHECK(stats.numel() == pmd_slots() * 2 * K, "stats buffer must be [slots, 2, K]");
+    } else {
+      stats = torch::zeros({pmd_slots(), 2, K}, xq.options().dtype(torch::kFloat32));
+    }
+  }
+  CHECK_RC(pmd::conv_fp8_fwd_launch(xq.data_ptr<uint8_t>(), wq.data_ptr<uint8_t>(), bfp_mut(y),
+                                    want_stats ? stats.data_ptr<float>() : nullptr,
+                                    descale.data_ptr<float>(), N, H, W, C, P, Q, K, R, S, (int)stride,
+                                    (int)pad, cur_stream()), "conv_fp8_fwd");
+  if (want_stats) return {y, stats};
+  return {y};
+}
+
 }  // namespace
 
 namespace pmd { void register_runtime(pybind11::module& m); }
@@ -480,4 +556,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sgd_", &sgd_);
   m.def("synth_images", &synth_images);
   m.def("cifar_augment", &cifar_augment);
+  m.def("quant_bf16_fp8", &quant_bf16_fp8);
+  m.def("quant_weight_fp8", &quant_weight_fp8);
+  m.def("dequant_fp8", &dequant_fp8);
+  m.def("fp8_mfma_probe", &fp8_mfma_probe);
+  m.def("conv_fp8_fwd", &conv_fp8_fwd);
 }

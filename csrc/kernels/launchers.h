@@ -65,6 +65,18 @@ int cifar_augment_launch(const uint8_t* data, const long long* idx, void* out, b
                          int Cp, bool train, int pad, unsigned long long seed, long long epoch,
                          hipStream_t st);
 
+// FP8 e4m3 (kernels/fp8.hip)
+int quant_bf16_fp8_launch(const bf16_t* x, uint8_t* q, const float* scale, float* amax, long long n,
+                          hipStream_t st);
+int quant_weight_fp8_launch(const float* w, uint8_t* q, const float* scale, float* amax, int K, int RS,
+                            int C, int Cp, hipStream_t st);
+int dequant_fp8_launch(const uint8_t* q, float* out, const float* inv_scale, long long n, hipStream_t st);
+int fp8_mfma_probe_launch(const uint8_t* A, const uint8_t* Bt, float* C, hipStream_t st);
+// y(bf16) = descale * conv(xq, wq) with e4m3 NHWC input / KRSC weight; optional BN stats slots
+int conv_fp8_fwd_launch(const uint8_t* x, const uint8_t* w, bf16_t* out, float* stats,
+                        const float* descale, int N, int H, int W, int C, int OH, int OW, int K, int R,
+                        int S, int stride, int pad, hipStream_t st);
+
 // One-shot xGMI all-reduce (kernels/xgmi.hip).  Receive-buffer layout per rank:
 // flags [kXgmiMaxRanks][kXgmiMaxBlocks] uint32 (kXgmiFlagBytes), then data
 // [2 parities][world][kXgmiCap] fp32.
