@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--syncbn_comm", default="auto", choices=["auto", "xgmi", "rccl"],
                     help="SyncBN statistics transport (auto: one-shot xGMI kernel when W>1)")
     ap.add_argument("--grad_compress", default="none", choices=["none", "bf16"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
+                    help="fp8 = BASELINE config 5: block-conv forwards on the e4m3 scaled MFMA "
+                         "(delayed per-tensor scaling), everything else bf16/fp32")
     ap.add_argument("--profile", default="", help="write a torch.profiler table here (rank 0)")
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole training step (fwd+bwd+SGD) in a HIP graph and replay it "
@@ -77,6 +80,9 @@ def bench_rank(rank, world, a):
     setup_syncbn(comm, a.sync_bn, a.syncbn_comm, True)
     model = DataParallel(model, comm, bucket_mb=a.bucket_mb, first_bucket_mb=a.first_bucket_mb,
                          compress=a.grad_compress)
+    if a.dtype == "fp8":
+        from pytorch_multiprocessing_distributed_amd.ops.fp8 import Fp8Scaling
+        OF.set_fp8(Fp8Scaling(dev))
     opt = FusedSGD(model, lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
     data = SyntheticImageNet(a.batch, a.image, a.classes, steps=a.warmup + a.steps, device=dev,
                              dtype=torch.bfloat16, cpad=8, seed=rank)
@@ -146,7 +152,7 @@ def bench_rank(rank, world, a):
             "metric": METRIC, "value": round(ips, 1), "unit": "images/sec",
             "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(1000.0 * dt / a.steps, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
             "data": "synthetic (on-device generated ImageNet-shaped batches, random-init weights)",
             "config": {"model": "ResNet-50", "global_batch": a.batch * world, "seq_len": None,
                        "image_size": a.image, "per_gpu_batch": a.batch,

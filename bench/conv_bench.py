@@ -54,6 +54,7 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--impls", default="5", help="conv staging/pipeline impls to time (see conv_igemm.hip; 5 = per-shape default)")
     ap.add_argument("--no-miopen", action="store_true")
+    ap.add_argument("--fp8", action="store_true", help="also time the e4m3 scaled-MFMA forward conv")
     a = ap.parse_args()
     torch.backends.cudnn.benchmark = True
     dev = "cuda"
@@ -89,6 +90,18 @@ def main():
                        if C != 8 else 0.0,
                        timeit(lambda: HP.conv_wgrad(dy, x, tuple(wp[0].shape), st, pad), a.iters))
         t_f, t_d, t_w = per[impls[-1]]
+        f8txt = ""
+        if a.fp8 and C % 16 == 0:
+            sx = torch.tensor([1.0], device=dev)
+            sw = torch.tensor([64.0], device=dev)
+            xq = _C.quant_bf16_fp8(x, sx, None)
+            wq = _C.quant_weight_fp8(w, C, sw, None)
+
+            def f8():
+                yy, ss = HP.conv_fp8_fwd(xq, wq, sx, sw, st, pad, True)
+                HP._release(ss)
+            t8 = timeit(f8, a.iters)
+            f8txt = f"   fp8 fwd {flops / t8 / 1e9:6.0f}"
         # MIOpen (NCHW-shaped channels_last views of the same data)
         xn = x.permute(0, 3, 1, 2)
         wn = w.to(torch.bfloat16)
@@ -108,7 +121,7 @@ def main():
         def cell(k, m):
             ours = "/".join(f"{tf(per[im][k]):.0f}" for im in impls)
             return f"{ours:>9} {tf(m):7.0f}"
-        print(f"{name:>24} | {cell(0, m_f)} | {cell(1, m_d)} | {cell(2, m_w)}", flush=True)
+        print(f"{name:>24} | {cell(0, m_f)} | {cell(1, m_d)} | {cell(2, m_w)}{f8txt}", flush=True)
         tot["ours"] += cnt * (t_f + t_d + t_w)
         tot["miopen"] += cnt * (m_f + m_d + m_w)
         rows.append(dict(shape=name, count=cnt, ms=dict(fwd=t_f, dgrad=t_d, wgrad=t_w),

@@ -1,0 +1,7 @@
+set -o pipefail
+mkdir -p gpurun_out
+export PMD_NO_AUTOBUILD=1
+timeout -k 10 300 python -m pytest tests/test_fp8_gpu.py -x -q > gpurun_out/fp8_tests.log 2>&1 && \
+timeout -k 10 400 python -m pytest tests/ -x -q -m gpu > gpurun_out/gpu_tests.log 2>&1 && \
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --dtype fp8 > gpurun_out/bench_fp8.log 2>&1 && \
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1

@@ -246,8 +246,10 @@ Tensor stats_finalize_local(Tensor slots, double count, Tensor gamma, Tensor bet
 }
 
 // returns {out} or {out, relu_bitmask} (one uint8 per 8-channel chunk) when relu && want_mask
+// q8_scale/q8_amax (optional): also return an e4m3 copy of the output (fp8 conv input)
 std::vector<Tensor> bn_apply(Tensor y1, Tensor p1, c10::optional<Tensor> res, c10::optional<Tensor> y2,
-                             c10::optional<Tensor> p2, bool relu, bool want_mask) {
+                             c10::optional<Tensor> p2, bool relu, bool want_mask,
+                             c10::optional<Tensor> q8_scale, c10::optional<Tensor> q8_amax) {
   CHECK_DEV(y1); CHECK_BF16(y1); CHECK_CONT(y1);
   const int C = y1.size(-1);
   const long long M = y1.numel() / C;
@@ -273,12 +275,24 @@ std::vector<Tensor> bn_apply(Tensor y1, Tensor p1, c10::optional<Tensor> res, c1
   Tensor mask;
   const bool wm = relu && want_mask;
   if (wm) mask = torch::empty({M * (C / 8)}, y1.options().dtype(torch::kUInt8));
+  const bool q8 = q8_scale && q8_scale->defined();
+  Tensor q;
+  if (q8) {
+    TORCH_CHECK(q8_amax && q8_amax->defined(), "fp8 output needs an amax accumulator");
+    CHECK_F32(*q8_scale); CHECK_F32(*q8_amax);
+    TORCH_CHECK(q8_amax->numel() >= 64 && q8_amax->is_contiguous(), "amax must be [64] slots");
+    q = torch::empty(y1.sizes(), y1.options().dtype(torch::kUInt8));
+  }
   const int rc = pmd::bn_apply_launch(bfp(y1), p1.data_ptr<float>(), r, pp2, bfp_mut(out),
                                       wm ? mask.data_ptr<uint8_t>() : nullptr, M, C, mode, relu,
-                                      cur_stream());
+                                      q8 ? q.data_ptr<uint8_t>() : nullptr,
+                                      q8 ? q8_scale->data_ptr<float>() : nullptr,
+                                      q8 ? q8_amax->data_ptr<float>() : nullptr, cur_stream());
   CHECK_RC(rc, "bn_apply");
-  if (wm) return {out, mask};
-  return {out};
+  std::vector<Tensor> ret{out};
+  if (wm) ret.push_back(mask);
+  if (q8) ret.push_back(q);
+  return ret;
 }
 
 const uint8_t* mask_ptr(const c10::optional<Tensor>& mask, long long chunks, bool relu) {
@@ -462,6 +476,7 @@ Tensor quant_bf16_fp8(Tensor x, Tensor scale, c10::optional<Tensor> amax) {
   c10::DeviceGuard g(x.device());
   Tensor q = torch::empty(x.sizes(), x.options().dtype(torch::kUInt8));
   float* am = (amax && amax->defined()) ? amax->data_ptr<float>() : nullptr;
+  TORCH_CHECK(!am || (amax->numel() >= 64 && amax->is_contiguous()), "amax must be [64] slots");
   CHECK_RC(pmd::quant_bf16_fp8_launch(bfp(x), q.data_ptr<uint8_t>(), scale.data_ptr<float>(), am,
                                       x.numel(), cur_stream()), "quant_bf16_fp8");
   return q;
@@ -476,6 +491,7 @@ Tensor quant_weight_fp8(Tensor w, int64_t cp, Tensor scale, c10::optional<Tensor
   Tensor wphys = w.permute({0, 2, 3, 1}).contiguous();
   Tensor q = torch::empty({K, R, S, cp}, w.options().dtype(torch::kUInt8));
   float* am = (amax && amax->defined()) ? amax->data_ptr<float>() : nullptr;
+  TORCH_CHECK(!am || (amax->numel() >= 64 && amax->is_contiguous()), "amax must be [64] slots");
   CHECK_RC(pmd::quant_weight_fp8_launch(wphys.data_ptr<float>(), q.data_ptr<uint8_t>(),
                                         scale.data_ptr<float>(), am, K, R * S, C, (int)cp, cur_stream()),
            "quant_weight_fp8");
@@ -502,9 +518,10 @@ Tensor fp8_mfma_probe(Tensor A, Tensor Bt) {
   return C;
 }
 
-std::vector<Tensor> conv_fp8_fwd(Tensor xq, Tensor wq, Tensor descale, int64_t stride, int64_t pad,
+// sx, sw: device scalars the operands were quantised with (y = conv(xq, wq) / (sx * sw))
+std::vector<Tensor> conv_fp8_fwd(Tensor xq, Tensor wq, Tensor sx, Tensor sw, int64_t stride, int64_t pad,
                                  bool want_stats, c10::optional<Tensor> stats_buf) {
-  CHECK_DEV(xq); CHECK_U8(xq); CHECK_CONT(xq); CHECK_U8(wq); CHECK_CONT(wq); CHECK_F32(descale);
+  CHECK_DEV(xq); CHECK_U8(xq); CHECK_CONT(xq); CHECK_U8(wq); CHECK_CONT(wq); CHECK_F32(sx); CHECK_F32(sw);
   TORCH_CHECK(xq.dim() == 4 && wq.dim() == 4, "fp8 conv: NHWC input and KRSC weight");
   const int N = xq.size(0), H = xq.size(1), W = xq.size(2), C = xq.size(3);
   const int K = wq.size(0), R = wq.size(1), S = wq.size(2);
@@ -523,7 +540,8 @@ std::vector<Tensor> conv_fp8_fwd(Tensor xq, Tensor wq, Tensor descale, int64_t s
   }
   CHECK_RC(pmd::conv_fp8_fwd_launch(xq.data_ptr<uint8_t>(), wq.data_ptr<uint8_t>(), bfp_mut(y),
                                     want_stats ? stats.data_ptr<float>() : nullptr,
-                                    descale.data_ptr<float>(), N, H, W, C, P, Q, K, R, S, (int)stride,
+                                    sx.data_ptr<float>(), sw.data_ptr<float>(), N, H, W, C, P, Q, K, R, S,
+                                    (int)stride,
                                     (int)pad, cur_stream()), "conv_fp8_fwd");
   if (want_stats) return {y, stats};
   return {y};

@@ -60,14 +60,21 @@ __global__ void bn_finalize_kernel(const float* __restrict__ sums, const float* 
 }
 
 // MODE 0: out = act(y1*s1+b1); 1: + res; 2: + y2*s2+b2
-template <int MODE, bool RELU>
+// Q8: also emit an e4m3 copy q = sat(out * qscale) (the fp8 conv's input, BASELINE
+// config 5) and accumulate amax(|out|) for the next step's delayed scale.
+template <int MODE, bool RELU, bool Q8>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ y1,
                                                        const float* __restrict__ p1,
                                                        const bf16_t* __restrict__ r,
                                                        const float* __restrict__ p2,
                                                        bf16_t* __restrict__ out,
                                                        uint8_t* __restrict__ mask_out,
+                                                       uint8_t* __restrict__ q_out,
+                                                       const float* __restrict__ qscale,
+                                                       float* __restrict__ qamax,
                                                        long long nchunk, int C) {
+  float qs = 0.f, qm = 0.f;
+  if (Q8) qs = qscale[0];
   const int C8 = C >> 3;
   const long long start = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long step = (long long)gridDim.x * blockDim.x;
@@ -95,9 +102,26 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
       }
       v[k] = o;
     }
-    reinterpret_cast<uint4*>(out)[i] = pack8(v);
+    const uint4 pk = pack8(v);
+    reinterpret_cast<uint4*>(out)[i] = pk;
     if (RELU && mask_out) mask_out[i] = (uint8_t)bits;
+    if (Q8) {
+      float o[8];
+      unpack8(pk, o);  // quantise the bf16 value the bf16 consumers see
+      // the convert does not saturate (|v| > 448 -> NaN code): clamp with v_med3
+      float c[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) c[k] = __builtin_amdgcn_fmed3f(o[k] * qs, -448.f, 448.f);
+      int w0 = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
+      w0 = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], w0, true);
+      int w1 = __builtin_amdgcn_cvt_pk_fp8_f32(c[4], c[5], 0, false);
+      w1 = __builtin_amdgcn_cvt_pk_fp8_f32(c[6], c[7], w1, true);
+      reinterpret_cast<uint2*>(q_out)[i] = make_uint2((uint32_t)w0, (uint32_t)w1);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) qm = fmaxf(qm, fabsf(o[k]));
+    }
   }
+  if (Q8) block_amax_update(qamax, qm);
 }
 
 // red out: [slot][2][C] += (sum dzm, sum dzm*xhat).
@@ -336,17 +360,23 @@ int bn_finalize_launch(const float* sums, const float* count, const float* gamma
 }
 
 int bn_apply_launch(const bf16_t* y1, const float* p1, const bf16_t* r, const float* p2, bf16_t* out,
-                    uint8_t* mask, long long M, int C, int mode, bool relu, hipStream_t st) {
+                    uint8_t* mask, long long M, int C, int mode, bool relu, uint8_t* q8,
+                    const float* qscale, float* qamax, hipStream_t st) {
   if (C % 8 || (C >> 3) > 256 || ((C >> 3) & ((C >> 3) - 1))) return 1;
+  if (q8 && (!qscale || !qamax)) return 2;
   const long long nchunk = M * (C / 8);
   const int g = ew_grid(nchunk, C / 8);
-#define APPLY(MD, RL) \
-  hipLaunchKernelGGL((bn_apply_kernel<MD, RL>), dim3(g), dim3(256), 0, st, y1, p1, r, p2, out, mask, \
-                     nchunk, C)
-  if (relu) {
-    if (mode == 0) APPLY(0, true); else if (mode == 1) APPLY(1, true); else APPLY(2, true);
+#define APPLY(MD, RL, Q)                                                                              \
+  hipLaunchKernelGGL((bn_apply_kernel<MD, RL, Q>), dim3(g), dim3(256), 0, st, y1, p1, r, p2, out, mask, \
+                     q8, qscale, qamax, nchunk, C)
+  if (q8) {
+    if (!relu) return 3;  // fp8 copies are only made of ReLU outputs (conv inputs)
+    if (mode == 0) APPLY(0, true, true); else if (mode == 1) APPLY(1, true, true); else APPLY(2, true, true);
+  } else if (relu) {
+    if (mode == 0) APPLY(0, true, false); else if (mode == 1) APPLY(1, true, false); else APPLY(2, true, false);
   } else {
-    if (mode == 0) APPLY(0, false); else if (mode == 1) APPLY(1, false); else APPLY(2, false);
+    if (mode == 0) APPLY(0, false, false); else if (mode == 1) APPLY(1, false, false);
+    else APPLY(2, false, false);
   }
 #undef APPLY
   return 0;

@@ -18,6 +18,26 @@ constexpr int kWave = 64;  // CDNA wavefront
 // atomics on the same 2C addresses; stats_collapse sums the slots.
 constexpr int kStatSlots = 64;
 
+// amax of a quantised tensor (fp8 delayed scaling): kAmaxSlots copies per site,
+// one per (block % kAmaxSlots), so thousands of blocks do not serialise on one
+// address; the host-side update takes the max over the slots.
+constexpr int kAmaxSlots = 64;
+
+// block-wide max of a non-negative value -> one atomicMax into slot blockIdx % kAmaxSlots
+// (all threads of the block must call it; blockDim.x <= 1024, multiple of 64)
+__device__ __forceinline__ void block_amax_update(float* slots, float v) {
+  __shared__ float red[16];
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m = red[0];
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) m = fmaxf(m, red[i]);
+    atomicMax(reinterpret_cast<unsigned int*>(slots + (blockIdx.x % kAmaxSlots)), __float_as_uint(m));
+  }
+}
+
 __device__ __forceinline__ float bf2f(bf16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
 
 // round-to-nearest-even; hipcc lowers the cast to v_cvt_pk_bf16_f32 (NaN-safe)

@@ -1,8 +1,9 @@
 // FP8 (OCP e4m3) support for the fp8 training path (BASELINE config 5, K20):
 //   * per-tensor quantisation with delayed scaling: q = sat_e4m3(x * scale),
 //     scale read from device memory (no host sync), amax of the input
-//     accumulated for the NEXT step's scale (atomicMax on the float bits of
-//     |x| -- order-preserving for non-negative floats);
+//     accumulated for the NEXT step's scale: block max, then atomicMax on the
+//     float bits of |x| (order-preserving for non-negative floats) into one of
+//     kAmaxSlots slots per site;
 //   * weight images: fp32 master [K,R,S,C] -> e4m3 [K][R][S][Cp] (+ amax);
 //   * a probe of the v_mfma_scale_f32_16x16x128_f8f6f4 operand lane map,
 //     checked with exact integer data (tests/test_fp8_gpu.py).
@@ -12,10 +13,13 @@ namespace pmd {
 
 typedef __attribute__((ext_vector_type(8))) int i32x8;
 
+// v_cvt_pk_fp8_f32 rounds to nearest even but does NOT saturate: |v| > 448
+// becomes the e4m3fn NaN code.  Clamp first (one v_med3_f32).
+__device__ __forceinline__ float sat_e4m3(float v) { return __builtin_amdgcn_fmed3f(v, -448.f, 448.f); }
+
 __device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d) {
-  // v_cvt_pk_fp8_f32: two floats -> two e4m3 bytes (saturating, RNE) in the word half
-  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(a), sat_e4m3(b), 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(c), sat_e4m3(d), w, true);
   return (uint32_t)w;
 }
 
@@ -23,9 +27,6 @@ __device__ __forceinline__ float fp8_to_f32(uint32_t byte) {
   return __builtin_amdgcn_cvt_f32_fp8((int)byte, 0);
 }
 
-__device__ __forceinline__ void amax_update(float* amax, float v) {
-  atomicMax(reinterpret_cast<unsigned int*>(amax), __float_as_uint(v));
-}
 
 // bf16 [n] (n % 16 == 0) -> e4m3 [n]; amax_in += max |x|
 __global__ __launch_bounds__(256) void quant_bf16_fp8_kernel(const bf16_t* __restrict__ x,
@@ -50,9 +51,7 @@ __global__ __launch_bounds__(256) void quant_bf16_fp8_kernel(const bf16_t* __res
     }
     reinterpret_cast<uint4*>(q)[i] = make_uint4(w[0], w[1], w[2], w[3]);
   }
-  // wave max then one atomic per wave
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-  if ((threadIdx.x & 63) == 0 && amax) amax_update(amax, m);
+  if (amax) block_amax_update(amax, m);
 }
 
 // fp32 master [K][RS][C] (channels_last physical) -> e4m3 [K][RS][Cp] (zero padded)
@@ -67,10 +66,9 @@ __global__ void quant_weight_fp8_kernel(const float* __restrict__ w, uint8_t* __
     const int krs = i / Cp;
     const float v = c < C ? w[(size_t)krs * C + c] : 0.f;
     m = fmaxf(m, fabsf(v));
-    q[i] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(v * s, 0.f, 0, false) & 0xff);
+    q[i] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(v * s), 0.f, 0, false) & 0xff);
   }
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-  if ((threadIdx.x & 63) == 0 && amax) amax_update(amax, m);
+  if (amax) block_amax_update(amax, m);
 }
 
 // e4m3 -> fp32 (tests / debugging)
@@ -119,7 +117,7 @@ int quant_bf16_fp8_launch(const bf16_t* x, uint8_t* q, const float* scale, float
 
 int quant_weight_fp8_launch(const float* w, uint8_t* q, const float* scale, float* amax, int K, int RS,
                             int C, int Cp, hipStream_t st) {
-  hipLaunchKernelGGL(quant_weight_fp8_kernel, dim3(blocks_for((long long)K * RS * Cp, 256)), dim3(256), 0,
+  hipLaunchKernelGGL(quant_weight_fp8_kernel, dim3(blocks_for((long long)K * RS * Cp, 256 * 16)), dim3(256), 0,
                      st, w, q, scale, amax, K, RS, C, Cp);
   return 0;
 }
@@ -153,7 +151,8 @@ struct Fp8ConvArgs {
   const uint8_t* wt;   // e4m3 [K][R][S][C]
   bf16_t* out;         // [M][K]
   float* stats;
-  const float* descale;  // device scalar: 1 / (sx * sw)
+  const float* sx;     // device scalars: the per-tensor scales the operands were quantised with
+  const float* sw;
   int N, H, W, Cs, log2Cs, OH, OW, Nout, R, S, stride, pad, M, Kg;
 };
 
@@ -267,7 +266,7 @@ __global__ __launch_bounds__(256, 2) void conv_fp8_fwd_kernel(Fp8ConvArgs a) {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
   // ---- epilogue: descale, bf16, BN statistics, LDS-staged coalesced stores
-  const float ds = a.descale[0];
+  const float ds = 1.f / (a.sx[0] * a.sw[0]);
   bf16_t* Cs = reinterpret_cast<bf16_t*>(smem);
   const int crow0 = wm * (BM / 2) + (lane >> 4) * 4;
   const int ccol0 = wn * (BN / 2) + (lane & 15);
@@ -324,8 +323,8 @@ __global__ __launch_bounds__(256, 2) void conv_fp8_fwd_kernel(Fp8ConvArgs a) {
   }
 }
 
-int conv_fp8_fwd_launch(const uint8_t* x, const uint8_t* w, bf16_t* out, float* stats,
-                        const float* descale, int N, int H, int W, int C, int OH, int OW, int K, int R,
+int conv_fp8_fwd_launch(const uint8_t* x, const uint8_t* w, bf16_t* out, float* stats, const float* sx,
+                        const float* sw, int N, int H, int W, int C, int OH, int OW, int K, int R,
                         int S, int stride, int pad, hipStream_t st) {
   if (C % 16 != 0 || (C & (C - 1)) != 0) return 1;  // a 16-B chunk = 16 channels of one tap
   if (K % 8 != 0) return 2;
@@ -334,7 +333,8 @@ int conv_fp8_fwd_launch(const uint8_t* x, const uint8_t* w, bf16_t* out, float* 
   a.wt = w;
   a.out = out;
   a.stats = stats;
-  a.descale = descale;
+  a.sx = sx;
+  a.sw = sw;
   a.N = N; a.H = H; a.W = W; a.Cs = C;
   int l = 0;
   while ((1 << l) < C) ++l;

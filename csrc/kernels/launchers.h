@@ -37,8 +37,10 @@ int stats_finalize_local_launch(float* slots, float count, const float* gamma, c
                                 float* params, float* rm, float* rv, long long* nbt, int C, float eps,
                                 float momentum, hipStream_t st);
 // mask: ReLU bitmask, one byte per 8-channel chunk (bit k = element k of the chunk > 0)
+// q8 (optional): e4m3 copy of the output scaled by *qscale, amax(|out|) -> *qamax
 int bn_apply_launch(const bf16_t* y1, const float* p1, const bf16_t* r, const float* p2, bf16_t* out,
-                    uint8_t* mask, long long M, int C, int mode, bool relu, hipStream_t st);
+                    uint8_t* mask, long long M, int C, int mode, bool relu, uint8_t* q8,
+                    const float* qscale, float* qamax, hipStream_t st);
 int bn_bwd_reduce_launch(const bf16_t* dout, const uint8_t* mask, const bf16_t* y,
                          const float* params, float* red, int M, int C, bool relu, hipStream_t st);
 int bn_bwd_elemt_launch(const bf16_t* dout, const uint8_t* mask, const bf16_t* y, const float* params,
@@ -72,9 +74,9 @@ int quant_weight_fp8_launch(const float* w, uint8_t* q, const float* scale, floa
                             int C, int Cp, hipStream_t st);
 int dequant_fp8_launch(const uint8_t* q, float* out, const float* inv_scale, long long n, hipStream_t st);
 int fp8_mfma_probe_launch(const uint8_t* A, const uint8_t* Bt, float* C, hipStream_t st);
-// y(bf16) = descale * conv(xq, wq) with e4m3 NHWC input / KRSC weight; optional BN stats slots
-int conv_fp8_fwd_launch(const uint8_t* x, const uint8_t* w, bf16_t* out, float* stats,
-                        const float* descale, int N, int H, int W, int C, int OH, int OW, int K, int R,
+// y(bf16) = conv(xq, wq) / (sx * sw) with e4m3 NHWC input / KRSC weight; optional BN stats slots
+int conv_fp8_fwd_launch(const uint8_t* x, const uint8_t* w, bf16_t* out, float* stats, const float* sx,
+                        const float* sw, int N, int H, int W, int C, int OH, int OW, int K, int R,
                         int S, int stride, int pad, hipStream_t st);
 
 // One-shot xGMI all-reduce (kernels/xgmi.hip).  Receive-buffer layout per rank:

@@ -197,6 +197,9 @@ class ResNet(nn.Module):
             return self.linear(out)
         if self.nchw_input and x.dim() == 4 and x.shape[1] in (3, 8) and x.shape[-1] not in (3, 8):
             x = x.permute(0, 2, 3, 1).contiguous()
+        f8 = OF.get_fp8()
+        if f8 is not None and self.training and torch.is_grad_enabled():
+            f8.update()                          # delayed scaling: one device op per step
         out = OF.conv_bn_act(x, self.conv1, self.bn1, relu=True)
         if self.stem == "imagenet":
             out = OF.max_pool3x3s2(out)

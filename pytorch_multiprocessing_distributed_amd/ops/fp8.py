@@ -1,0 +1,68 @@
+"""FP8 (OCP e4m3) training precision -- BASELINE config 5.
+
+Recipe ("fp8 weights + activations" for the convolution GEMMs):
+  * every block convolution's FORWARD runs on the CDNA4 scaled fp8 MFMA
+    (``v_mfma_scale_f32_16x16x128_f8f6f4``, 2x the bf16 rate): its weight is
+    quantised per step from the fp32 master into an e4m3 KRSC image, its input
+    activation is the e4m3 copy that the producing BN-apply kernel writes next
+    to the bf16 one (no extra pass);
+  * per-tensor *delayed* scaling: each site (weight / activation) owns a scale
+    and an amax in two flat device buffers; kernels accumulate amax while they
+    quantise, and ``Fp8Scaling.update()`` (once per training step, one fused
+    device op, no host sync) turns last step's amax into this step's scale
+    ``448 / amax``;
+  * the stem conv, the classifier, BatchNorm, the loss and every backward GEMM
+    stay in bf16 / fp32 (fp32 master weights, reference checkpoint format
+    unchanged).
+"""
+from __future__ import annotations
+
+import torch
+
+E4M3_MAX = 448.0
+AMAX_SLOTS = 64     # == kAmaxSlots (csrc/kernels/common.h)
+
+
+class Fp8Scaling:
+    def __init__(self, device, capacity: int = 1024, margin: float = 1.0):
+        self.device = torch.device(device)
+        # [site][slot]: kernels atomicMax into slot (block % 64) -- no single-address contention
+        self.amax = torch.zeros(capacity, AMAX_SLOTS, dtype=torch.float32, device=self.device)
+        self.scale = torch.ones(capacity, dtype=torch.float32, device=self.device)
+        self.capacity = capacity
+        self.margin = float(margin)
+        self.sites: dict = {}
+        self.steps = 0
+
+    def site(self, key, init_from: torch.Tensor | None = None):
+        """(scale [1], amax [64 slots]) views for ``key``; a new weight site takes
+        its first scale from the tensor's current amax (device op, no sync)."""
+        idx = self.sites.get(key)
+        if idx is None:
+            idx = len(self.sites)
+            if idx >= self.capacity:
+                raise RuntimeError("Fp8Scaling capacity exceeded")
+            self.sites[key] = idx
+            if init_from is not None:
+                a = init_from.detach().abs().max().float().clamp_min(1e-12)
+                self.scale[idx:idx + 1].copy_((E4M3_MAX / self.margin) / a)
+        return self.scale[idx:idx + 1], self.amax[idx]
+
+    @torch.no_grad()
+    def update(self):
+        """Delayed scaling: scale <- 448 / amax(previous step) where observed; amax <- 0."""
+        n = len(self.sites)
+        if n == 0:
+            return
+        a = self.amax[:n].amax(dim=1)
+        s = self.scale[:n]
+        torch.where(a > 0, (E4M3_MAX / self.margin) / a.clamp_min(1e-12), s, out=s)
+        self.amax[:n].zero_()
+        self.steps += 1
+
+    def amax_of(self, key):
+        """Current-step amax of a site (max over its slots)."""
+        return self.amax[self.sites[key]].max()
+
+    def state_dict(self):
+        return {"scale": self.scale.cpu(), "amax": self.amax.amax(dim=1).cpu(), "sites": len(self.sites)}

@@ -40,10 +40,13 @@ import torch
 
 from . import torch_prims
 
+_NAN_CHECK = os.environ.get("PMD_NAN_CHECK", "0") == "1"   # debug: finite-check block backward
+
 _state = {"bn_sync": None, "force_torch": os.environ.get("PMD_PRIMS", "") == "torch",
           # fuse each BN-backward reduce into the dgrad epilogue that produces its input
           "fuse_bnred": os.environ.get("PMD_FUSE_BNRED", "1") != "0",
-          "fused_site_hits": 0}
+          "fused_site_hits": 0,
+          "fp8": None}          # Fp8Scaling when the block convs run in fp8 (config 5)
 
 
 def set_bn_sync(comm):
@@ -53,6 +56,30 @@ def set_bn_sync(comm):
 
 def get_bn_sync():
     return _state["bn_sync"]
+
+
+def set_fp8(scaling):
+    """Install an :class:`ops.fp8.Fp8Scaling` (block convolutions' forward in fp8
+    on the gfx950 path) or ``None`` for bf16."""
+    _state["fp8"] = scaling
+
+
+def get_fp8():
+    return _state["fp8"]
+
+
+def _fp8_for(P):
+    f = _state["fp8"]
+    return f if (f is not None and getattr(P, "SUPPORTS_FP8", False)) else None
+
+
+def _conv_fwd_any(P, f8, h, hq, wp, conv_m, want_stats):
+    """bf16 conv, or the fp8 one when ``hq = (e4m3 input, scale)`` is given."""
+    if f8 is None or hq is None:
+        return P.conv_fwd(h, wp, conv_m.stride, conv_m.padding, want_stats)
+    sw, aw = f8.site(("w", id(conv_m)), init_from=conv_m.weight)
+    wq = P.quant_weight_fp8(conv_m.weight, h.shape[-1], sw, aw)
+    return P.conv_fp8_fwd(hq[0], wq, hq[1], sw, conv_m.stride, conv_m.padding, want_stats)
 
 
 def set_fuse_bn_reduce(flag: bool):
@@ -325,28 +352,49 @@ class _ResidualBlockFn(torch.autograd.Function):
         stages, final, shortcut, training = cfg
         P = prims_for(x)
         sync = _state["bn_sync"] if training else None
+        f8 = _fp8_for(P)
+        hq = None
+        if f8 is not None:
+            # e4m3 copy of the block input: written by the previous block's BN-apply,
+            # else quantised here (first block: the max-pool output)
+            hq = getattr(x, "_pmd_q8", None)
+            if hq is not None:
+                x._pmd_q8 = None                # consumed: do not keep it alive with x
+            else:
+                sx, ax = f8.site(("in", id(stages[0][0])))
+                hq = (P.quant_bf16_fp8(x, sx, ax), sx)
+        xq = hq
         h = x
         recs = []
         for conv_m, bn in stages:
             wp = P.conv_weight(conv_m.weight, x.dtype, h.shape[-1], True)
-            y, st = P.conv_fwd(h, wp, conv_m.stride, conv_m.padding, training)
+            y, st = _conv_fwd_any(P, f8, h, hq, wp, conv_m, training)
             p, _, count = _bn_forward_params(P, y, st, bn, training, sync)
-            z, zmask = P.bn_apply(y, p, relu=True)
+            if f8 is not None:
+                site = f8.site(("a", id(bn)))
+                z, zmask, zq = P.bn_apply(y, p, relu=True, fp8=site)
+                hq = (zq, site[0])
+            else:
+                z, zmask = P.bn_apply(y, p, relu=True)
             recs.append((h, wp, y, p, zmask, count))
             h = z
         fconv, fbn = final
         wpf = P.conv_weight(fconv.weight, x.dtype, h.shape[-1], True)
-        yf, stf = P.conv_fwd(h, wpf, fconv.stride, fconv.padding, training)
+        yf, stf = _conv_fwd_any(P, f8, h, hq, wpf, fconv, training)
+        osite = f8.site(("a", id(fbn))) if f8 is not None else None
         if shortcut is not None:
             sconv, sbn = shortcut
             wps = P.conv_weight(sconv.weight, x.dtype, x.shape[-1], x.requires_grad)
-            ys, sts = P.conv_fwd(x, wps, sconv.stride, sconv.padding, training)
+            ys, sts = _conv_fwd_any(P, f8, x, xq, wps, sconv, training)
             pf, ps, countf = _bn_forward_params(P, yf, stf, fbn, training, sync, ys, sts, sbn)
-            out, omask = P.bn_apply(yf, pf, None, ys, ps, relu=True)
+            r = P.bn_apply(yf, pf, None, ys, ps, relu=True, **({"fp8": osite} if osite else {}))
         else:
             wps = None
             pf, _, countf = _bn_forward_params(P, yf, stf, fbn, training, sync)
-            out, omask = P.bn_apply(yf, pf, x, relu=True)
+            r = P.bn_apply(yf, pf, x, relu=True, **({"fp8": osite} if osite else {}))
+        out, omask = r[0], r[1]
+        if osite is not None:
+            out._pmd_q8 = (r[2], osite[0])      # the next block's fp8 conv input
         ctx.cfg = (cfg, sync, [r[5] for r in recs], countf, len(wpf),
                    0 if wps is None else len(wps), [len(r[1]) for r in recs])
         # cross-block fusion: the NEXT block's first dgrad computes d(out) and can
@@ -387,6 +435,12 @@ class _ResidualBlockFn(torch.autograd.Function):
         dout = dout.contiguous()
         fconv, fbn = final
         grads = {}
+        nan_check = _NAN_CHECK
+
+        def chk(name, t):
+            if nan_check and t is not None and not torch.isfinite(t.float()).all():
+                raise FloatingPointError(f"non-finite {name} in block backward ({fconv.weight.shape})")
+        chk("dout", dout)
 
         def put(p, g):
             if g is not None:
@@ -417,8 +471,10 @@ class _ResidualBlockFn(torch.autograd.Function):
                 return P.conv_dgrad(dy_, wp_, shape, stride, pad, addend), None
             _hin, _wp, y_, p_, z_ = rec
             return P.conv_dgrad(dy_, wp_, shape, stride, pad, addend, bnred=(z_, [(y_, p_)]))
+        chk("dyf", dyf)
         # --- final conv
         dh, pre_k = dgrad_fused(dyf, wpf, tuple(hlast.shape), fconv.stride, fconv.padding, recs[-1])
+        chk("dh(final)", dh)
         put(fconv.weight, _wgrad(P, dyf, hlast, wpf, fconv.stride, fconv.padding, fconv.weight))
         dx = None
         # --- conv->BN->ReLU stages in reverse; the block-input gradient of the
@@ -430,6 +486,7 @@ class _ResidualBlockFn(torch.autograd.Function):
                                        pre=pre_k)
             put(bn.weight, g[0])
             put(bn.bias, g[1])
+            chk(f"dy(stage {k})", dy)
             if k > 0:
                 dh, pre_k = dgrad_fused(dy, wp, tuple(hin.shape), conv_m.stride, conv_m.padding,
                                         recs[k - 1])

@@ -34,6 +34,26 @@ def _release(*bufs):
             _POOL.setdefault((b.device, b.shape[-1]), []).append(b)
 
 
+SUPPORTS_FP8 = True
+
+
+# ---------------------------------------------------------------------- fp8
+def quant_bf16_fp8(x, scale, amax):
+    return _C.quant_bf16_fp8(x, scale, amax)
+
+
+def quant_weight_fp8(w, cin, scale, amax):
+    return _C.quant_weight_fp8(w.detach(), int(cin), scale, amax)
+
+
+def conv_fp8_fwd(xq, wq, sx, sw, stride, pad, want_stats):
+    if want_stats:
+        buf = _acquire(wq.shape[0], xq.device)
+        y, st = _C.conv_fp8_fwd(xq, wq, sx, sw, int(stride), int(pad), True, buf)
+        return y, st
+    return _C.conv_fp8_fwd(xq, wq, sx, sw, int(stride), int(pad), False, None)[0], None
+
+
 # --------------------------------------------------------------------- conv
 def conv_weight(w, dtype, cin, want_t=True):
     if dtype != torch.bfloat16:
@@ -103,10 +123,14 @@ def stats_collapse(a, b=None, count=None, acc_a=None, acc_b=None):
     return out
 
 
-def bn_apply(y1, p1, res=None, y2=None, p2=None, relu=True):
+def bn_apply(y1, p1, res=None, y2=None, p2=None, relu=True, fp8=None):
     """-> (out, mask): mask is the ReLU bitmask (uint8 per 8-channel chunk) the
-    backward reads instead of re-reading ``out`` (1/16 of the bytes)."""
-    r = _C.bn_apply(y1, p1, res, y2, p2, bool(relu), True)
+    backward reads instead of re-reading ``out`` (1/16 of the bytes).
+    ``fp8=(scale, amax)`` -> (out, mask, q): q is an e4m3 copy of out * scale."""
+    if fp8 is not None:
+        r = _C.bn_apply(y1, p1, res, y2, p2, True, True, fp8[0], fp8[1])
+        return r[0], r[1], r[2]
+    r = _C.bn_apply(y1, p1, res, y2, p2, bool(relu), True, None, None)
     return (r[0], r[1]) if relu else (r[0], None)
 
 
