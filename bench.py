@@ -32,6 +32,8 @@ METRIC = ("images/sec (whole node) ResNet-50 224×224 bf16 at 1/2/4/8 MI355X; "
 # stock PyTorch-ROCm reference path (DDP+SyncBN+MIOpen, bench/comparator_torch.py),
 # measured on one MI355X at per-GPU batch 256: profiles/comparator_r01.txt
 STOCK_IPS_PER_GPU = 6612.5
+_MODEL_NAMES = {"resnet50": "ResNet-50", "resnet101": "ResNet-101", "resnet152": "ResNet-152",
+                "resnet34": "ResNet-34", "resnet18": "ResNet-18-ref", "res": "ResNet-18-ref"}
 
 
 def parse():
@@ -154,14 +156,16 @@ def bench_rank(rank, world, a):
             "ms_per_step": round(1000.0 * dt / a.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
             "data": "synthetic (on-device generated ImageNet-shaped batches, random-init weights)",
-            "config": {"model": "ResNet-50", "global_batch": a.batch * world, "seq_len": None,
+            "config": {"model": _MODEL_NAMES.get(a.model.lower(), a.model), "global_batch": a.batch * world,
+                       "seq_len": None,
                        "image_size": a.image, "per_gpu_batch": a.batch,
                        "parallelism": f"dp{world}", "sync_bn": a.sync_bn == "on" and world > 1,
                        "bucket_mb": a.bucket_mb, "hip_graph": bool(a.graph and world == 1),
                        "syncbn_comm": ("xgmi" if comm is not None and comm.xgmi is not None
                                        else "rccl" if world > 1 else None),
                        "grad_compress": a.grad_compress},
-            "vs_stock_pytorch_rocm": round(ips / (STOCK_IPS_PER_GPU * world), 3),
+            "vs_stock_pytorch_rocm": (round(ips / (STOCK_IPS_PER_GPU * world), 3)
+                                      if a.model.lower() == "resnet50" and a.dtype == "bf16" else None),
             "final_loss": round(final_loss, 4),
         }
         print(json.dumps(rec), flush=True)
