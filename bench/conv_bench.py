@@ -55,6 +55,8 @@ def main():
     ap.add_argument("--impls", default="5", help="conv staging/pipeline impls to time (see conv_igemm.hip; 5 = per-shape default)")
     ap.add_argument("--no-miopen", action="store_true")
     ap.add_argument("--fp8", action="store_true", help="also time the e4m3 scaled-MFMA forward conv")
+    ap.add_argument("--bnred", action="store_true",
+                    help="also time dgrad with the fused BN-backward reduce, and the separate reduce")
     a = ap.parse_args()
     torch.backends.cudnn.benchmark = True
     dev = "cuda"
@@ -91,6 +93,22 @@ def main():
                        timeit(lambda: HP.conv_wgrad(dy, x, tuple(wp[0].shape), st, pad), a.iters))
         t_f, t_d, t_w = per[impls[-1]]
         f8txt = ""
+        if a.bnred and C != 8:
+            yb = torch.randn_like(x)
+            pb = torch.stack([torch.zeros(C, device=dev), torch.ones(C, device=dev),
+                              torch.ones(C, device=dev), torch.zeros(C, device=dev)]).contiguous()
+            _, mk = HP.bn_apply(yb, pb, relu=True)
+
+            def dg_fused():
+                _, rr = HP.conv_dgrad(dy, wp, tuple(x.shape), st, pad, None, bnred=(mk, [(yb, pb)]))
+                HP._release(*rr)
+            dxx = HP.conv_dgrad(dy, wp, tuple(x.shape), st, pad)
+
+            def red_sep():
+                HP._release(HP.bn_bwd_reduce(dxx, mk, yb, pb, True))
+            tdf = timeit(dg_fused, a.iters)
+            trs = timeit(red_sep, a.iters)
+            f8txt += f"   dgrad+fusedred {tdf * 1e3:6.0f}us  dgrad {t_d * 1e3:6.0f}us  sep.reduce {trs * 1e3:5.0f}us"
         if a.fp8 and C % 16 == 0:
             sx = torch.tensor([1.0], device=dev)
             sw = torch.tensor([64.0], device=dev)

@@ -26,8 +26,9 @@ def build_parser():
     p.add_argument("--stem", "--arch", dest="stem", default="cifar", choices=["cifar", "imagenet"])
     p.add_argument("--image_size", default=None, type=int, help="input size (32 cifar / 224 imagenet)")
     p.add_argument("--num_classes", default=None, type=int, help="10 cifar / 1000 imagenet")
-    p.add_argument("--dtype", default="auto", choices=["auto", "bf16", "fp32"],
-                   help="activation dtype (auto: bf16 on GPU, fp32 on CPU)")
+    p.add_argument("--dtype", default="auto", choices=["auto", "bf16", "fp32", "fp8"],
+                   help="activation dtype (auto: bf16 on GPU, fp32 on CPU); fp8 = block-conv "
+                        "forwards on the e4m3 scaled MFMA with bf16 elsewhere (GPU only)")
     p.add_argument("--backend", default="auto", choices=["auto", "nccl", "rccl", "gloo"],
                    help="auto: RCCL (torch 'nccl') with GPUs, gloo on CPU")
     p.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])

@@ -166,17 +166,33 @@ def setup_syncbn(comm, sync_bn="on", transport="auto", on_gpu=True):
     if transport == "xgmi" or (transport == "auto" and on_gpu and comm.backend == "nccl"):
         if not on_gpu:
             raise ValueError("--syncbn_comm xgmi needs GPU ranks")
-        comm.enable_xgmi()
+        try:
+            x = comm.enable_xgmi()
+            if not x.self_test():
+                raise RuntimeError("xGMI all-reduce self-test mismatch")
+        except Exception as e:  # noqa: BLE001
+            if transport == "xgmi":
+                raise
+            # "auto": keep training on the RCCL transport, and say so
+            comm.xgmi = None
+            if comm.rank == 0:
+                print(f"[pmd] one-shot xGMI SyncBN transport unavailable ({e}); using RCCL",
+                      flush=True)
     OF.set_bn_sync(comm)
     return comm
 
 
 def _run(rank, world_size, args, dev):
     on_gpu = dev.type == "cuda"
-    dtype = torch.bfloat16 if (args.dtype == "bf16" or (args.dtype == "auto" and on_gpu)) \
+    dtype = torch.bfloat16 if (args.dtype in ("bf16", "fp8") or (args.dtype == "auto" and on_gpu)) \
         else torch.float32
     if on_gpu and dtype != torch.bfloat16:
-        raise ValueError("the gfx950 kernels compute in bf16; use --dtype bf16 on GPU")
+        raise ValueError("the gfx950 kernels compute in bf16; use --dtype bf16 (or fp8) on GPU")
+    if args.dtype == "fp8":
+        if not on_gpu:
+            raise ValueError("--dtype fp8 needs the gfx950 path (GPU)")
+        from ..ops.fp8 import Fp8Scaling
+        OF.set_fp8(Fp8Scaling(dev))
     cpad = 8 if on_gpu else 3
     train_loader, test_loader = build_loaders(args, rank, world_size, dev, dtype, cpad)
     if args.seed is not None:

@@ -33,6 +33,22 @@ class XgmiAllReduce:
         dist.barrier(group=group)
         self.capacity = self._c.capacity
 
+    def self_test(self, n: int = 4097, rounds: int = 3) -> bool:
+        """Collective: exact check of the kernel against the known sum of
+        rank-dependent integers (run once at setup; host-syncing)."""
+        ok = True
+        for r in range(rounds):
+            t = torch.arange(n, device="cuda", dtype=torch.float32) + 1000.0 * self.rank + r
+            self._c.all_reduce_(t)
+            W = self.world_size
+            want = (torch.arange(n, device="cuda", dtype=torch.float32) * W
+                    + 1000.0 * (W * (W - 1) / 2) + r * W)
+            torch.cuda.synchronize()
+            ok = ok and bool(torch.equal(t, want)) and self._c.check()
+        flag = torch.tensor([1 if ok else 0], device="cuda")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(flag.item() == 1)
+
     def accepts(self, t: torch.Tensor) -> bool:
         return (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
                 and t.numel() <= self.capacity)

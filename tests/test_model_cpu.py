@@ -159,3 +159,30 @@ def test_fused_bn_reduce_matches_unfused(arch):
     OF.set_fuse_bn_reduce(True)
     for n, g0 in grads[False].items():
         torch.testing.assert_close(grads[True][n], g0, rtol=1e-9, atol=1e-12, msg=n)
+
+
+REF_RESNET = "/root/reference/model/resnet.py"
+
+
+@pytest.mark.skipif(not __import__("os").path.exists(REF_RESNET), reason="reference tree not mounted")
+def test_checkpoint_loads_into_reference_model_class(tmp_path):
+    """SURVEY §4.2 format compatibility: our model_<E>.pth, with ``module.``
+    stripped, loads strict=True into the reference's own ``ResNet18()`` and
+    gives the same forward (fp32, eval)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ref_resnet", REF_RESNET)
+    ref = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ref)           # plain source: class definitions only
+    torch.manual_seed(0)
+    m = DataParallel(build_model("res"), comm=None)
+    path = save_model(m, str(tmp_path), 3)
+    sd = torch.load(path, weights_only=True)
+    rm = ref.ResNet18()
+    rm.load_state_dict({k[7:]: v for k, v in sd.items()}, strict=True)
+    rm.eval()
+    m.module.eval()
+    x = torch.randn(2, 3, 32, 32)
+    with torch.no_grad():
+        want = rm(x)
+        got = m.module(x.permute(0, 2, 3, 1).contiguous())
+    torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-5)

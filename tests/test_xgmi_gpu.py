@@ -30,6 +30,7 @@ def _worker(rank, world, port, out):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     xg = XgmiAllReduce(timeout_s=20.0)
+    assert xg.self_test()
     errs = []
     for it in range(3):
         for n in SIZES:
