@@ -24,12 +24,28 @@ class XgmiAllReduce:
         self.rank = dist.get_rank(group)
         self.world_size = dist.get_world_size(group)
         dev = torch.cuda.current_device()
-        self._c = C.XgmiComm(self.rank, self.world_size, dev, timeout_s)
+        # every step is agreed on by all ranks, so a local failure (e.g. IPC not
+        # permitted) raises on EVERY rank instead of leaving peers in a barrier
+        err = ""
+        handle = b""
+        try:
+            self._c = C.XgmiComm(self.rank, self.world_size, dev, timeout_s)
+            handle = self._c.handle()
+        except Exception as e:  # noqa: BLE001
+            err = f"rank {self.rank}: {e}"
         handles = [None] * self.world_size
-        dist.all_gather_object(handles, self._c.handle(), group=group)
-        self._c.open(handles)
-        # nobody may write into a peer buffer before every rank mapped its peers
+        dist.all_gather_object(handles, handle, group=group)
+        if not err:
+            try:
+                self._c.open(handles)
+            except Exception as e:  # noqa: BLE001
+                err = f"rank {self.rank}: {e}"
         torch.cuda.synchronize()
+        flag = torch.tensor([0 if err else 1], device="cuda")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+        if flag.item() != 1:
+            raise RuntimeError(f"xGMI transport setup failed ({err or 'on a peer rank'})")
+        # nobody may write into a peer buffer before every rank mapped its peers
         dist.barrier(group=group)
         self.capacity = self._c.capacity
 
