@@ -90,4 +90,32 @@ constexpr int kXgmiFlagBytes = 4096;
 int xgmi_allreduce_launch(float* const* data, uint32_t* const* flags, float* x, int n, int rank,
                           int world, uint32_t* epochs, uint32_t* err, long long spin_limit,
                           hipStream_t st);
+
+// SyncBN collapse + one-shot exchange + finalize (fwd) / global sums (bwd) in one kernel
+struct BnFinalizeOut {
+  const float* gamma;
+  const float* beta;
+  float* params;  // [4][C]
+  float* rm;      // running stats (nullable)
+  float* rv;
+  long long* nbt;
+  float eps, momentum;
+};
+struct XgmiBnArgs {
+  int mode;                 // 0 forward statistics, 1 backward reduce
+  float* slotsA;            // [kStatSlots][2][CA], read-and-clear
+  float* slotsB;            // optional second BN (projection shortcut)
+  int CA, CB;               // CB = 0 without B
+  float count;              // local element count per channel (forward)
+  BnFinalizeOut fA, fB;     // forward outputs
+  float* count_out;         // forward: global count [1]
+  float* accA0;             // backward: += local sums (d_beta, d_gamma arena views; nullable)
+  float* accA1;
+  float* accB0;
+  float* accB1;
+  float* outA;              // backward: global [2][CA]
+  float* outB;
+};
+int xgmi_bn_launch(float* const* data, uint32_t* const* flags, const XgmiBnArgs& args, int rank, int world,
+                   uint32_t* epochs, uint32_t* err, long long spin_limit, hipStream_t st);
 }  // namespace pmd

@@ -100,3 +100,141 @@ int xgmi_allreduce_launch(float* const* data, uint32_t* const* flags, float* x, 
 }
 
 }  // namespace pmd
+
+namespace pmd {
+
+// ---------------------------------------------------------------------------
+// SyncBN in ONE kernel per BN site and pass (instead of collapse -> all-reduce
+// -> finalize): each block owns up to kBnPairs channels (of BN A, then BN B),
+//   0) collapses their kStatSlots statistic slots (read-and-clear) into
+//      (s0, s1) pairs -- backward also adds the LOCAL sums into the gamma/beta
+//      gradient arena (DDP averages those later, like every other gradient);
+//   1-3) exchanges the pairs (+ the local element count) one-shot over xGMI
+//      exactly like xgmi_allreduce_kernel;
+//   4) forward: BatchNorm finalize from the global sums (params [4][C],
+//      running stats, num_batches_tracked, global count); backward: writes the
+//      global (sum dz, sum dz*xhat) as [2][C] for bn_bwd_elemt.
+constexpr int kBnPairs = (kXgmiChunk - 2) / 2;  // 1023 channels per block; [2*kBnPairs] = count
+
+__global__ __launch_bounds__(256) void xgmi_bn_kernel(XgmiPeers peers, XgmiBnArgs a, int rank, int world,
+                                                     uint32_t* __restrict__ epochs,
+                                                     uint32_t* __restrict__ err, long long spin_limit) {
+  __shared__ float loc[kXgmiChunk];
+  __shared__ uint32_t e_sh;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0) {
+    e_sh = epochs[b] + 1;
+    epochs[b] = e_sh;
+  }
+  const int P = a.CA + a.CB;
+  const int p0 = b * kBnPairs;
+  const int np = min(kBnPairs, P - p0);
+  // 0) collapse my channels' slots
+  for (int j = tid; j < np; j += 256) {
+    const int pi = p0 + j;
+    const bool isA = pi < a.CA;
+    float* slots = isA ? a.slotsA : a.slotsB;
+    const int C = isA ? a.CA : a.CB;
+    const int c = isA ? pi : pi - a.CA;
+    float s0 = 0.f, s1 = 0.f;
+    for (int k = 0; k < kStatSlots; ++k) {
+      float* q = slots + (size_t)k * 2 * C;
+      s0 += q[c];
+      s1 += q[C + c];
+      q[c] = 0.f;
+      q[C + c] = 0.f;
+    }
+    loc[2 * j] = s0;
+    loc[2 * j + 1] = s1;
+    if (a.mode == 1) {
+      float* acc0 = isA ? a.accA0 : a.accB0;
+      float* acc1 = isA ? a.accA1 : a.accB1;
+      if (acc0) acc0[c] += s0;
+      if (acc1) acc1[c] += s1;
+    }
+  }
+  if (tid == 0) loc[2 * kBnPairs] = a.count;
+  __syncthreads();
+  const uint32_t e = e_sh;
+  const int par = e & 1;
+  // 1) push pairs + count into slot [par][rank] of every rank's receive buffer
+  const size_t my_slot = ((size_t)par * world + rank) * kXgmiCap + (size_t)b * kXgmiChunk;
+  for (int r = 0; r < world; ++r) {
+    float* dst = peers.data[r] + my_slot;
+    for (int i = tid; i < 2 * np; i += 256) dst[i] = loc[i];
+    if (tid == 0) dst[2 * kBnPairs] = loc[2 * kBnPairs];
+  }
+  __threadfence_system();
+  __syncthreads();
+  // 2) flag, 3) wait
+  if (tid < world)
+    __hip_atomic_store(peers.flags[tid] + rank * kXgmiMaxBlocks + b, e, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid < world) {
+    const uint32_t* f = peers.flags[rank] + tid * kXgmiMaxBlocks + b;
+    long long it = 0;
+    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+      if (++it > spin_limit) {
+        atomicOr(err, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  // 4) global sums in rank order, then finalize / publish
+  const float* mine = peers.data[rank] + (size_t)par * world * kXgmiCap + (size_t)b * kXgmiChunk;
+  float cnt = 0.f;
+  for (int r = 0; r < world; ++r) cnt += mine[(size_t)r * kXgmiCap + 2 * kBnPairs];
+  for (int j = tid; j < np; j += 256) {
+    float g0 = 0.f, g1 = 0.f;
+    for (int r = 0; r < world; ++r) {
+      g0 += mine[(size_t)r * kXgmiCap + 2 * j];
+      g1 += mine[(size_t)r * kXgmiCap + 2 * j + 1];
+    }
+    const int pi = p0 + j;
+    const bool isA = pi < a.CA;
+    const int C = isA ? a.CA : a.CB;
+    const int c = isA ? pi : pi - a.CA;
+    if (a.mode == 0) {
+      const BnFinalizeOut& o = isA ? a.fA : a.fB;
+      const float mean = g0 / cnt;
+      const float var = fmaxf(g1 / cnt - mean * mean, 0.f);
+      const float inv = rsqrtf(var + o.eps);
+      const float sc = o.gamma[c] * inv;
+      o.params[c] = mean;
+      o.params[C + c] = inv;
+      o.params[2 * C + c] = sc;
+      o.params[3 * C + c] = o.beta[c] - mean * sc;
+      if (o.rm) {
+        const float unb = var * (cnt / fmaxf(cnt - 1.f, 1.f));
+        o.rm[c] = (1.f - o.momentum) * o.rm[c] + o.momentum * mean;
+        o.rv[c] = (1.f - o.momentum) * o.rv[c] + o.momentum * unb;
+      }
+      if (c == 0 && o.nbt) o.nbt[0] += 1;
+    } else {
+      float* out = isA ? a.outA : a.outB;
+      out[c] = g0;
+      out[C + c] = g1;
+    }
+  }
+  if (a.mode == 0 && b == 0 && tid == 0 && a.count_out) a.count_out[0] = cnt;
+}
+
+int xgmi_bn_launch(float* const* data, uint32_t* const* flags, const XgmiBnArgs& args, int rank, int world,
+                   uint32_t* epochs, uint32_t* err, long long spin_limit, hipStream_t st) {
+  if (world < 1 || world > kXgmiMaxRanks) return 1;
+  const int P = args.CA + args.CB;
+  const int nb = (P + kBnPairs - 1) / kBnPairs;
+  if (P <= 0 || nb > kXgmiMaxBlocks) return 2;
+  XgmiPeers p{};
+  for (int r = 0; r < world; ++r) {
+    p.data[r] = data[r];
+    p.flags[r] = flags[r];
+  }
+  hipLaunchKernelGGL(xgmi_bn_kernel, dim3(nb), dim3(256), 0, st, p, args, rank, world, epochs, err,
+                     spin_limit);
+  return 0;
+}
+
+}  // namespace pmd

@@ -96,6 +96,82 @@ class XgmiComm {
     return x;
   }
 
+  // SyncBN fused statistics exchange (see xgmi_bn_kernel).  Forward (mode 0):
+  // slots -> params_a/params_b [4][C], running stats, nbt, count_out [1].
+  // Backward (mode 1): slots -> acc_* += local sums, out_a/out_b [2][C] global.
+  void bn_(int64_t mode, at::Tensor slots_a, c10::optional<at::Tensor> slots_b, double count,
+           c10::optional<at::Tensor> gamma_a, c10::optional<at::Tensor> beta_a,
+           c10::optional<at::Tensor> params_a, c10::optional<at::Tensor> rm_a,
+           c10::optional<at::Tensor> rv_a, c10::optional<at::Tensor> nbt_a, double eps_a, double mom_a,
+           c10::optional<at::Tensor> gamma_b, c10::optional<at::Tensor> beta_b,
+           c10::optional<at::Tensor> params_b, c10::optional<at::Tensor> rm_b,
+           c10::optional<at::Tensor> rv_b, c10::optional<at::Tensor> nbt_b, double eps_b, double mom_b,
+           c10::optional<at::Tensor> count_out, c10::optional<at::Tensor> acc_a0,
+           c10::optional<at::Tensor> acc_a1, c10::optional<at::Tensor> acc_b0,
+           c10::optional<at::Tensor> acc_b1, c10::optional<at::Tensor> out_a,
+           c10::optional<at::Tensor> out_b) {
+    TORCH_CHECK(opened_ || world_ == 1, "xgmi: open() the peer handles first");
+    auto fptr = [](const c10::optional<at::Tensor>& t) -> float* {
+      if (!t || !t->defined()) return nullptr;
+      TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->is_cuda(),
+                  "xgmi bn: fp32 contiguous GPU tensors expected");
+      return t->data_ptr<float>();
+    };
+    TORCH_CHECK(slots_a.scalar_type() == at::kFloat && slots_a.is_contiguous() && slots_a.dim() == 3 &&
+                    slots_a.size(0) == 64 && slots_a.size(1) == 2, "xgmi bn: slots must be [64, 2, C]");
+    pmd::XgmiBnArgs a{};
+    a.mode = (int)mode;
+    a.slotsA = slots_a.data_ptr<float>();
+    a.CA = (int)slots_a.size(2);
+    const bool hasB = slots_b && slots_b->defined();
+    if (hasB) {
+      TORCH_CHECK(slots_b->dim() == 3 && slots_b->size(0) == 64 && slots_b->size(1) == 2 &&
+                  slots_b->is_contiguous(), "xgmi bn: slots_b must be [64, 2, C]");
+      a.slotsB = slots_b->data_ptr<float>();
+      a.CB = (int)slots_b->size(2);
+    }
+    a.count = (float)count;
+    auto fin = [&](pmd::BnFinalizeOut& o, const c10::optional<at::Tensor>& g, const c10::optional<at::Tensor>& bt,
+                   const c10::optional<at::Tensor>& pr, const c10::optional<at::Tensor>& rm,
+                   const c10::optional<at::Tensor>& rv, const c10::optional<at::Tensor>& nbt, double eps,
+                   double mom, int C) {
+      o.gamma = fptr(g);
+      o.beta = fptr(bt);
+      o.params = fptr(pr);
+      TORCH_CHECK(o.gamma && o.beta && o.params && pr->numel() == 4 * C, "xgmi bn fwd: gamma/beta/params");
+      o.rm = fptr(rm);
+      o.rv = fptr(rv);
+      o.nbt = (nbt && nbt->defined()) ? reinterpret_cast<long long*>(nbt->data_ptr<int64_t>()) : nullptr;
+      o.eps = (float)eps;
+      o.momentum = (float)mom;
+    };
+    if (mode == 0) {
+      fin(a.fA, gamma_a, beta_a, params_a, rm_a, rv_a, nbt_a, eps_a, mom_a, a.CA);
+      if (hasB) fin(a.fB, gamma_b, beta_b, params_b, rm_b, rv_b, nbt_b, eps_b, mom_b, a.CB);
+      a.count_out = fptr(count_out);
+    } else {
+      a.accA0 = fptr(acc_a0);
+      a.accA1 = fptr(acc_a1);
+      a.accB0 = fptr(acc_b0);
+      a.accB1 = fptr(acc_b1);
+      a.outA = fptr(out_a);
+      a.outB = fptr(out_b);
+      TORCH_CHECK(a.outA && out_a->numel() == 2 * a.CA && (!hasB || (a.outB && out_b->numel() == 2 * a.CB)),
+                  "xgmi bn bwd: out tensors [2, C]");
+    }
+    float* data[kXgmiMaxRanks];
+    uint32_t* flags[kXgmiMaxRanks];
+    for (int r = 0; r < world_; ++r) {
+      flags[r] = reinterpret_cast<uint32_t*>(peers_[r]);
+      data[r] = reinterpret_cast<float*>(static_cast<char*>(peers_[r]) + kXgmiFlagBytes);
+    }
+    c10::DeviceGuard g(slots_a.device());
+    const int rc = xgmi_bn_launch(data, flags, a, rank_, world_, epochs_, err_, spin_limit_,
+                                  c10::hip::getCurrentHIPStream().stream());
+    TORCH_CHECK(rc == 0, "xgmi bn: launch rejected (", rc, ")");
+    calls_++;
+  }
+
   // host-blocking: did any call time out waiting for a peer?
   bool check() {
     c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, device_));
@@ -127,6 +203,7 @@ void register_xgmi(pybind11::module& m) {
       .def("handle", &XgmiComm::handle)
       .def("open", &XgmiComm::open)
       .def("all_reduce_", &XgmiComm::all_reduce_)
+      .def("bn_", &XgmiComm::bn_)
       .def("check", &XgmiComm::check)
       .def_property_readonly("capacity", &XgmiComm::capacity)
       .def_property_readonly("calls", &XgmiComm::calls);

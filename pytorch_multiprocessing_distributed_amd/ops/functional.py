@@ -168,6 +168,16 @@ def _bn_forward_params(P, y, st, bn, training, sync, y2=None, st2=None, bn2=None
                                         bn2.running_mean, bn2.running_var, bn2.momentum,
                                         bn2.num_batches_tracked)
         return p1, p2, float(m_local)
+    fused = getattr(sync, "fused_bn_ok", None)
+    if fused is not None and fused(st) and hasattr(P, "_release"):
+        # collapse + one-shot xGMI exchange + finalize in ONE kernel
+        dev = y.device
+        p1 = torch.empty(4, c1, dtype=torch.float32, device=dev)
+        p2 = torch.empty(4, y2.shape[-1], dtype=torch.float32, device=dev) if bn2 is not None else None
+        count = torch.empty(1, dtype=torch.float32, device=dev)
+        sync.bn_stats_fwd(st, st2, float(m_local), bn, bn2, p1, p2, count)
+        P._release(st, st2)
+        return p1, p2, count
     buf = P.stats_collapse(st, st2, float(m_local))
     sync.all_reduce_stats_(buf)
     count = buf[-1:]
@@ -196,8 +206,26 @@ def _bn_backward(P, dout, mask, relu, training, sync, count, y1, p1, bn1, y2=Non
         r2 = P.bn_bwd_reduce(dout, mask, y2, p2, relu) if y2 is not None else None
     acc1 = _bn_acc(bn1)
     acc2 = _bn_acc(bn2) if bn2 is not None else None
-    red = P.stats_collapse(r1, r2, None, acc1, acc2)     # local sums; gamma/beta grads += local
     c1 = y1.shape[-1]
+    fused = getattr(sync, "fused_bn_ok", None) if training else None
+    if (fused is not None and fused(r1) and hasattr(P, "_release") and acc1 is not None
+            and (bn2 is None or acc2 is not None)):
+        # collapse (+= local gamma/beta grads) + one-shot exchange in ONE kernel
+        c2 = y2.shape[-1] if y2 is not None else 0
+        red = torch.empty(2 * c1 + 2 * c2, dtype=torch.float32, device=dout.device)
+        sync.bn_stats_bwd(r1, r2, acc1, acc2, red[:2 * c1], red[2 * c1:] if c2 else None)
+        P._release(r1, r2)
+        _ready(bn1.bias, bn1.weight)
+        if bn2 is not None:
+            _ready(bn2.bias, bn2.weight)
+        dy1, dzm = P.bn_bwd_elemt(dout, mask, y1, p1, bn1.weight, red[:2 * c1].view(2, c1), count,
+                                  relu, want_dzm=want_dzm)
+        dy2 = None
+        if y2 is not None:
+            dy2, _ = P.bn_bwd_elemt(dout, mask, y2, p2, bn2.weight, red[2 * c1:].view(2, -1), count,
+                                    relu)
+        return dy1, dy2, dzm, [None, None, None, None]
+    red = P.stats_collapse(r1, r2, None, acc1, acc2)     # local sums; gamma/beta grads += local
     grads = [None, None, None, None]
     if acc1 is None:
         grads[0], grads[1] = red[c1:2 * c1], red[:c1]

@@ -72,6 +72,18 @@ class Comm:
             return x.all_reduce_(t)
         return self.all_reduce_(t)
 
+    def fused_bn_ok(self, t):
+        """Can the fused SyncBN statistics kernel handle these slot buffers?"""
+        return self.xgmi is not None and t.is_cuda and t.dim() == 3 and t.shape[0] == 64
+
+    def bn_stats_fwd(self, slots_a, slots_b, count, bn_a, bn_b, params_a, params_b, count_out):
+        self._record("xgmi_bn_fwd", slots_a)
+        self.xgmi.bn_fwd(slots_a, slots_b, count, bn_a, bn_b, params_a, params_b, count_out)
+
+    def bn_stats_bwd(self, slots_a, slots_b, acc_a, acc_b, out_a, out_b):
+        self._record("xgmi_bn_bwd", slots_a)
+        self.xgmi.bn_bwd(slots_a, slots_b, acc_a, acc_b, out_a, out_b)
+
     def broadcast_(self, t, src=0):
         self._record("broadcast", t)
         dist.broadcast(t, src=src, group=self.group)

@@ -74,3 +74,78 @@ def test_xgmi_oneshot_allreduce_two_ranks(tmp_path):
     assert got["errs"].max().item() == 0.0, got["errs"]
     assert got["burst"]
     print(f"xgmi one-shot all-reduce (2 ranks, 1 GPU, 4097 floats): {got['us_per_call']:.1f} us/call")
+
+
+def _bn_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    from pytorch_multiprocessing_distributed_amd.parallel.xgmi import XgmiAllReduce
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    xg = XgmiAllReduce(timeout_s=20.0)
+    res = {}
+    for CA, CB in ((64, 0), (256, 256), (2048, 2048)):
+        g = torch.Generator().manual_seed(10 * CA + rank)
+        sa = torch.rand(64, 2, CA, generator=g).cuda()
+        sb = torch.rand(64, 2, CB, generator=g).cuda() if CB else None
+        bns = [torch.nn.BatchNorm2d(c).cuda() for c in (CA, CB) if c]
+        for bn in bns:
+            bn.weight.data.uniform_(0.5, 1.5, generator=None)
+        # expected: local collapse -> global sums (gloo) -> finalize
+        loc = torch.cat([sa.sum(0).reshape(-1)] + ([sb.sum(0).reshape(-1)] if CB else [])).cpu()
+        cnt_local = 1000.0 + rank
+        glob = loc.clone()
+        dist.all_reduce(glob)
+        cnt = sum(1000.0 + r for r in range(world))
+        pa = torch.empty(4, CA, device="cuda")
+        pb = torch.empty(4, CB, device="cuda") if CB else None
+        co = torch.empty(1, device="cuda")
+        rm0 = [bn.running_mean.clone() for bn in bns]
+        xg.bn_fwd(sa, sb, cnt_local, bns[0], bns[1] if CB else None, pa, pb, co)
+        torch.cuda.synchronize()
+        errs = [float(sa.abs().max()), float(sb.abs().max()) if CB else 0.0]   # slots cleared
+        off = 0
+        for bn, p, C, rm in zip(bns, [pa, pb], [CA, CB], rm0):
+            s0, s1 = glob[off:off + C], glob[off + C:off + 2 * C]
+            off += 2 * C
+            mean = s0 / cnt
+            var = (s1 / cnt - mean * mean).clamp_min(0)
+            inv = torch.rsqrt(var + bn.eps)
+            errs.append(float((p[0].cpu() - mean).abs().max() / mean.abs().max()))
+            errs.append(float((p[1].cpu() - inv).abs().max() / inv.abs().max()))
+            want_rm = 0.9 * rm.cpu() + 0.1 * mean
+            errs.append(float((bn.running_mean.cpu() - want_rm).abs().max() / want_rm.abs().max()))
+        errs.append(abs(co.item() - cnt) / cnt)
+        # backward: acc += local, out = global
+        acc = [torch.zeros(C, device="cuda") for C in (CA, CA, CB, CB) if C]
+        sa2 = torch.rand(64, 2, CA, generator=g).cuda()
+        sb2 = torch.rand(64, 2, CB, generator=g).cuda() if CB else None
+        loc2 = torch.cat([sa2.sum(0).reshape(-1)] + ([sb2.sum(0).reshape(-1)] if CB else [])).cpu()
+        glob2 = loc2.clone()
+        dist.all_reduce(glob2)
+        oa = torch.empty(2 * CA, device="cuda")
+        ob = torch.empty(2 * CB, device="cuda") if CB else None
+        xg.bn_bwd(sa2, sb2, (acc[0], acc[1]), (acc[2], acc[3]) if CB else None, oa, ob)
+        torch.cuda.synchronize()
+        got = torch.cat([oa.cpu()] + ([ob.cpu()] if CB else []))
+        errs.append(float((got - glob2).abs().max() / glob2.abs().max()))
+        errs.append(float((acc[0].cpu() - loc2[:CA]).abs().max() / loc2[:CA].abs().max()))
+        errs.append(float((acc[1].cpu() - loc2[CA:2 * CA]).abs().max() / loc2[CA:2 * CA].abs().max()))
+        res[(CA, CB)] = errs
+    xg.check()
+    if rank == 0:
+        torch.save({str(k): torch.tensor(v) for k, v in res.items()}, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_xgmi_fused_syncbn_statistics(tmp_path):
+    """Fused SyncBN kernel: slot collapse (read-and-clear) + one-shot exchange +
+    finalize (params, running stats, global count) / backward global sums and
+    local gamma/beta accumulation -- vs a gloo all-reduce of the same data."""
+    out = str(tmp_path / "bn.pt")
+    mp.spawn(_bn_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    for k, v in got.items():
+        assert (v < 1e-5).all(), (k, v)
