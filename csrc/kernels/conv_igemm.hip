@@ -168,9 +168,70 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     b_ok[i] = nn < a.Nout;
     b_row[i] = a.wt + (size_t)(b_ok[i] ? nn : 0) * a.Kg;
   }
+  // Uniform-tap fast path (LDS-DMA, Cs % BK == 0 -- every layer but the stem):
+  // a K-tile then lies inside ONE filter tap, so the tap (r, s) and its pixel
+  // offset are wave-uniform scalars; per row the gather needs only
+  //   ih = u_h + dr, iw = u_w + ds, pix = u_p + dr*W + ds   (dr, ds scalars)
+  // with (dr, ds) = (r, s) fwd, (-r, -s) stride-1 dgrad, (-tr, -ts) stride-2
+  // dgrad (the phase fixes r = r0 + 2 tr, so (h + pad - r) / 2 = u_h - tr).
+  const bool uni = DMA && a.Cs >= BK;
+  int u_h[PA], u_w[PA], u_p[PA];
+#pragma unroll
+  for (int i = 0; i < PA; ++i) {
+    int hh = a_h[i], ww = a_w[i];
+    if (DGRAD && a.stride == 2) {
+      hh = (a_h[i] - r0) >> 1;
+      ww = (a_w[i] - s0) >> 1;
+    }
+    u_h[i] = hh;
+    u_w[i] = ww;
+    u_p[i] = a_base[i] + hh * a.W + ww;
+  }
+  const int lane_c = (lane % CH ^ swz<BK>(lane / CH)) * 8;  // == chunk * 8 on the DMA path
+  const int wid_s = __builtin_amdgcn_readfirstlane(wid);
 
   uint4 ra[DMA ? 1 : PA], rb[DMA ? 1 : PB];
   const int nk = (Kgp + BK - 1) / BK;
+
+  auto load_tile_uni = [&](int kt, int dbuf) {
+    const int k0 = kt * BK;                       // all scalar until lane_c
+    const bool kok = k0 < Kgp;
+    const int tap = k0 >> a.log2Cs;
+    const int tr = tap / ns;
+    const int ts = tap - tr * ns;
+    const int r = r0 + rstep * tr, sx = s0 + rstep * ts;
+    int dr, ds;
+    if (!DGRAD) {
+      dr = r;
+      ds = sx;
+    } else if (a.stride == 2) {
+      dr = -tr;
+      ds = -ts;
+    } else {
+      dr = -r;
+      ds = -sx;
+    }
+    const int dpix = dr * a.W + ds;
+    const int c = (k0 & (a.Cs - 1)) + lane_c;
+    const int boff = ((r * a.S + sx) << a.log2Cs) + c;
+#pragma unroll
+    for (int i = 0; i < PA; ++i) {
+      const bool ok = kok && a_ok[i] && (unsigned)(u_h[i] + dr) < (unsigned)a.H &&
+                      (unsigned)(u_w[i] + ds) < (unsigned)a.W;
+      const bf16_t* real = a.src + ((size_t)(unsigned)(u_p[i] + dpix) << a.log2Cs) + c;
+      const void* src = ok ? (const void*)real : (const void*)g_zero16;
+      bf16_t* dst = lds + dbuf * STAGE + (wid_s * (BM / 4) + RPI * i) * LDR;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+      const void* src = (b_ok[i] && kok) ? (const void*)(b_row[i] + boff) : (const void*)g_zero16;
+      bf16_t* dst = lds + dbuf * STAGE + A_ELEMS + (wid_s * (BN / 4) + RPI * i) * LDR;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
 
   auto load_tile = [&](int kt, int dbuf) {
     const int k0 = kt * BK + chunk * 8;
@@ -271,10 +332,14 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
   };
 
   if constexpr (DMA) {
+    auto load = [&](int kt, int buf) {
+      if (uni) load_tile_uni(kt, buf);
+      else load_tile(kt, buf);
+    };
     // prologue: tiles 0 .. NST-2 in flight
 #pragma unroll
     for (int t = 0; t < NST - 1; ++t)
-      if (t < nk) load_tile(t, t);
+      if (t < nk) load(t, t);
     for (int kt = 0; kt < nk; ++kt) {
       // own DMAs of tile kt done; later tiles (at most NST-2 of them) may still fly
       const int rem = min(NST - 2, nk - 1 - kt);
@@ -291,7 +356,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
       // publishes tile kt to all waves AND retires every wave's reads of tile kt-1,
       // whose buffer the DMA below overwrites
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      if (kt + NST - 1 < nk) load_tile(kt + NST - 1, (kt + NST - 1) % NST);
+      if (kt + NST - 1 < nk) load(kt + NST - 1, (kt + NST - 1) % NST);
       compute(kt % NST);
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
