@@ -76,9 +76,15 @@ __device__ __forceinline__ int swz(int row) {
   else return (row >> 2) & 2;
 }
 
-template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA>
+// MF32: v_mfma_f32_32x32x16_bf16 instead of 16x16x32 (same FLOPs in half the
+// instructions, so the MFMA holds the SIMD's issue port 8 of every 32 cycles
+// instead of 8 of 16 -- more room for the gather math and LDS reads).  Needs
+// the LDS-DMA uniform-tap path with BK=64; chunk swizzle phys = q ^ ((row>>1)&7)
+// keeps the 32-row ds_read_b128 lane groups conflict-free.
+template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA, bool MF32 = false>
 __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
   static_assert(DMA || (BK == 64 && NST == 2), "register staging: BK=64, 2 stages");
+  static_assert(!MF32 || (DMA && BK == 64), "32x32 MFMA path: LDS-DMA, BK=64");
   constexpr int CH = BK / 8;                      // 16-B chunks per LDS row
   constexpr int RPI = DMA ? 64 / CH : 32;         // rows per load instruction (wave / block)
   constexpr int PA = DMA ? BM / (4 * RPI) : BM / 32;  // A load instructions per thread per tile
@@ -188,6 +194,10 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     u_p[i] = a_base[i] + hh * a.W + ww;
   }
   const int lane_c = (lane % CH ^ swz<BK>(lane / CH)) * 8;  // == chunk * 8 on the DMA path
+  // MF32 swizzle depends on row bits 1..3: instruction i covers rows base + 8i + l/8 with
+  // base % 32 == 0 (BM/4, BN/4 multiples of 16 -> (base >> 1) % 8 == 0)
+  const int lane_c32[2] = {((lane & 7) ^ (((lane >> 3) >> 1) & 7)) * 8,
+                           ((lane & 7) ^ ((4 + ((lane >> 3) >> 1)) & 7)) * 8};
   const int wid_s = __builtin_amdgcn_readfirstlane(wid);
 
   uint4 ra[DMA ? 1 : PA], rb[DMA ? 1 : PB];
@@ -212,13 +222,15 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
       ds = -sx;
     }
     const int dpix = dr * a.W + ds;
-    const int c = (k0 & (a.Cs - 1)) + lane_c;
-    const int boff = ((r * a.S + sx) << a.log2Cs) + c;
+    const int cb = k0 & (a.Cs - 1);
+    const int c = cb + lane_c;
+    const int tapo = (r * a.S + sx) << a.log2Cs;
 #pragma unroll
     for (int i = 0; i < PA; ++i) {
       const bool ok = kok && a_ok[i] && (unsigned)(u_h[i] + dr) < (unsigned)a.H &&
                       (unsigned)(u_w[i] + ds) < (unsigned)a.W;
-      const bf16_t* real = a.src + ((size_t)(unsigned)(u_p[i] + dpix) << a.log2Cs) + c;
+      const int ci = MF32 ? cb + lane_c32[i & 1] : c;
+      const bf16_t* real = a.src + ((size_t)(unsigned)(u_p[i] + dpix) << a.log2Cs) + ci;
       const void* src = ok ? (const void*)real : (const void*)g_zero16;
       bf16_t* dst = lds + dbuf * STAGE + (wid_s * (BM / 4) + RPI * i) * LDR;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
@@ -226,6 +238,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
+      const int boff = tapo + (MF32 ? cb + lane_c32[i & 1] : c);
       const void* src = (b_ok[i] && kok) ? (const void*)(b_row[i] + boff) : (const void*)g_zero16;
       bf16_t* dst = lds + dbuf * STAGE + A_ELEMS + (wid_s * (BN / 4) + RPI * i) * LDR;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
@@ -298,11 +311,22 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     }
   };
 
-  f32x4 acc[MI][NI];
+  constexpr int MI2 = MF32 ? BM / 64 : 1, NI2 = MF32 ? BN / 64 : 1;  // 32x32 tiles per wave
+  f32x4 acc[MF32 ? 1 : MI][MF32 ? 1 : NI];
+  f32x16 acc2[MI2][NI2];
+  if constexpr (MF32) {
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
+    for (int i = 0; i < MI2; ++i)
 #pragma unroll
-    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NI2; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc2[i][j][e] = 0.f;
+  } else {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
   const int frow = lane & 15;
   // fragment read: row r, logical 16-B chunk q of the current K-step
@@ -315,6 +339,30 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
   auto compute = [&](int buf) {
     const bf16_t* As = lds + buf * STAGE;
     const bf16_t* Bs = lds + buf * STAGE + A_ELEMS;
+    if constexpr (MF32) {
+      const int r32 = lane & 31;
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        bf16x8 af[MI2], bfg[NI2];
+        const int q = ks * 2 + (lane >> 5);
+#pragma unroll
+        for (int i = 0; i < MI2; ++i) {
+          const int r = wm * (BM / 2) + i * 32 + r32;
+          af[i] = *reinterpret_cast<const bf16x8*>(As + r * LDR + ((q ^ ((r >> 1) & 7)) << 3));
+        }
+#pragma unroll
+        for (int j = 0; j < NI2; ++j) {
+          const int r = wn * (BN / 2) + j * 32 + r32;
+          bfg[j] = *reinterpret_cast<const bf16x8*>(Bs + r * LDR + ((q ^ ((r >> 1) & 7)) << 3));
+        }
+#pragma unroll
+        for (int i = 0; i < MI2; ++i)
+#pragma unroll
+          for (int j = 0; j < NI2; ++j)
+            acc2[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfg[j], acc2[i][j], 0, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       bf16x8 af[MI], bfg[NI];
@@ -385,21 +433,54 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     csum[j] = 0.f;
     csq[j] = 0.f;
   }
+  if constexpr (MF32) {
+    // 32x32 C layout: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
+    for (int i = 0; i < MI2; ++i)
 #pragma unroll
-    for (int j = 0; j < NI; ++j)
+      for (int j = 0; j < NI2; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const bf16_t h = f2bf(acc[i][j][e]);
-        Cs[(crow0 + i * 16 + e) * LDC + ccol0 + j * 16] = h;
-        if (STATS) {
-          const float v = bf2f(h);
-          csum[j] += v;
-          csq[j] += v * v;
+        for (int e = 0; e < 16; ++e) {
+          const bf16_t h = f2bf(acc2[i][j][e]);
+          const int row = wm * (BM / 2) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+          Cs[row * LDC + wn * (BN / 2) + j * 32 + (lane & 31)] = h;
+          if (STATS) {
+            const float v = bf2f(h);
+            csum[j] += v;
+            csq[j] += v * v;
+          }
         }
+  } else {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bf16_t h = f2bf(acc[i][j][e]);
+          Cs[(crow0 + i * 16 + e) * LDC + ccol0 + j * 16] = h;
+          if (STATS) {
+            const float v = bf2f(h);
+            csum[j] += v;
+            csq[j] += v * v;
+          }
+        }
+  }
+  if (STATS && MF32) {
+    // column sums: lanes l and l+32 hold the two row halves of column l & 31
+    float* st = reinterpret_cast<float*>(smem + SMEM);  // [2 wm][2][BN]
+#pragma unroll
+    for (int j = 0; j < NI2; ++j) {
+      float s1 = csum[j], s2 = csq[j];
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (lane < 32) {
+        st[(wm * 2 + 0) * BN + wn * (BN / 2) + j * 32 + lane] = s1;
+        st[(wm * 2 + 1) * BN + wn * (BN / 2) + j * 32 + lane] = s2;
       }
-  if (STATS) {
+    }
+  }
+  if (STATS && !MF32) {
     float* st = reinterpret_cast<float*>(smem + SMEM);  // [2 wm][2][BN]
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
@@ -542,6 +623,7 @@ static int ilog2(int v) {
 //   0 register staging, BK=64, 2 stages
 //   1 LDS-DMA BK=64, 2 stages      2 LDS-DMA BK=32, 4 stages
 //   3 LDS-DMA BK=64, 3 stages      4 LDS-DMA BK=32, 3 stages
+//   6 LDS-DMA BK=64, 2 stages, 32x32x16 MFMA
 //   5 (default) per shape: BK=32/3 stages for short reductions (Kg <= 512: the
 //     prologue/epilogue dominate, a shallower K-tile fills the pipe sooner),
 //     BK=64/2 stages otherwise (fewer barriers per MFMA) -- measured on all 23
@@ -553,18 +635,18 @@ void conv_set_impl(int impl) { g_conv_impl = impl; }
 static int conv_impl() {
   if (g_conv_impl < 0) {
     const char* e = getenv("PMD_CONV_IMPL");
-    g_conv_impl = (e && e[0] >= '0' && e[0] <= '5') ? e[0] - '0' : 5;
+    g_conv_impl = (e && e[0] >= '0' && e[0] <= '6') ? e[0] - '0' : 5;
   }
   return g_conv_impl;
 }
 
-template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA>
+template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA, bool MF32 = false>
 static void launch_k(const ConvArgs& a, hipStream_t st) {
   const bool ph2 = DGRAD && a.stride == 2;
   const int Mgrid = ph2 ? a.N * ((a.OH + 1) >> 1) * ((a.OW + 1) >> 1) : a.M;
   const int tiles = ((Mgrid + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
   const int phases = ph2 ? 4 : 1;
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, NST, DGRAD, STATS, DMA>), dim3(tiles, phases),
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, NST, DGRAD, STATS, DMA, MF32>), dim3(tiles, phases),
                      dim3(256), 0, st, a);
 }
 
@@ -577,6 +659,10 @@ static void launch_t(const ConvArgs& a, hipStream_t st) {
     case 1: launch_k<BM, BN, 64, 2, DGRAD, STATS, true>(a, st); break;
     case 2: launch_k<BM, BN, 32, 4, DGRAD, STATS, true>(a, st); break;
     case 3: launch_k<BM, BN, 64, 3, DGRAD, STATS, true>(a, st); break;
+    case 6:  // 32x32x16 MFMA: needs the uniform-tap loader (Cs % 64 == 0)
+      if (a.Cs % 64 == 0) launch_k<BM, BN, 64, 2, DGRAD, STATS, true, true>(a, st);
+      else launch_k<BM, BN, 64, 2, DGRAD, STATS, true>(a, st);
+      break;
     default: launch_k<BM, BN, 32, 3, DGRAD, STATS, true>(a, st); break;
   }
 }
