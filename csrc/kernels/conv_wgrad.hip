@@ -21,6 +21,7 @@
 // single-carry increments, so the gather costs no integer divisions in the
 // main loop.
 #include "common.h"
+#include <stdlib.h>
 
 namespace pmd {
 
@@ -257,12 +258,28 @@ static int ilog2w(int v) {
   return l;
 }
 
+// Total blocks the split-K plan aims for, by filter size (measured on the R50
+// layers, profiles/conv_bench_r01_wgrad_blocks.txt): 1x1 filters do best with
+// fewer, longer splits (less fp32 partial traffic), 3x3 with 1024, the 7x7 stem
+// with 2048.  Overridable: PMD_WGRAD_BLOCKS_R1 / _R3 / _R7.
+static int env_int(const char* k, int dflt) {
+  const char* e = getenv(k);
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? v : dflt;
+}
+static int wgrad_target_blocks(int R) {
+  static const int t1 = env_int("PMD_WGRAD_BLOCKS_R1", 512);
+  static const int t3 = env_int("PMD_WGRAD_BLOCKS_R3", 1024);
+  static const int t7 = env_int("PMD_WGRAD_BLOCKS_R7", 2048);
+  return R == 1 ? t1 : (R <= 3 ? t3 : t7);
+}
+
 template <int BM>
 static void plan(const WgradArgs& a, int* splits_out, int* cps_out) {
   constexpr int BN = 128;
   const int tiles = ((a.K + BM - 1) / BM) * ((a.Kg + BN - 1) / BN);
   const int chunks = (a.M + BR - 1) / BR;
-  int splits = (1024 + tiles - 1) / tiles;
+  int splits = (wgrad_target_blocks(a.R) + tiles - 1) / tiles;
   const int max_splits = (chunks + 3) / 4;
   if (splits > max_splits) splits = max_splits;
   // keep the partial workspace bounded (<= 96 MiB)
