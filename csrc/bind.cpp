@@ -77,7 +77,8 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor wk, int64_t stride, int64_t pad, b
   }
   const int rc = pmd::conv_igemm_launch(bfp(x), bfp(wk), bfp_mut(y),
                                         want_stats ? stats.data_ptr<float>() : nullptr, N, H, W, C, P,
-                                        Q, K, R, S, (int)stride, (int)pad, false, nullptr, nullptr, cur_stream());
+                                        Q, K, R, S, (int)stride, (int)pad, false, nullptr, nullptr, nullptr,
+                                        cur_stream());
   CHECK_RC(rc, "conv_fwd");
   if (want_stats) return {y, stats};
   return {y};
@@ -91,7 +92,8 @@ Tensor conv_dgrad(Tensor dy, Tensor wkt, int64_t H, int64_t W, int64_t stride, i
                   c10::optional<Tensor> addend, c10::optional<Tensor> bn_mask,
                   c10::optional<Tensor> bn_y0, c10::optional<Tensor> bn_p0,
                   c10::optional<Tensor> bn_red0, c10::optional<Tensor> bn_y1,
-                  c10::optional<Tensor> bn_p1, c10::optional<Tensor> bn_red1) {
+                  c10::optional<Tensor> bn_p1, c10::optional<Tensor> bn_red1,
+                  c10::optional<Tensor> addend_mask) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONT(dy);
   CHECK_DEV(wkt); CHECK_BF16(wkt); CHECK_CONT(wkt);
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), K = dy.size(3);
@@ -106,6 +108,13 @@ Tensor conv_dgrad(Tensor dy, Tensor wkt, int64_t H, int64_t W, int64_t stride, i
     CHECK_BF16(*addend); CHECK_CONT(*addend);
     TORCH_CHECK(addend->sizes() == dx.sizes(), "addend shape");
     add = bfp(*addend);
+  }
+  const uint8_t* amask = nullptr;
+  if (addend_mask && addend_mask->defined()) {
+    TORCH_CHECK(add, "addend_mask needs an addend");
+    TORCH_CHECK(addend_mask->scalar_type() == torch::kUInt8 && addend_mask->is_contiguous() &&
+                addend_mask->numel() == dx.numel() / 8, "addend_mask must be uint8 [M, C/8]");
+    amask = addend_mask->data_ptr<uint8_t>();
   }
   pmd::BnReduceArgs bnr{};
   const bool fused = bn_red0 && bn_red0->defined();
@@ -131,7 +140,7 @@ Tensor conv_dgrad(Tensor dy, Tensor wkt, int64_t H, int64_t W, int64_t stride, i
   }
   // the gathered operand is dy (spatial P x Q, K channels); output spatial is H x W
   const int rc = pmd::conv_igemm_launch(bfp(dy), bfp(wkt), bfp_mut(dx), nullptr, N, P, Q, K, (int)H,
-                                        (int)W, Cp, R, S, (int)stride, (int)pad, true, add,
+                                        (int)W, Cp, R, S, (int)stride, (int)pad, true, add, amask,
                                         fused ? &bnr : nullptr, cur_stream());
   CHECK_RC(rc, "conv_dgrad");
   return dx;

@@ -33,6 +33,7 @@ struct ConvArgs {
   bf16_t* out;        // [M][Nout]
   float* stats;       // [kStatSlots][2][Nout] or nullptr
   const bf16_t* addend;  // optional [M][Nout] tensor added to the output (grad accumulation)
+  const uint8_t* addend_mask;  // optional ReLU bitmask gating the addend (identity-path dz = dout*mask)
   // optional fused BatchNorm-backward reduce over the (final, bf16) output tile
   // (dgrad of the conv that CONSUMED a BN+ReLU output): per channel n
   //   red[slot][0][n] += sum dz,  red[slot][1][n] += sum dz * (y - mean) * invstd
@@ -545,6 +546,11 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
         float f[8], g[8];
         unpack8(v, f);
         unpack8(*reinterpret_cast<const uint4*>(a.addend + orow * a.Nout + n), g);
+        if (a.addend_mask) {
+          const uint32_t am = a.addend_mask[orow * (a.Nout >> 3) + (n >> 3)];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) g[e] = ((am >> e) & 1u) ? g[e] : 0.f;
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e) f[e] += g[e];
         v = pack8(f);
@@ -678,7 +684,8 @@ static void launch_sel(const ConvArgs& a, hipStream_t st) {
 // Returns 0 on success, nonzero on unsupported shape.
 int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* stats, int N, int H,
                       int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
-                      bool dgrad, const bf16_t* addend, const BnReduceArgs* bnr, hipStream_t st) {
+                      bool dgrad, const bf16_t* addend, const uint8_t* addend_mask,
+                      const BnReduceArgs* bnr, hipStream_t st) {
   if (Cs % 8 != 0 || (Cs & (Cs - 1)) != 0) return 1;  // power-of-two channels (>= 8)
   if (Nout % 8 != 0) return 2;
   if (stride != 1 && stride != 2) return 3;
@@ -688,6 +695,7 @@ int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* s
   a.out = out;
   a.stats = stats;
   a.addend = addend;
+  a.addend_mask = addend ? addend_mask : nullptr;
   a.bn_mask = nullptr;
   for (int t = 0; t < 2; ++t) {
     a.bn_y[t] = nullptr;

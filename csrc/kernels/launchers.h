@@ -16,7 +16,8 @@ struct BnReduceArgs {
 };
 int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* stats, int N, int H,
                       int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
-                      bool dgrad, const bf16_t* addend, const BnReduceArgs* bnr, hipStream_t st);
+                      bool dgrad, const bf16_t* addend, const uint8_t* addend_mask,
+                      const BnReduceArgs* bnr, hipStream_t st);
 void conv_set_impl(int impl);  // 0 register staging, 1 LDS-DMA
 void conv_weight_prep_launch(const float* w, bf16_t* wk, bf16_t* wkt, int K, int RS, int C, int Cp,
                              hipStream_t st);

@@ -487,8 +487,11 @@ class _ResidualBlockFn(torch.autograd.Function):
             put(sbn.bias, g[3])
             dres = None
         else:
-            dyf, _, dres, g = _bn_backward(P, dout, omask, True, training, sync, countf,
-                                           yf, pf, fbn, want_dzm=True, pre=pre)
+            # the identity-path gradient dout * relu_mask is NOT materialised: the first
+            # stage's dgrad epilogue adds dout gated by the mask bits
+            dyf, _, _, g = _bn_backward(P, dout, omask, True, training, sync, countf,
+                                        yf, pf, fbn, pre=pre)
+            dres = (dout, omask)
         put(fbn.weight, g[0])
         put(fbn.bias, g[1])
         fuse = _state["fuse_bnred"] and training
@@ -519,17 +522,21 @@ class _ResidualBlockFn(torch.autograd.Function):
                 dh, pre_k = dgrad_fused(dy, wp, tuple(hin.shape), conv_m.stride, conv_m.padding,
                                         recs[k - 1])
             elif ctx.needs_input_grad[1]:
-                addend = dres
                 if shortcut is not None:
                     addend = P.conv_dgrad(dys, wps, tuple(x.shape), sconv.stride, sconv.padding)
+                    amask = None
+                else:
+                    addend, amask = dres
                 site = ctx.in_site
                 if site is not None:
                     # d(x) is the previous block's d(out): reduce ITS final BN(s) here
                     dx, site_red = P.conv_dgrad(dy, wp, tuple(x.shape), conv_m.stride,
-                                                conv_m.padding, addend, bnred=(site.mask, site.sets))
+                                                conv_m.padding, addend, bnred=(site.mask, site.sets),
+                                                addend_mask=amask)
                     site.put(dx, site_red)
                 else:
-                    dx = P.conv_dgrad(dy, wp, tuple(x.shape), conv_m.stride, conv_m.padding, addend)
+                    dx = P.conv_dgrad(dy, wp, tuple(x.shape), conv_m.stride, conv_m.padding, addend,
+                                      addend_mask=amask)
             put(conv_m.weight, _wgrad(P, dy, hin, wp, conv_m.stride, conv_m.padding,
                                       conv_m.weight))
         if shortcut is not None:

@@ -69,20 +69,21 @@ def conv_fwd(x, wpack, stride, pad, want_stats):
     return _C.conv_fwd(x, wpack[0], int(stride), int(pad), False, None)[0], None
 
 
-def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None, bnred=None):
-    """dX (+ addend).  ``bnred = (mask, [(y, params)] or [(y1, p1), (y2, p2)])``
-    fuses the BN-backward reduce of dX into the epilogue and returns
-    ``(dx, [slot buffers])`` (same contract as :func:`bn_bwd_reduce`)."""
+def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None, bnred=None, addend_mask=None):
+    """dX (+ addend [* relu bitmask addend_mask]).  ``bnred = (mask, [(y, params)] or
+    [(y1, p1), (y2, p2)])`` fuses the BN-backward reduce of dX into the epilogue
+    and returns ``(dx, [slot buffers])`` (same contract as :func:`bn_bwd_reduce`)."""
     if len(wpack) < 2:
         raise RuntimeError("dgrad image was not prepared (input did not require grad)")
     if bnred is None:
         return _C.conv_dgrad(dy, wpack[1], int(x_shape[1]), int(x_shape[2]), int(stride), int(pad),
-                             addend, None, None, None, None, None, None, None)
+                             addend, None, None, None, None, None, None, None, addend_mask)
     mask, sets = bnred
     bufs = [_acquire(y.shape[-1], y.device) for y, _ in sets]
     (y0, p0), (y1, p1) = sets[0], (sets[1] if len(sets) > 1 else (None, None))
     dx = _C.conv_dgrad(dy, wpack[1], int(x_shape[1]), int(x_shape[2]), int(stride), int(pad),
-                       addend, mask, y0, p0, bufs[0], y1, p1, bufs[1] if len(bufs) > 1 else None)
+                       addend, mask, y0, p0, bufs[0], y1, p1, bufs[1] if len(bufs) > 1 else None,
+                       addend_mask)
     return dx, bufs
 
 

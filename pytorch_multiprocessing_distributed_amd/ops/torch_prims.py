@@ -46,7 +46,7 @@ def conv_fwd(x, wpack, stride, pad, want_stats):
     return y, stats
 
 
-def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None, bnred=None):
+def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None, bnred=None, addend_mask=None):
     """dX (+ addend).  With ``bnred = (mask, [(y, params), ...])`` also returns
     the BN-backward reduce of the result for each set (the fused form of
     ``bn_bwd_reduce(dx, mask, y, params, relu=mask is not None)``)."""
@@ -56,7 +56,7 @@ def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None, bnred=None):
                                     _f(_nchw(dy)), stride=stride, padding=pad)
     dx = _nhwc(dx)
     if addend is not None:
-        dx = dx + _f(addend)
+        dx = dx + (_dzm(addend, addend_mask, True) if addend_mask is not None else _f(addend))
     dx = dx.to(dy.dtype)
     if bnred is None:
         return dx
