@@ -619,6 +619,39 @@ __global__ void conv_weight_prep_kernel(const float* __restrict__ w, bf16_t* __r
   }
 }
 
+// All conv weight images of a model in ONE launch (instead of one small launch
+// per conv per step): block b finds its descriptor by scanning the block-start
+// table (<= a few dozen entries) once, then grid-strides inside that weight.
+__global__ void conv_weight_prep_grouped_kernel(const WeightPrepDesc* __restrict__ descs,
+                                                const int* __restrict__ block_start, int n) {
+  __shared__ int e_sh;
+  if (threadIdx.x == 0) {
+    int e = 0;
+    while (e + 1 < n && block_start[e + 1] <= (int)blockIdx.x) ++e;
+    e_sh = e;
+  }
+  __syncthreads();
+  const WeightPrepDesc d = descs[e_sh];
+  const int lb = blockIdx.x - block_start[e_sh];
+  const int nb = block_start[e_sh + 1] - block_start[e_sh];
+  const int total = d.K * d.RS * d.Cp;
+  for (int i = lb * blockDim.x + threadIdx.x; i < total; i += nb * blockDim.x) {
+    const int c = i % d.Cp;
+    const int rs = (i / d.Cp) % d.RS;
+    const int k = i / (d.Cp * d.RS);
+    const float v = c < d.C ? d.w[((size_t)k * d.RS + rs) * d.C + c] : 0.f;
+    const bf16_t h = f2bf(v);
+    d.wk[i] = h;
+    if (d.wkt) d.wkt[((size_t)c * d.RS + rs) * d.K + k] = h;
+  }
+}
+
+void conv_weight_prep_grouped_launch(const WeightPrepDesc* d_descs, const int* d_block_start, int n,
+                                     int total_blocks, hipStream_t st) {
+  hipLaunchKernelGGL(conv_weight_prep_grouped_kernel, dim3(total_blocks), dim3(256), 0, st, d_descs,
+                     d_block_start, n);
+}
+
 static int ilog2(int v) {
   int l = 0;
   while ((1 << l) < v) ++l;

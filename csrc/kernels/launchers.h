@@ -18,7 +18,16 @@ int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* s
                       int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
                       bool dgrad, const bf16_t* addend, const uint8_t* addend_mask,
                       const BnReduceArgs* bnr, hipStream_t st);
-void conv_set_impl(int impl);  // 0 register staging, 1 LDS-DMA
+void conv_set_impl(int impl);
+// grouped weight-image prep (one launch for every conv of a model)
+struct WeightPrepDesc {
+  const float* w;  // fp32 [K][R][S][C] (channels_last parameter storage)
+  bf16_t* wk;      // [K][R][S][Cp]
+  bf16_t* wkt;     // [Cp][R][S][K] or nullptr
+  int K, RS, C, Cp;
+};
+void conv_weight_prep_grouped_launch(const WeightPrepDesc* d_descs, const int* d_block_start, int n,
+                                     int total_blocks, hipStream_t st);  // 0 register staging, 1 LDS-DMA
 void conv_weight_prep_launch(const float* w, bf16_t* wk, bf16_t* wkt, int K, int RS, int C, int Cp,
                              hipStream_t st);
 // split-K plan: number of partial slices the workspace must hold ([splits][K][R*S*C] fp32)

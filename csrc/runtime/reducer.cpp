@@ -151,11 +151,13 @@ class Reducer {
 
 void register_xgmi(pybind11::module& m);
 void register_trace(pybind11::module& m);
+void register_weights(pybind11::module& m);
 
 void register_runtime(pybind11::module& m) {
   namespace py = pybind11;
   register_xgmi(m);
   register_trace(m);
+  register_weights(m);
   py::class_<Reducer>(m, "Reducer")
       .def(py::init<c10::intrusive_ptr<c10d::ProcessGroup>, at::Tensor, std::vector<int64_t>,
                     std::vector<int64_t>, bool, bool>(),

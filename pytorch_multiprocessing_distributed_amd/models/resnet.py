@@ -200,12 +200,30 @@ class ResNet(nn.Module):
         f8 = OF.get_fp8()
         if f8 is not None and self.training and torch.is_grad_enabled():
             f8.update()                          # delayed scaling: one device op per step
-        out = OF.conv_bn_act(x, self.conv1, self.bn1, relu=True)
-        if self.stem == "imagenet":
-            out = OF.max_pool3x3s2(out)
-        out = self.layer4(self.layer3(self.layer2(self.layer1(out))))
+        with OF.weight_images(self._weight_set(x)):
+            out = OF.conv_bn_act(x, self.conv1, self.bn1, relu=True)
+            if self.stem == "imagenet":
+                out = OF.max_pool3x3s2(out)
+            out = self.layer4(self.layer3(self.layer2(self.layer1(out))))
         out = OF.global_avg_pool(out)            # [N, C] fp32
         return OF.linear(out, self.linear)
+
+    def _weight_set(self, x):
+        """All conv weight images in one grouped launch per forward (GPU path)."""
+        P = OF.prims_for(x)
+        if not getattr(P, "SUPPORTS_FP8", False):          # the gfx950 prims only
+            return None
+        ws = self.__dict__.get("_pmd_wset")
+        key = (x.shape[-1], self.conv1.weight.data_ptr(), self.linear.weight.data_ptr())
+        if ws is None or self.__dict__.get("_pmd_wset_key") != key:
+            entries = [(self.conv1, x.shape[-1], False)]
+            for mod in self.modules():
+                if isinstance(mod, nn.Conv2d) and mod is not self.conv1:
+                    entries.append((mod, mod.in_channels, True))
+            ws = OF.WeightImageSet(entries)
+            self.__dict__["_pmd_wset"] = ws
+            self.__dict__["_pmd_wset_key"] = key
+        return ws
 
 
 def _factory(block, nb):

@@ -46,7 +46,8 @@ _state = {"bn_sync": None, "force_torch": os.environ.get("PMD_PRIMS", "") == "to
           # fuse each BN-backward reduce into the dgrad epilogue that produces its input
           "fuse_bnred": os.environ.get("PMD_FUSE_BNRED", "1") != "0",
           "fused_site_hits": 0,
-          "fp8": None}          # Fp8Scaling when the block convs run in fp8 (config 5)
+          "fp8": None,          # Fp8Scaling when the block convs run in fp8 (config 5)
+          "wimg": None}         # WeightImageSet of the running forward (grouped weight prep)
 
 
 def set_bn_sync(comm):
@@ -56,6 +57,59 @@ def set_bn_sync(comm):
 
 def get_bn_sync():
     return _state["bn_sync"]
+
+
+class WeightImageSet:
+    """bf16 weight images of every conv of a model, refreshed by ONE grouped
+    kernel per forward (native ``_C.WeightImages``) instead of one prep launch
+    per conv.  ``entries``: [(conv module, padded input channels, want dgrad image)]."""
+
+    def __init__(self, entries):
+        from .native import C
+        self.entries = list(entries)
+        self.index = {(id(m.weight), cp, wt): i for i, (m, cp, wt) in enumerate(self.entries)}
+        self._c = C.WeightImages([m.weight for m, _, _ in self.entries],
+                                 [cp for _, cp, _ in self.entries], [wt for _, _, wt in self.entries])
+
+    def refresh(self):
+        self._c.refresh()
+
+    def lookup(self, w, cin, want_t):
+        i = self.index.get((id(w), cin, want_t))
+        if i is None and not want_t:
+            i = self.index.get((id(w), cin, True))   # a superset of what was asked
+        return None if i is None else tuple(self._c.get(i))
+
+
+def _weight_images(P, w, dtype, cin, want_t):
+    wi = _state["wimg"]
+    if wi is not None:
+        r = wi.lookup(w, cin, want_t)
+        if r is not None:
+            return r
+    return P.conv_weight(w, dtype, cin, want_t)
+
+
+def _conv_weight(P, conv_m, dtype, cin, want_t):
+    return _weight_images(P, conv_m.weight, dtype, cin, want_t)
+
+
+class weight_images:
+    """Context manager: install ``wset`` (refreshed) for the duration of a forward."""
+
+    def __init__(self, wset):
+        self.wset = wset
+
+    def __enter__(self):
+        if self.wset is not None:
+            self.wset.refresh()
+        self.prev = _state["wimg"]
+        _state["wimg"] = self.wset
+        return self.wset
+
+    def __exit__(self, *exc):
+        _state["wimg"] = self.prev
+        return False
 
 
 def set_fp8(scaling):
@@ -258,7 +312,7 @@ class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, stride, pad, want_stats):
         P = prims_for(x)
-        wpack = P.conv_weight(w, x.dtype, x.shape[-1], x.requires_grad)
+        wpack = _weight_images(P, w, x.dtype, x.shape[-1], x.requires_grad)
         y, stats = P.conv_fwd(x, wpack, stride, pad, want_stats)
         ctx.save_for_backward(x, *wpack)
         ctx.conf = (stride, pad, w)
@@ -395,7 +449,7 @@ class _ResidualBlockFn(torch.autograd.Function):
         h = x
         recs = []
         for conv_m, bn in stages:
-            wp = P.conv_weight(conv_m.weight, x.dtype, h.shape[-1], True)
+            wp = _conv_weight(P, conv_m, x.dtype, h.shape[-1], True)
             y, st = _conv_fwd_any(P, f8, h, hq, wp, conv_m, training)
             p, _, count = _bn_forward_params(P, y, st, bn, training, sync)
             if f8 is not None:
@@ -407,12 +461,12 @@ class _ResidualBlockFn(torch.autograd.Function):
             recs.append((h, wp, y, p, zmask, count))
             h = z
         fconv, fbn = final
-        wpf = P.conv_weight(fconv.weight, x.dtype, h.shape[-1], True)
+        wpf = _conv_weight(P, fconv, x.dtype, h.shape[-1], True)
         yf, stf = _conv_fwd_any(P, f8, h, hq, wpf, fconv, training)
         osite = f8.site(("a", id(fbn))) if f8 is not None else None
         if shortcut is not None:
             sconv, sbn = shortcut
-            wps = P.conv_weight(sconv.weight, x.dtype, x.shape[-1], x.requires_grad)
+            wps = _conv_weight(P, sconv, x.dtype, x.shape[-1], x.requires_grad)
             ys, sts = _conv_fwd_any(P, f8, x, xq, wps, sconv, training)
             pf, ps, countf = _bn_forward_params(P, yf, stf, fbn, training, sync, ys, sts, sbn)
             r = P.bn_apply(yf, pf, None, ys, ps, relu=True, **({"fp8": osite} if osite else {}))
