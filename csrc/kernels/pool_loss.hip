@@ -13,84 +13,82 @@
 namespace pmd {
 
 // ---------------------------------------------------------------- maxpool
-// x [N,H,W,C] -> out [N,P,Q,C], arg [N,P,Q,C] (uint8 tap index 0..8)
-__global__ void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ out,
-                                   uint8_t* __restrict__ arg, int N, int H, int W, int C, int P,
-                                   int Q) {
+// x [N,H,W,C] -> out [N,P,Q,C], arg [N,P,Q,C] (uint8 tap index 0..8).
+// grid.y = output row (n, p), x covers Q * C/8 chunks: 32-bit index math only
+// (C/8 a power of two -> shift/mask), no 64-bit divisions per element.
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restrict__ x,
+                                                          bf16_t* __restrict__ out,
+                                                          uint8_t* __restrict__ arg, int N, int H,
+                                                          int W, int C, int P, int Q, int log2C8) {
   const int C8 = C >> 3;
-  const long long total = (long long)N * P * Q * C8;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int cc = (int)(i % C8);
-    long long pix = i / C8;
-    const int q = (int)(pix % Q);
-    pix /= Q;
-    const int p = (int)(pix % P);
-    const int n = (int)(pix / P);
-    float best[8];
-    int bi[8];
+  const int row = blockIdx.y;  // n * P + p
+  const int n = row / P, p = row - (row / P) * P;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= Q * C8) return;
+  const int q = j >> log2C8, cc = j & (C8 - 1);
+  float best[8];
+  int bi[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      best[k] = -INFINITY;
-      bi[k] = 0;
-    }
-    for (int t = 0; t < 9; ++t) {
-      const int ih = p * 2 - 1 + t / 3, iw = q * 2 - 1 + t % 3;
-      if ((unsigned)ih >= (unsigned)H || (unsigned)iw >= (unsigned)W) continue;
-      float v[8];
-      unpack8(*reinterpret_cast<const uint4*>(x + (((size_t)n * H + ih) * W + iw) * C + cc * 8), v);
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (v[k] > best[k] || (v[k] != v[k] && best[k] == best[k])) {
-          best[k] = v[k];
-          bi[k] = t;
-        }
-    }
-    reinterpret_cast<uint4*>(out)[i] = pack8(best);
-    uint2 packed;
-    packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
-    packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
-    reinterpret_cast<uint2*>(arg)[i] = packed;
+  for (int k = 0; k < 8; ++k) {
+    best[k] = -INFINITY;
+    bi[k] = 0;
   }
+  const bf16_t* xb = x + (size_t)n * H * W * C + cc * 8;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int ih = p * 2 - 1 + t / 3, iw = q * 2 - 1 + t % 3;
+    if ((unsigned)ih >= (unsigned)H || (unsigned)iw >= (unsigned)W) continue;
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(xb + ((size_t)ih * W + iw) * C), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (v[k] > best[k] || (v[k] != v[k] && best[k] == best[k])) {
+        best[k] = v[k];
+        bi[k] = t;
+      }
+  }
+  const size_t o = (size_t)row * Q * C8 + j;
+  reinterpret_cast<uint4*>(out)[o] = pack8(best);
+  uint2 packed;
+  packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
+  packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
+  reinterpret_cast<uint2*>(arg)[o] = packed;
 }
 
-// gather form: every input chunk sums the dout of the (<= 4) windows whose argmax is it
-__global__ void maxpool_bwd_kernel(const bf16_t* __restrict__ dout, const uint8_t* __restrict__ arg,
-                                   bf16_t* __restrict__ dx, int N, int H, int W, int C, int P,
-                                   int Q) {
+// gather form: every input chunk sums the dout of the (<= 4) windows whose argmax is it.
+// grid.y = input row (n, h), x covers W * C/8 chunks.
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restrict__ dout,
+                                                          const uint8_t* __restrict__ arg,
+                                                          bf16_t* __restrict__ dx, int N, int H, int W,
+                                                          int C, int P, int Q, int log2C8) {
   const int C8 = C >> 3;
-  const long long total = (long long)N * H * W * C8;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int cc = (int)(i % C8);
-    long long pix = i / C8;
-    const int w = (int)(pix % W);
-    pix /= W;
-    const int h = (int)(pix % H);
-    const int n = (int)(pix / H);
-    float acc[8];
+  const int row = blockIdx.y;  // n * H + h
+  const int n = row / H, h = row - (row / H) * H;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= W * C8) return;
+  const int w = j >> log2C8, cc = j & (C8 - 1);
+  float acc[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-    const int p_lo = (h + 1 - 2 + 1) >> 1 > 0 ? (h + 1 - 2 + 1) >> 1 : 0;  // ceil((h-1)/2)
-    const int p_hi = (h + 1) >> 1 < P - 1 ? (h + 1) >> 1 : P - 1;
-    const int q_lo = (w + 1 - 2 + 1) >> 1 > 0 ? (w + 1 - 2 + 1) >> 1 : 0;
-    const int q_hi = (w + 1) >> 1 < Q - 1 ? (w + 1) >> 1 : Q - 1;
-    for (int p = p_lo; p <= p_hi; ++p)
-      for (int q = q_lo; q <= q_hi; ++q) {
-        const int dh = h - (p * 2 - 1), dw = w - (q * 2 - 1);
-        if (dh < 0 || dh > 2 || dw < 0 || dw > 2) continue;
-        const int tap = dh * 3 + dw;
-        const size_t o = (((size_t)n * P + p) * Q + q) * C8 + cc;
-        const uint2 a = reinterpret_cast<const uint2*>(arg)[o];
-        float g[8];
-        unpack8(reinterpret_cast<const uint4*>(dout)[o], g);
-        const uint32_t aw[2] = {a.x, a.y};
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  const int p_lo = h > 0 ? h >> 1 : 0;             // windows p with 2p-1 <= h <= 2p+1
+  const int p_hi = min((h + 1) >> 1, P - 1);
+  const int q_lo = w > 0 ? w >> 1 : 0;
+  const int q_hi = min((w + 1) >> 1, Q - 1);
+  for (int p = p_lo; p <= p_hi; ++p)
+    for (int q = q_lo; q <= q_hi; ++q) {
+      const int dh = h - (p * 2 - 1), dw = w - (q * 2 - 1);
+      if (dh < 0 || dh > 2 || dw < 0 || dw > 2) continue;
+      const int tap = dh * 3 + dw;
+      const size_t o = (((size_t)n * P + p) * Q + q) * C8 + cc;
+      const uint2 a = reinterpret_cast<const uint2*>(arg)[o];
+      float g[8];
+      unpack8(reinterpret_cast<const uint4*>(dout)[o], g);
+      const uint32_t aw[2] = {a.x, a.y};
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if ((int)((aw[k >> 2] >> ((k & 3) * 8)) & 0xff) == tap) acc[k] += g[k];
-      }
-    reinterpret_cast<uint4*>(dx)[i] = pack8(acc);
-  }
+      for (int k = 0; k < 8; ++k)
+        if ((int)((aw[k >> 2] >> ((k & 3) * 8)) & 0xff) == tap) acc[k] += g[k];
+    }
+  reinterpret_cast<uint4*>(dx)[(size_t)row * W * C8 + j] = pack8(acc);
 }
 
 // ---------------------------------------------------------------- avgpool
@@ -258,18 +256,25 @@ static int grid_for(long long work, int cap = 4096) {
   return b < 1 ? 1 : (int)b;
 }
 
+static int log2_exact(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return (1 << l) == v ? l : -1;
+}
 int maxpool_fwd_launch(const bf16_t* x, bf16_t* out, uint8_t* arg, int N, int H, int W, int C, int P,
                        int Q, hipStream_t st) {
-  if (C % 8) return 1;
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((long long)N * P * Q * (C / 8))), dim3(256), 0,
-                     st, x, out, arg, N, H, W, C, P, Q);
+  const int l = log2_exact(C / 8);
+  if (C % 8 || l < 0 || N * P > 65535) return 1;
+  const dim3 grid((Q * (C / 8) + 255) / 256, N * P);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, grid, dim3(256), 0, st, x, out, arg, N, H, W, C, P, Q, l);
   return 0;
 }
 int maxpool_bwd_launch(const bf16_t* dout, const uint8_t* arg, bf16_t* dx, int N, int H, int W, int C,
                        int P, int Q, hipStream_t st) {
-  if (C % 8) return 1;
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((long long)N * H * W * (C / 8))), dim3(256), 0,
-                     st, dout, arg, dx, N, H, W, C, P, Q);
+  const int l = log2_exact(C / 8);
+  if (C % 8 || l < 0 || N * H > 65535) return 1;
+  const dim3 grid((W * (C / 8) + 255) / 256, N * H);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, grid, dim3(256), 0, st, dout, arg, dx, N, H, W, C, P, Q, l);
   return 0;
 }
 int avgpool_fwd_launch(const bf16_t* x, float* out, int N, int HW, int C, hipStream_t st) {
