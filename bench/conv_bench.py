@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--json", default="")
     ap.add_argument("--only", default="")
     ap.add_argument("--impls", default="5", help="conv staging/pipeline impls to time (see conv_igemm.hip; 5 = per-shape default)")
+    ap.add_argument("--wimpls", default="", help="also time these wgrad staging impls (conv_wgrad.hip)")
     ap.add_argument("--no-miopen", action="store_true")
     ap.add_argument("--fp8", action="store_true", help="also time the e4m3 scaled-MFMA forward conv")
     ap.add_argument("--bnred", action="store_true",
@@ -93,6 +94,13 @@ def main():
                        timeit(lambda: HP.conv_wgrad(dy, x, tuple(wp[0].shape), st, pad), a.iters))
         t_f, t_d, t_w = per[impls[-1]]
         f8txt = ""
+        if a.wimpls:
+            wt = []
+            for wi in [int(v) for v in a.wimpls.split(",")]:
+                _C.conv_wgrad_set_impl(wi)
+                wt.append(timeit(lambda: HP.conv_wgrad(dy, x, tuple(wp[0].shape), st, pad), a.iters))
+            _C.conv_wgrad_set_impl(1)
+            f8txt += "   wgrad impls " + "/".join(f"{flops / t / 1e9:.0f}" for t in wt)
         if a.bnred and C != 8:
             yb = torch.randn_like(x)
             pb = torch.stack([torch.zeros(C, device=dev), torch.ones(C, device=dev),

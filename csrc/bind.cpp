@@ -565,6 +565,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   pmd::register_runtime(m);
   m.def("conv_weight_prep", &conv_weight_prep);
   m.def("conv_set_impl", &pmd::conv_set_impl, "conv staging/pipeline variant 0-4, 5 = per-shape default");
+  m.def("conv_wgrad_set_impl", &pmd::conv_wgrad_set_impl,
+        "wgrad staging variant: 0 registers, 1 LDS-DMA 64x2 (default), 2 LDS-DMA 32x4, 3 LDS-DMA 64x3");
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);

@@ -216,6 +216,190 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
       }
 }
 
+// LDS-DMA variant: both operand tiles are copied global->LDS with
+// global_load_lds_dwordx4 (no VGPR round trip, no ds_write pass) into an NST-deep
+// ring of BR-row stages, ONE barrier per stage (publishes stage ch and retires the
+// reads of the buffer the next DMA overwrites), counted vmcnt so NST-2 stages stay
+// in flight across it.  The DMA writes lane-linearly, and the thread->(row, 16-B
+// chunk) map of the register path is already lane-linear per wave (a wave covers
+// 1024 contiguous bytes = whole rows), so the 32-B-window swizzle moves to the
+// SOURCE: the thread at physical chunk p of a row loads logical window
+// (p >> 1) ^ swz(row).  swz only depends on row bits 0..3 and every pass adds a
+// multiple of 16 rows, so each thread's logical column (hence its im2col tap and
+// channel) stays fixed for the whole kernel, exactly as on the register path.
+__device__ __attribute__((aligned(16))) unsigned char g_wzero16[64];
+
+template <int N>
+__device__ __forceinline__ void wg_wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int BRD, int NST>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_dma_kernel(WgradArgs a) {
+  constexpr int MI = BM / 32, NI = BN / 32;
+  constexpr int A_BYTES = BRD * BM * 2, B_BYTES = BRD * BN * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tilesM = a.K / BM + (a.K % BM != 0);
+  const int tilesN = (a.Kg + BN - 1) / BN;
+  const int tiles = tilesM * tilesN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = L / tiles;
+  const int t = L % tiles;
+  const int k0 = (t / tilesN) * BM;
+  const int g0 = (t % tilesN) * BN;
+  const int mbeg = split * a.chunks_per_split * BR;  // split plan is in BR=64-row chunks
+  if (mbeg >= a.M) return;
+  int mend = mbeg + a.chunks_per_split * BR;
+  if (mend > a.M) mend = a.M;
+  const int nchunks = (mend - mbeg + BRD - 1) / BRD;
+
+  constexpr int CA = BM / 8, RA = 256 / CA, PA = BRD / RA;
+  constexpr int CB = BN / 8, RB = 256 / CB, PB = BRD / RB;
+  static_assert(PA >= 1 && PB >= 1 && RA % 16 == 0 && RB % 16 == 0, "DMA wgrad tile shape");
+  constexpr int LPT = PA + PB;  // DMA instructions per thread per stage
+  const int a_row = tid / CA, b_row = tid / CB;
+  const int a_pc = tid % CA, b_pc = tid % CB;  // physical 16-B chunk in the row
+  const int a_col = ((((a_pc >> 1) ^ swz<BM * 2>(a_row)) << 1) | (a_pc & 1)) * 8;
+  const int b_col = ((((b_pc >> 1) ^ swz<BN * 2>(b_row)) << 1) | (b_pc & 1)) * 8;
+  const bool a_colok = k0 + a_col < a.K;
+  const int kg = g0 + b_col;
+  const bool b_colok = kg < a.Kg;
+  const int tap = b_colok ? (kg >> a.log2C) : 0;
+  const int cch = kg & (a.C - 1);
+  const int rr = tap / a.S, ss = tap - (tap / a.S) * a.S;
+  int bn_[PB], bp_[PB], bq_[PB];
+  const int pq = a.P * a.Q;
+#pragma unroll
+  for (int i = 0; i < PB; ++i) {
+    const int m = mbeg + b_row + RB * i;
+    const int n = m / pq, rem = m - n * pq;
+    bn_[i] = n;
+    bp_[i] = rem / a.Q;
+    bq_[i] = rem - bp_[i] * a.Q;
+  }
+  const int dq = BRD % a.Q, dp = (BRD / a.Q) % a.P, dn = BRD / pq;
+  const int wid_s = __builtin_amdgcn_readfirstlane(wid);
+
+  auto load = [&](int ch, int buf) {
+    const int mb = mbeg + ch * BRD;
+    char* As = smem + buf * STAGE;
+    char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < PA; ++i) {
+      const int m = mb + a_row + RA * i;
+      const void* src = (a_colok && m < mend) ? (const void*)(a.dy + (size_t)m * a.K + k0 + a_col)
+                                             : (const void*)g_wzero16;
+      char* dst = As + (RA * i) * (BM * 2) + wid_s * 1024;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+      const int m = mb + b_row + RB * i;
+      const int ih = bp_[i] * a.stride - a.pad + rr;
+      const int iw = bq_[i] * a.stride - a.pad + ss;
+      const bool ok = b_colok && m < mend && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      const size_t pix = ((size_t)bn_[i] * a.H + ih) * a.W + iw;
+      const void* src = ok ? (const void*)(a.x + (pix << a.log2C) + cch) : (const void*)g_wzero16;
+      char* dst = Bs + (RB * i) * (BN * 2) + wid_s * 1024;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      int q = bq_[i] + dq, c1 = q >= a.Q;
+      q -= c1 ? a.Q : 0;
+      int p = bp_[i] + dp + c1, c2 = p >= a.P;
+      p -= c2 ? a.P : 0;
+      bq_[i] = q;
+      bp_[i] = p;
+      bn_[i] += dn + c2;
+    }
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < BRD / 32; ++ks) {
+      bf16x8 af[MI], bfg[NI];
+      const int r0 = ks * 32 + 8 * g + q4;
+      typedef __attribute__((ext_vector_type(8))) short s16x8;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int col = wm * (BM / 2) + i * 16 + 4 * p4;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(As + toff<BM>(r0, col)));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(As + toff<BM>(r0 + 4, col)));
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int col = wn * (BN / 2) + j * 16 + 4 * p4;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(Bs + toff<BN>(r0, col)));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(Bs + toff<BN>(r0 + 4, col)));
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfg[j] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < nchunks) load(s, s);
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const int rem = min(NST - 2, nchunks - 1 - ch);
+    if constexpr (NST >= 4) {
+      if (rem >= 2) wg_wait_vmcnt<2 * LPT>();
+      else if (rem == 1) wg_wait_vmcnt<LPT>();
+      else wg_wait_vmcnt<0>();
+    } else if constexpr (NST == 3) {
+      if (rem >= 1) wg_wait_vmcnt<LPT>();
+      else wg_wait_vmcnt<0>();
+    } else {
+      wg_wait_vmcnt<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (ch + NST - 1 < nchunks) load(ch + NST - 1, (ch + NST - 1) % NST);
+    compute(ch % NST);
+  }
+
+  float* dst = a.ws ? a.ws + (size_t)split * a.K * a.Kg : a.dw;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = k0 + wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + e;
+        const int gg = g0 + wn * (BN / 2) + j * 16 + (lane & 15);
+        if (k < a.K && gg < a.Kg) {
+          float* p = dst + (size_t)k * a.Kg + gg;
+          if (a.ws)
+            *p = acc[i][j][e];
+          else
+            *p += acc[i][j][e];
+        }
+      }
+}
+
 // dW[i] += sum_s ws[s][i].  blockIdx.y = split group of <= kSplitGroup slices:
 // one group -> plain read-modify-write in fixed order (deterministic); several
 // groups (tiny outputs with hundreds of splits) -> one fp32 atomic per group.
@@ -272,6 +456,18 @@ static int wgrad_target_blocks(int R) {
   static const int t3 = env_int("PMD_WGRAD_BLOCKS_R3", 1024);
   static const int t7 = env_int("PMD_WGRAD_BLOCKS_R7", 2048);
   return R == 1 ? t1 : (R <= 3 ? t3 : t7);
+}
+
+// Staging variant (conv_wgrad_set_impl or PMD_WGRAD_IMPL): 0 register staging
+// (2 stages), 1 LDS-DMA 64-row stages x2, 2 LDS-DMA 32-row x4, 3 LDS-DMA 64-row x3.
+static int g_wgrad_impl = -1;
+void conv_wgrad_set_impl(int impl) { g_wgrad_impl = impl; }
+static int wgrad_impl() {
+  if (g_wgrad_impl < 0) {
+    const char* e = getenv("PMD_WGRAD_IMPL");
+    g_wgrad_impl = (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 1;
+  }
+  return g_wgrad_impl;
 }
 
 template <int BM>
@@ -341,10 +537,25 @@ int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, float* ws, i
   if (splits > 1 && !ws) return 5;
   const int BM = K == 64 ? 64 : 128;
   const int tiles = ((a.K + BM - 1) / BM) * ((a.Kg + 127) / 128);
-  if (K == 64)
-    hipLaunchKernelGGL((conv_wgrad_kernel<64, 128>), dim3(tiles * splits), dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), dim3(tiles * splits), dim3(256), 0, st, a);
+  const dim3 grid(tiles * splits);
+  switch (wgrad_impl()) {
+    case 0:
+      if (K == 64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), grid, dim3(256), 0, st, a);
+      break;
+    case 2:  // DMA, 32-row stages, 4-deep ring
+      if (K == 64) hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 128, 32, 4>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 32, 4>), grid, dim3(256), 0, st, a);
+      break;
+    case 3:  // DMA, 64-row stages, 3-deep ring (1 block/CU at BM=128)
+      if (K == 64) hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 128, 64, 3>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 64, 3>), grid, dim3(256), 0, st, a);
+      break;
+    default:  // 1: DMA, 64-row stages, 2-deep ring
+      if (K == 64) hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 128, 64, 2>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 64, 2>), grid, dim3(256), 0, st, a);
+      break;
+  }
   if (splits > 1) {
     const long long n4 = (long long)a.K * a.Kg / 4;
     const int groups = (splits + kSplitGroup - 1) / kSplitGroup;

@@ -19,6 +19,7 @@ int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* s
                       bool dgrad, const bf16_t* addend, const uint8_t* addend_mask,
                       const BnReduceArgs* bnr, hipStream_t st);
 void conv_set_impl(int impl);
+void conv_wgrad_set_impl(int impl);
 // grouped weight-image prep (one launch for every conv of a model)
 struct WeightPrepDesc {
   const float* w;  // fp32 [K][R][S][C] (channels_last parameter storage)

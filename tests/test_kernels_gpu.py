@@ -81,6 +81,31 @@ def test_conv_fwd_dgrad_wgrad(shape):
     _close(dw, dwr, 2e-3)
 
 
+@pytest.mark.parametrize("impl", [0, 1, 2, 3])
+@pytest.mark.parametrize("shape", R50_SHAPES + CIFAR_SHAPES, ids=lambda s: "C%d_H%d_K%d_R%d_s%d" % s)
+def test_wgrad_variants(shape, impl):
+    """Every operand-staging variant of the split-K wgrad kernel (register
+    staging; LDS-DMA rings of 64-row x2 / 32-row x4 / 64-row x3 stages), with a
+    batch large enough that several splits and ragged split tails occur."""
+    from pytorch_multiprocessing_distributed_amd.ops.native import C as _C
+    HP = _hp()
+    torch.manual_seed(2)
+    C, H, K, R, st = shape
+    pad = R // 2
+    N = _batch_for(H) + 1  # odd batch: the last split ends mid-chunk
+    x = torch.randn(N, H, H, C, device=DEV).to(torch.bfloat16)
+    P = (H + 2 * pad - R) // st + 1
+    dy = torch.randn(N, P, P, K, device=DEV).to(torch.bfloat16)
+    dwr = TP.conv_wgrad(dy, x, (K, R, R, C), st, pad)
+    _C.conv_wgrad_set_impl(impl)
+    try:
+        dw = HP.conv_wgrad(dy, x, (K, R, R, C), st, pad)
+        torch.cuda.synchronize()
+    finally:
+        _C.conv_wgrad_set_impl(1)
+    _close(dw, dwr, 2e-3)
+
+
 @pytest.mark.parametrize("impl", [0, 1, 3, 4, 6])
 @pytest.mark.parametrize("shape", R50_SHAPES + CIFAR_SHAPES, ids=lambda s: "C%d_H%d_K%d_R%d_s%d" % s)
 def test_conv_pipeline_variants(shape, impl):
