@@ -53,6 +53,8 @@ def main():
     ap.add_argument("--json", default="")
     ap.add_argument("--only", default="")
     ap.add_argument("--impls", default="5", help="conv staging/pipeline impls to time (see conv_igemm.hip; 5 = per-shape default)")
+    ap.add_argument("--tiles", default="", help="also time fwd/dgrad with these conv tile policies "
+                    "(conv_set_tile) as tile[:bigpipe], e.g. 1,2:0,2:1,3:0")
     ap.add_argument("--wimpls", default="", help="also time these wgrad staging impls (conv_wgrad.hip)")
     ap.add_argument("--no-miopen", action="store_true")
     ap.add_argument("--fp8", action="store_true", help="also time the e4m3 scaled-MFMA forward conv")
@@ -94,6 +96,18 @@ def main():
                        timeit(lambda: HP.conv_wgrad(dy, x, tuple(wp[0].shape), st, pad), a.iters))
         t_f, t_d, t_w = per[impls[-1]]
         f8txt = ""
+        if a.tiles and C != 8:
+            tt = []
+            for spec in a.tiles.split(","):
+                tl, _, bp = spec.partition(":")
+                _C.conv_set_tile(int(tl))
+                _C.conv_set_big_pipe(int(bp or 0))
+                tt.append((timeit(fwd, a.iters),
+                           timeit(lambda: HP.conv_dgrad(dy, wp, tuple(x.shape), st, pad), a.iters)))
+            _C.conv_set_tile(0)
+            _C.conv_set_big_pipe(0)
+            f8txt += "   tiles fwd " + "/".join(f"{flops / t[0] / 1e9:.0f}" for t in tt)
+            f8txt += " dgrad " + "/".join(f"{flops / t[1] / 1e9:.0f}" for t in tt)
         if a.wimpls:
             wt = []
             for wi in [int(v) for v in a.wimpls.split(",")]:

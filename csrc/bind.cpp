@@ -565,6 +565,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   pmd::register_runtime(m);
   m.def("conv_weight_prep", &conv_weight_prep);
   m.def("conv_set_impl", &pmd::conv_set_impl, "conv staging/pipeline variant 0-4, 5 = per-shape default");
+  m.def("conv_set_tile", &pmd::conv_set_tile,
+        "conv fwd/dgrad tile policy: 0 auto, 1 128-row only, 2 256x128, 3 256x256 where legal");
+  m.def("conv_set_big_pipe", &pmd::conv_set_big_pipe,
+        "256-row conv tiles: 0 BK=64 x2 stages, 1 BK=64 x3 (256x128 only), 2 BK=32 x4");
+  m.def("conv_set_autotune", &pmd::conv_set_autotune, "per-shape conv kernel autotuning on/off");
+  m.def("conv_autotune_entries", &pmd::conv_autotune_entries);
+  m.def("conv_autotune_clear", &pmd::conv_autotune_clear);
   m.def("conv_wgrad_set_impl", &pmd::conv_wgrad_set_impl,
         "wgrad staging variant: 0 registers, 1 LDS-DMA 64x2 (default), 2 LDS-DMA 32x4, 3 LDS-DMA 64x3");
   m.def("conv_fwd", &conv_fwd);

@@ -23,7 +23,11 @@
 // atomic per channel per block), then the tile is staged through LDS and
 // written with coalesced 16-byte row stores.
 #include "common.h"
+#include <stdio.h>
 #include <stdlib.h>
+
+#include <map>
+#include <mutex>
 
 namespace pmd {
 
@@ -82,18 +86,25 @@ __device__ __forceinline__ int swz(int row) {
 // instead of 8 of 16 -- more room for the gather math and LDS reads).  Needs
 // the LDS-DMA uniform-tap path with BK=64; chunk swizzle phys = q ^ ((row>>1)&7)
 // keeps the 32-row ds_read_b128 lane groups conflict-free.
-template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA, bool MF32 = false>
-__global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
-  static_assert(DMA || (BK == 64 && NST == 2), "register staging: BK=64, 2 stages");
+// WM x WN waves (NT = 64 WM WN threads): 2x2 = the 128-row tiles at 2 blocks/CU;
+// 4x2 / 2x4 = 256-row tiles at one 8-wave block per CU, i.e. half the operand
+// bytes per MFMA FLOP from L2 (128x128: 64 FLOP/B -> 256x128: 85, 256x256: 128),
+// for the layers whose grid still fills the chip with the bigger tile.
+template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA, bool MF32 = false,
+          int WM = 2, int WN = 2>
+__global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a) {
+  constexpr int NW = WM * WN, NT = 64 * NW;
+  static_assert(DMA || (BK == 64 && NST == 2 && NW == 4), "register staging: BK=64, 2 stages, 4 waves");
   static_assert(!MF32 || (DMA && BK == 64), "32x32 MFMA path: LDS-DMA, BK=64");
   constexpr int CH = BK / 8;                      // 16-B chunks per LDS row
   constexpr int RPI = DMA ? 64 / CH : 32;         // rows per load instruction (wave / block)
-  constexpr int PA = DMA ? BM / (4 * RPI) : BM / 32;  // A load instructions per thread per tile
-  constexpr int PB = DMA ? BN / (4 * RPI) : BN / 32;
+  constexpr int PA = DMA ? BM / (NW * RPI) : BM / 32;  // A load instructions per thread per tile
+  constexpr int PB = DMA ? BN / (NW * RPI) : BN / 32;
   static_assert(PA >= 1 && PB >= 1, "tile too small for this BK");
+  static_assert(!DMA || ((BM / NW) % RPI == 0 && (BN / NW) % RPI == 0), "wave row slabs");
   constexpr int LPT = PA + PB;
-  constexpr int MI = BM / 32;        // 16-row MFMA tiles per wave (wave covers BM/2)
-  constexpr int NI = BN / 32;        // 16-col MFMA tiles per wave
+  constexpr int MI = BM / (16 * WM);  // 16-row MFMA tiles per wave
+  constexpr int NI = BN / (16 * WN);  // 16-col MFMA tiles per wave
   constexpr int LDR = DMA ? BK : BK + 8;  // LDS row length (elements)
   constexpr int A_ELEMS = BM * LDR;
   constexpr int B_ELEMS = BN * LDR;
@@ -102,14 +113,15 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
   constexpr int SMEM_MAIN = NST * STAGE * 2;
   constexpr int SMEM_EPI = BM * LDC * 2;
   constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
-  static_assert(SMEM >= 256 * 33 * 4, "LDS too small for the fused BN-reduce partials");
-  __shared__ __attribute__((aligned(16))) char smem[SMEM + (STATS ? 2 * 2 * BN * 4 : 0)];
+  static_assert(SMEM >= NT * 33 * 4, "LDS too small for the fused BN-reduce partials");
+  static_assert(SMEM + (STATS ? WM * 2 * BN * 4 : 0) <= 160 * 1024, "exceeds the 160 KiB LDS of a CU");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM + (STATS ? WM * 2 * BN * 4 : 0)];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WN, wn = wid % WN;
 
   // Strided dgrad is split into stride^2 output phases (blockIdx.y): in phase
   // (ph, pw) only taps r == (ph+pad) mod 2 (resp. s) contribute, so every
@@ -144,8 +156,8 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
   //      holding logical chunk (l%CH) ^ swz(row)
   const int chunk = DMA ? ((lane % CH) ^ swz<BK>(lane / CH)) : (tid & 7);
   const int rsub = tid >> 3;  // 0..31
-  auto a_row_of = [&](int i) { return DMA ? wid * (BM / 4) + RPI * i + lane / CH : rsub + 32 * i; };
-  auto b_row_of = [&](int i) { return DMA ? wid * (BN / 4) + RPI * i + lane / CH : rsub + 32 * i; };
+  auto a_row_of = [&](int i) { return DMA ? wid * (BM / NW) + RPI * i + lane / CH : rsub + 32 * i; };
+  auto b_row_of = [&](int i) { return DMA ? wid * (BN / NW) + RPI * i + lane / CH : rsub + 32 * i; };
   int a_base[PA], a_h[PA], a_w[PA];
   bool a_ok[PA];
   const int ohw = OHp * OWp;
@@ -233,7 +245,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
       const int ci = MF32 ? cb + lane_c32[i & 1] : c;
       const bf16_t* real = a.src + ((size_t)(unsigned)(u_p[i] + dpix) << a.log2Cs) + ci;
       const void* src = ok ? (const void*)real : (const void*)g_zero16;
-      bf16_t* dst = lds + dbuf * STAGE + (wid_s * (BM / 4) + RPI * i) * LDR;
+      bf16_t* dst = lds + dbuf * STAGE + (wid_s * (BM / NW) + RPI * i) * LDR;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
     }
@@ -241,7 +253,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     for (int i = 0; i < PB; ++i) {
       const int boff = tapo + (MF32 ? cb + lane_c32[i & 1] : c);
       const void* src = (b_ok[i] && kok) ? (const void*)(b_row[i] + boff) : (const void*)g_zero16;
-      bf16_t* dst = lds + dbuf * STAGE + A_ELEMS + (wid_s * (BN / 4) + RPI * i) * LDR;
+      bf16_t* dst = lds + dbuf * STAGE + A_ELEMS + (wid_s * (BN / NW) + RPI * i) * LDR;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
     }
@@ -273,7 +285,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
       if constexpr (DMA) {
         const void* src = g_zero16;
         if (ok) src = a.src + (((size_t)(a_base[i] + ih * a.W + iw)) << a.log2Cs) + c;
-        bf16_t* dst = lds + dbuf * STAGE + (wid * (BM / 4) + RPI * i) * LDR;
+        bf16_t* dst = lds + dbuf * STAGE + (wid * (BM / NW) + RPI * i) * LDR;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
       } else {
@@ -289,7 +301,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     for (int i = 0; i < PB; ++i) {
       if constexpr (DMA) {
         const void* src = (b_ok[i] && kok) ? (const void*)(b_row[i] + boff) : (const void*)g_zero16;
-        bf16_t* dst = lds + dbuf * STAGE + A_ELEMS + (wid * (BN / 4) + RPI * i) * LDR;
+        bf16_t* dst = lds + dbuf * STAGE + A_ELEMS + (wid * (BN / NW) + RPI * i) * LDR;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
       } else {
@@ -312,7 +324,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     }
   };
 
-  constexpr int MI2 = MF32 ? BM / 64 : 1, NI2 = MF32 ? BN / 64 : 1;  // 32x32 tiles per wave
+  constexpr int MI2 = MF32 ? BM / (32 * WM) : 1, NI2 = MF32 ? BN / (32 * WN) : 1;  // 32x32 tiles per wave
   f32x4 acc[MF32 ? 1 : MI][MF32 ? 1 : NI];
   f32x16 acc2[MI2][NI2];
   if constexpr (MF32) {
@@ -348,12 +360,12 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
         const int q = ks * 2 + (lane >> 5);
 #pragma unroll
         for (int i = 0; i < MI2; ++i) {
-          const int r = wm * (BM / 2) + i * 32 + r32;
+          const int r = wm * (BM / WM) + i * 32 + r32;
           af[i] = *reinterpret_cast<const bf16x8*>(As + r * LDR + ((q ^ ((r >> 1) & 7)) << 3));
         }
 #pragma unroll
         for (int j = 0; j < NI2; ++j) {
-          const int r = wn * (BN / 2) + j * 32 + r32;
+          const int r = wn * (BN / WN) + j * 32 + r32;
           bfg[j] = *reinterpret_cast<const bf16x8*>(Bs + r * LDR + ((q ^ ((r >> 1) & 7)) << 3));
         }
 #pragma unroll
@@ -369,9 +381,9 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
       bf16x8 af[MI], bfg[NI];
       const int q = ks * 4 + (lane >> 4);
 #pragma unroll
-      for (int i = 0; i < MI; ++i) af[i] = frag(As, wm * (BM / 2) + i * 16 + frow, q);
+      for (int i = 0; i < MI; ++i) af[i] = frag(As, wm * (BM / WM) + i * 16 + frow, q);
 #pragma unroll
-      for (int j = 0; j < NI; ++j) bfg[j] = frag(Bs, wn * (BN / 2) + j * 16 + frow, q);
+      for (int j = 0; j < NI; ++j) bfg[j] = frag(Bs, wn * (BN / WN) + j * 16 + frow, q);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -426,8 +438,8 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
 
   // ---- epilogue
   bf16_t* Cs = lds;
-  const int crow0 = wm * (BM / 2) + (lane >> 4) * 4;
-  const int ccol0 = wn * (BN / 2) + (lane & 15);
+  const int crow0 = wm * (BM / WM) + (lane >> 4) * 4;
+  const int ccol0 = wn * (BN / WN) + (lane & 15);
   float csum[NI], csq[NI];
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
@@ -443,8 +455,8 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const bf16_t h = f2bf(acc2[i][j][e]);
-          const int row = wm * (BM / 2) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-          Cs[row * LDC + wn * (BN / 2) + j * 32 + (lane & 31)] = h;
+          const int row = wm * (BM / WM) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+          Cs[row * LDC + wn * (BN / WN) + j * 32 + (lane & 31)] = h;
           if (STATS) {
             const float v = bf2f(h);
             csum[j] += v;
@@ -469,20 +481,20 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
   }
   if (STATS && MF32) {
     // column sums: lanes l and l+32 hold the two row halves of column l & 31
-    float* st = reinterpret_cast<float*>(smem + SMEM);  // [2 wm][2][BN]
+    float* st = reinterpret_cast<float*>(smem + SMEM);  // [WM][2][BN]
 #pragma unroll
     for (int j = 0; j < NI2; ++j) {
       float s1 = csum[j], s2 = csq[j];
       s1 += __shfl_xor(s1, 32, 64);
       s2 += __shfl_xor(s2, 32, 64);
       if (lane < 32) {
-        st[(wm * 2 + 0) * BN + wn * (BN / 2) + j * 32 + lane] = s1;
-        st[(wm * 2 + 1) * BN + wn * (BN / 2) + j * 32 + lane] = s2;
+        st[(wm * 2 + 0) * BN + wn * (BN / WN) + j * 32 + lane] = s1;
+        st[(wm * 2 + 1) * BN + wn * (BN / WN) + j * 32 + lane] = s2;
       }
     }
   }
   if (STATS && !MF32) {
-    float* st = reinterpret_cast<float*>(smem + SMEM);  // [2 wm][2][BN]
+    float* st = reinterpret_cast<float*>(smem + SMEM);  // [WM][2][BN]
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       float s1 = csum[j], s2 = csq[j];
@@ -499,16 +511,19 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
   __syncthreads();
   if (STATS) {
     const float* st = reinterpret_cast<const float*>(smem + SMEM);
-    for (int c = tid; c < 2 * BN; c += 256) {
+    for (int c = tid; c < 2 * BN; c += NT) {
       const int which = c / BN, col = c % BN;
       if (n0 + col < a.Nout) {
-        const float v = st[(0 * 2 + which) * BN + col] + st[(1 * 2 + which) * BN + col];
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) v += st[(w * 2 + which) * BN + col];
         atomicAdd(a.stats + ((size_t)((m0 / BM) % kStatSlots) * 2 + which) * a.Nout + n0 + col, v);
       }
     }
   }
   constexpr int CPR = BN / 8;  // 16-B chunks per output row
-  // fused BN-backward reduce: each thread owns one 8-channel chunk column (256 % CPR == 0)
+  // fused BN-backward reduce: each thread owns one 8-channel chunk column (NT % CPR == 0)
+  static_assert(NT % CPR == 0, "chunk column per thread");
   const int nbn = (DGRAD && a.bn_red[0]) ? (a.bn_red[1] ? 2 : 1) : 0;
   float bsum[2][8], bdot[2][8], bmean[2][8], binv[2][8];
   {
@@ -531,7 +546,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
           }
     }
   }
-  for (int idx = tid; idx < BM * CPR; idx += 256) {
+  for (int idx = tid; idx < BM * CPR; idx += NT) {
     const int row = idx / CPR, cc = idx % CPR;
     const int m = m0 + row, n = n0 + cc * 8;
     if (m < Mp && n < a.Nout) {
@@ -581,7 +596,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
     // block-level combine of the 256/CPR threads sharing a chunk column, then one
     // fp32 atomic per channel per block into a kStatSlots slot (like conv_fwd stats)
     __syncthreads();  // everyone is done reading Cs
-    float* part = reinterpret_cast<float*>(smem);  // [256][33]
+    float* part = reinterpret_cast<float*>(smem);  // [NT][33]
     for (int t = 0; t < nbn; ++t) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -589,10 +604,10 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvArgs a) {
         part[tid * 33 + 8 + e] = bdot[t][e];
       }
       __syncthreads();
-      for (int q = tid; q < CPR * 16; q += 256) {
+      for (int q = tid; q < CPR * 16; q += NT) {
         const int col = q >> 4, k = q & 15;
         float acc2 = 0.f;
-        for (int r = col; r < 256; r += CPR) acc2 += part[r * 33 + k];
+        for (int r = col; r < NT; r += CPR) acc2 += part[r * 33 + k];
         const int n = n0 + col * 8 + (k & 7);
         if (n < a.Nout)
           atomicAdd(a.bn_red[t] + ((size_t)((m0 / BM) % kStatSlots) * 2 + (k >> 3)) * a.Nout + n, acc2);
@@ -679,19 +694,19 @@ static int conv_impl() {
   return g_conv_impl;
 }
 
-template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA, bool MF32 = false>
+template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA, bool MF32 = false,
+          int WM = 2, int WN = 2>
 static void launch_k(const ConvArgs& a, hipStream_t st) {
   const bool ph2 = DGRAD && a.stride == 2;
   const int Mgrid = ph2 ? a.N * ((a.OH + 1) >> 1) * ((a.OW + 1) >> 1) : a.M;
   const int tiles = ((Mgrid + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
   const int phases = ph2 ? 4 : 1;
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, NST, DGRAD, STATS, DMA, MF32>), dim3(tiles, phases),
-                     dim3(256), 0, st, a);
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, NST, DGRAD, STATS, DMA, MF32, WM, WN>),
+                     dim3(tiles, phases), dim3(64 * WM * WN), 0, st, a);
 }
 
 template <int BM, int BN, bool DGRAD, bool STATS>
-static void launch_t(const ConvArgs& a, hipStream_t st) {
-  int impl = conv_impl();
+static void launch_t(const ConvArgs& a, hipStream_t st, int impl) {
   if (impl == 5) impl = a.Kg <= 512 ? 4 : 1;
   switch (impl) {
     case 0: launch_k<BM, BN, 64, 2, DGRAD, STATS, false>(a, st); break;
@@ -706,12 +721,188 @@ static void launch_t(const ConvArgs& a, hipStream_t st) {
   }
 }
 
+// 8-wave 256-row tiles (LDS-DMA only; one block per CU).  Pipeline by
+// PMD_CONV_BIGPIPE: 0 (default) BK=64 x2 stages, 1 BK=64 x3, 2 BK=32 x4.
+static int g_big_pipe = -1;
+void conv_set_big_pipe(int p) { g_big_pipe = p; }
+static int big_pipe() {
+  if (g_big_pipe < 0) {
+    const char* e = getenv("PMD_CONV_BIGPIPE");
+    g_big_pipe = (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 0;
+  }
+  return g_big_pipe;
+}
+
+template <int BM, int BN, int WM, int WN, bool DGRAD, bool STATS>
+static void launch_big(const ConvArgs& a, hipStream_t st) {
+  switch (big_pipe()) {
+    case 1:  // 3 x (256+BN) x 64 x 2 B: fits the CU's LDS only at BN = 128
+      if constexpr (BN <= 128) launch_k<BM, BN, 64, 3, DGRAD, STATS, true, false, WM, WN>(a, st);
+      else launch_k<BM, BN, 64, 2, DGRAD, STATS, true, false, WM, WN>(a, st);
+      break;
+    case 2: launch_k<BM, BN, 32, 4, DGRAD, STATS, true, false, WM, WN>(a, st); break;
+    default: launch_k<BM, BN, 64, 2, DGRAD, STATS, true, false, WM, WN>(a, st); break;
+  }
+}
+
+// Tile policy (conv_set_tile or PMD_CONV_TILE): 0 auto (autotuned per shape, else
+// 128-row tiles), 1 128-row tiles only, 2 256x128 wherever legal, 3 256x256
+// wherever legal (Nout >= 256).
+static int g_conv_tile = -1;
+void conv_set_tile(int t) { g_conv_tile = t; }
+static int conv_tile() {
+  if (g_conv_tile < 0) {
+    const char* e = getenv("PMD_CONV_TILE");
+    g_conv_tile = (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 0;
+  }
+  return g_conv_tile;
+}
+
+static bool big_ok(const ConvArgs& a) {
+  // 256-row tiles need the uniform-tap DMA loader (Cs >= 64) and >= 128 output channels
+  return a.Cs >= 64 && a.Nout >= 128;
+}
+
+// One candidate kernel configuration of the autotuner:
+//   0  128-row tile, LDS-DMA BK=32 x3 stages      1  128-row tile, LDS-DMA BK=64 x2
+//   2  256x256 tile (8 waves), BK=64 x2            3  256x128 tile (8 waves), BK=64 x2
+template <bool DGRAD, bool STATS>
+static void launch_choice(int c, const ConvArgs& a, hipStream_t st) {
+  if (c == 2 && big_ok(a) && a.Nout >= 256) {
+    launch_k<256, 256, 64, 2, DGRAD, STATS, true, false, 2, 4>(a, st);
+  } else if (c == 3 && big_ok(a)) {
+    launch_k<256, 128, 64, 2, DGRAD, STATS, true, false, 4, 2>(a, st);
+  } else {
+    const int impl = c == 0 ? 4 : 1;
+    if (a.Nout <= 64) launch_t<128, 64, DGRAD, STATS>(a, st, impl);
+    else launch_t<128, 128, DGRAD, STATS>(a, st, impl);
+  }
+}
+
+// ---- per-shape autotuner: the framework's cudnn.benchmark (reference main.py:45).
+// The first launch of every (shape, pass) outside HIP-graph capture times each
+// legal candidate on the live operands (best of 3 after one warm launch, HIP
+// events on the caller's stream) and caches the winner; later launches go
+// straight to it.  Candidates write the real output (every candidate overwrites
+// all of it, and the chosen kernel runs last), but BN statistics go to a
+// scratch slot buffer and the fused BN-backward reduce is left out of the
+// timing runs, so nothing accumulates twice.  PMD_CONV_AUTOTUNE=0 disables it
+// (then: 128-row tiles, BK by reduction depth); PMD_CONV_AUTOTUNE_LOG=1 prints
+// every decision.
+struct TuneKey {
+  int v[13];
+  bool operator<(const TuneKey& o) const {
+    for (int i = 0; i < 13; ++i)
+      if (v[i] != o.v[i]) return v[i] < o.v[i];
+    return false;
+  }
+};
+static std::map<TuneKey, int> g_tune;
+static std::mutex g_tune_mu;
+static int g_autotune = -1;
+void conv_set_autotune(int on) { g_autotune = on; }
+static bool autotune_on() {
+  if (g_autotune < 0) {
+    const char* e = getenv("PMD_CONV_AUTOTUNE");
+    g_autotune = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_autotune == 1;
+}
+int conv_autotune_entries() {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  return (int)g_tune.size();
+}
+void conv_autotune_clear() {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  g_tune.clear();
+}
+
+template <bool DGRAD, bool STATS>
+static int tune(const ConvArgs& a0, hipStream_t st) {
+  ConvArgs a = a0;
+  a.bn_red[0] = a.bn_red[1] = nullptr;  // no fused reduce in the timing runs
+  static float* scratch_stats = nullptr;
+  static int scratch_n = 0;
+  if (STATS) {
+    const int need = kStatSlots * 2 * a.Nout;
+    if (need > scratch_n) {
+      if (scratch_stats) (void)hipFree(scratch_stats);
+      if (hipMalloc(&scratch_stats, sizeof(float) * need) != hipSuccess) return -1;
+      scratch_n = need;
+    }
+    a.stats = scratch_stats;
+  }
+  static hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (!e0) {
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+  }
+  int best = -1;
+  float best_ms = 1e30f;
+  const int ncand = 4;
+  for (int c = 0; c < ncand; ++c) {
+    if ((c == 2 && !(big_ok(a) && a.Nout >= 256)) || (c == 3 && !big_ok(a))) continue;
+    launch_choice<DGRAD, STATS>(c, a, st);  // warm (code object load, caches)
+    float t = 1e30f;
+    for (int r = 0; r < 3; ++r) {
+      (void)hipEventRecord(e0, st);
+      launch_choice<DGRAD, STATS>(c, a, st);
+      (void)hipEventRecord(e1, st);
+      if (hipEventSynchronize(e1) != hipSuccess) return -1;
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      t = ms < t ? ms : t;
+    }
+    if (t < best_ms) {
+      best_ms = t;
+      best = c;
+    }
+  }
+  const char* lg = getenv("PMD_CONV_AUTOTUNE_LOG");
+  if (lg && lg[0] == '1')
+    fprintf(stderr, "[pmd autotune] %s N=%d H=%d W=%d C=%d -> %dx%d K=%d R=%d s=%d: choice %d (%.1f us)\n",
+            DGRAD ? "dgrad" : "fwd", a.N, a.H, a.W, a.Cs, a.OH, a.OW, a.Nout, a.R, a.stride, best,
+            best_ms * 1e3f);
+  return best;
+}
+
 template <bool DGRAD, bool STATS>
 static void launch_sel(const ConvArgs& a, hipStream_t st) {
-  if (a.Nout <= 64)
-    launch_t<128, 64, DGRAD, STATS>(a, st);
-  else
-    launch_t<128, 128, DGRAD, STATS>(a, st);
+  if (conv_impl() == 5 && conv_tile() == 0 && autotune_on()) {
+    const TuneKey k{{a.N, a.H, a.W, a.Cs, a.OH, a.OW, a.Nout, a.R, a.S, a.stride, a.pad, (int)DGRAD,
+                     (int)STATS}};
+    int c = -1;
+    {
+      std::lock_guard<std::mutex> lk(g_tune_mu);
+      auto it = g_tune.find(k);
+      if (it != g_tune.end()) c = it->second;
+    }
+    if (c < 0) {
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      (void)hipStreamIsCapturing(st, &cs);
+      if (cs == hipStreamCaptureStatusNone) {
+        c = tune<DGRAD, STATS>(a, st);
+        if (c >= 0) {
+          std::lock_guard<std::mutex> lk(g_tune_mu);
+          g_tune[k] = c;
+        }
+      }
+    }
+    if (c >= 0) {
+      launch_choice<DGRAD, STATS>(c, a, st);
+      return;
+    }
+  }
+  const int t = conv_tile();
+  if (big_ok(a) && t == 3 && a.Nout >= 256) {
+    launch_big<256, 256, 2, 4, DGRAD, STATS>(a, st);
+  } else if (big_ok(a) && t == 2) {
+    launch_big<256, 128, 4, 2, DGRAD, STATS>(a, st);
+  } else if (a.Nout <= 64) {
+    launch_t<128, 64, DGRAD, STATS>(a, st, conv_impl());
+  } else {
+    launch_t<128, 128, DGRAD, STATS>(a, st, conv_impl());
+  }
 }
 
 // Returns 0 on success, nonzero on unsupported shape.

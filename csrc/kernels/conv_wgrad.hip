@@ -21,7 +21,11 @@
 // single-carry increments, so the gather costs no integer divisions in the
 // main loop.
 #include "common.h"
+#include <stdio.h>
 #include <stdlib.h>
+
+#include <map>
+#include <mutex>
 
 namespace pmd {
 
@@ -470,6 +474,95 @@ static int wgrad_impl() {
   return g_wgrad_impl;
 }
 
+static void wgrad_dispatch(int impl, const WgradArgs& a, dim3 grid, hipStream_t st) {
+  const bool k64 = a.K == 64;
+  switch (impl) {
+    case 0:
+      if (k64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), grid, dim3(256), 0, st, a);
+      break;
+    case 2:  // DMA, 32-row stages, 4-deep ring
+      if (k64) hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 128, 32, 4>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 32, 4>), grid, dim3(256), 0, st, a);
+      break;
+    case 3:  // DMA, 64-row stages, 3-deep ring (1 block/CU at BM=128)
+      if (k64) hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 128, 64, 3>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 64, 3>), grid, dim3(256), 0, st, a);
+      break;
+    default:  // 1: DMA, 64-row stages, 2-deep ring
+      if (k64) hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 128, 64, 2>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 64, 2>), grid, dim3(256), 0, st, a);
+      break;
+  }
+}
+
+// Per-shape autotuning of the staging variant (register staging vs LDS-DMA),
+// like the conv fwd/dgrad tuner: timed on the live operands outside graph
+// capture, the partial tile written to a scratch dW so nothing is accumulated
+// twice into the caller's gradient.  PMD_WGRAD_AUTOTUNE=0 disables it.
+struct WgradKey {
+  int v[11];
+  bool operator<(const WgradKey& o) const {
+    for (int i = 0; i < 11; ++i)
+      if (v[i] != o.v[i]) return v[i] < o.v[i];
+    return false;
+  }
+};
+static std::map<WgradKey, int> g_wtune;
+static std::mutex g_wtune_mu;
+static bool wgrad_autotune_on() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("PMD_WGRAD_AUTOTUNE");
+    on = (e && e[0] == '0') ? 0 : 1;
+  }
+  return on == 1;
+}
+
+static int wgrad_tune(const WgradArgs& a0, dim3 grid, int splits, hipStream_t st) {
+  WgradArgs a = a0;
+  static float* scratch = nullptr;
+  static size_t scratch_n = 0;
+  const size_t need = (size_t)a.K * a.Kg;
+  if (need > scratch_n) {
+    if (scratch) (void)hipFree(scratch);
+    if (hipMalloc(&scratch, sizeof(float) * need) != hipSuccess) return -1;
+    scratch_n = need;
+  }
+  a.dw = scratch;  // splits == 1 accumulates into dw; otherwise dw is untouched here
+  (void)splits;
+  static hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (!e0) {
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+  }
+  const int cands[2] = {0, 1};
+  int best = -1;
+  float best_ms = 1e30f;
+  for (int c : cands) {
+    wgrad_dispatch(c, a, grid, st);
+    float t = 1e30f;
+    for (int r = 0; r < 3; ++r) {
+      (void)hipEventRecord(e0, st);
+      wgrad_dispatch(c, a, grid, st);
+      (void)hipEventRecord(e1, st);
+      if (hipEventSynchronize(e1) != hipSuccess) return -1;
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      t = ms < t ? ms : t;
+    }
+    if (t < best_ms) {
+      best_ms = t;
+      best = c;
+    }
+  }
+  const char* lg = getenv("PMD_CONV_AUTOTUNE_LOG");
+  if (lg && lg[0] == '1')
+    fprintf(stderr, "[pmd autotune] wgrad N=%d H=%d W=%d C=%d K=%d R=%d s=%d: impl %d (%.1f us)\n", a.N,
+            a.H, a.W, a.C, a.K, a.R, a.stride, best, best_ms * 1e3f);
+  return best;
+}
+
 template <int BM>
 static void plan(const WgradArgs& a, int* splits_out, int* cps_out) {
   constexpr int BN = 128;
@@ -538,24 +631,29 @@ int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, float* ws, i
   const int BM = K == 64 ? 64 : 128;
   const int tiles = ((a.K + BM - 1) / BM) * ((a.Kg + 127) / 128);
   const dim3 grid(tiles * splits);
-  switch (wgrad_impl()) {
-    case 0:
-      if (K == 64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128>), grid, dim3(256), 0, st, a);
-      else hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), grid, dim3(256), 0, st, a);
-      break;
-    case 2:  // DMA, 32-row stages, 4-deep ring
-      if (K == 64) hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 128, 32, 4>), grid, dim3(256), 0, st, a);
-      else hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 32, 4>), grid, dim3(256), 0, st, a);
-      break;
-    case 3:  // DMA, 64-row stages, 3-deep ring (1 block/CU at BM=128)
-      if (K == 64) hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 128, 64, 3>), grid, dim3(256), 0, st, a);
-      else hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 64, 3>), grid, dim3(256), 0, st, a);
-      break;
-    default:  // 1: DMA, 64-row stages, 2-deep ring
-      if (K == 64) hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 128, 64, 2>), grid, dim3(256), 0, st, a);
-      else hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 64, 2>), grid, dim3(256), 0, st, a);
-      break;
+  int impl = wgrad_impl();
+  if (impl == 1 && wgrad_autotune_on()) {
+    const WgradKey key{{N, H, W, C, P, Q, K, R, S, stride, pad}};
+    int c = -1;
+    {
+      std::lock_guard<std::mutex> lk(g_wtune_mu);
+      auto it = g_wtune.find(key);
+      if (it != g_wtune.end()) c = it->second;
+    }
+    if (c < 0) {
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      (void)hipStreamIsCapturing(st, &cs);
+      if (cs == hipStreamCaptureStatusNone) {
+        c = wgrad_tune(a, grid, splits, st);
+        if (c >= 0) {
+          std::lock_guard<std::mutex> lk(g_wtune_mu);
+          g_wtune[key] = c;
+        }
+      }
+    }
+    if (c >= 0) impl = c;
   }
+  wgrad_dispatch(impl, a, grid, st);
   if (splits > 1) {
     const long long n4 = (long long)a.K * a.Kg / 4;
     const int groups = (splits + kSplitGroup - 1) / kSplitGroup;

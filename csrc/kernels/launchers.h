@@ -20,6 +20,11 @@ int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* s
                       const BnReduceArgs* bnr, hipStream_t st);
 void conv_set_impl(int impl);
 void conv_wgrad_set_impl(int impl);
+void conv_set_tile(int t);
+void conv_set_big_pipe(int p);
+void conv_set_autotune(int on);
+int conv_autotune_entries();
+void conv_autotune_clear();
 // grouped weight-image prep (one launch for every conv of a model)
 struct WeightPrepDesc {
   const float* w;  // fp32 [K][R][S][C] (channels_last parameter storage)

@@ -137,6 +137,74 @@ def test_conv_pipeline_variants(shape, impl):
     _close(dx, dxr, 2e-2)
 
 
+@pytest.mark.parametrize("tile,pipe", [(2, 0), (2, 1), (2, 2), (3, 0), (3, 2)])
+@pytest.mark.parametrize("shape", R50_SHAPES + CIFAR_SHAPES, ids=lambda s: "C%d_H%d_K%d_R%d_s%d" % s)
+def test_conv_big_tiles(shape, tile, pipe):
+    """8-wave 256x128 / 256x256 tiles (forced wherever legal: Cs >= 64, Nout >= 128)
+    with each LDS-DMA pipeline, fwd (+BN stats epilogue) and dgrad."""
+    from pytorch_multiprocessing_distributed_amd.ops.native import C as _C
+    HP = _hp()
+    torch.manual_seed(4)
+    C, H, K, R, st = shape
+    pad = R // 2
+    N = _batch_for(H)
+    x = torch.randn(N, H, H, C, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(K, C, R, R, device=DEV) / (C * R * R) ** 0.5).contiguous(
+        memory_format=torch.channels_last)
+    wp = HP.conv_weight(w, torch.bfloat16, C, True)
+    wref = TP.conv_weight(w, torch.bfloat16, C)
+    yr, sr = TP.conv_fwd(x, wref, st, pad, True)
+    dy = torch.randn_like(yr)
+    dxr = TP.conv_dgrad(dy, wref, tuple(x.shape), st, pad)
+    _C.conv_set_tile(tile)
+    _C.conv_set_big_pipe(pipe)
+    try:
+        y, st_ = HP.conv_fwd(x, wp, st, pad, True)
+        dx = HP.conv_dgrad(dy, wp, tuple(x.shape), st, pad)
+        torch.cuda.synchronize()
+    finally:
+        _C.conv_set_tile(0)
+        _C.conv_set_big_pipe(0)
+    _close(y, yr, 2e-2)
+    _close(HP.stats_collapse(st_).view(2, -1), sr, 2e-2)
+    _close(dx, dxr, 2e-2)
+
+
+def test_conv_autotuner_caches_and_matches():
+    """The per-shape autotuner (cudnn.benchmark equivalent) picks a kernel on the
+    first call, caches it, and the tuned launch equals the untuned one up to
+    bf16 rounding; BN statistics are not double-counted by the timing runs."""
+    from pytorch_multiprocessing_distributed_amd.ops.native import C as _C
+    HP = _hp()
+    torch.manual_seed(5)
+    C, H, K, R, st = 256, 14, 256, 3, 1
+    x = torch.randn(8, H, H, C, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(K, C, R, R, device=DEV) / (C * R * R) ** 0.5).contiguous(
+        memory_format=torch.channels_last)
+    wp = HP.conv_weight(w, torch.bfloat16, C, True)
+    _C.conv_set_autotune(0)
+    try:
+        y0, s0 = HP.conv_fwd(x, wp, st, 1, True)
+        dy = torch.randn_like(y0)
+        dx0 = HP.conv_dgrad(dy, wp, tuple(x.shape), st, 1)
+        dw0 = HP.conv_wgrad(dy, x, tuple(wp[0].shape), st, 1)
+        ref = HP.stats_collapse(s0).view(2, -1)
+    finally:
+        _C.conv_set_autotune(1)
+    _C.conv_autotune_clear()
+    y1, s1 = HP.conv_fwd(x, wp, st, 1, True)          # tunes
+    assert _C.conv_autotune_entries() >= 1
+    dx1 = HP.conv_dgrad(dy, wp, tuple(x.shape), st, 1)
+    dw1 = HP.conv_wgrad(dy, x, tuple(wp[0].shape), st, 1)
+    y2, s2 = HP.conv_fwd(x, wp, st, 1, True)          # cached
+    _close(y1, y0, 1e-2)
+    _close(HP.stats_collapse(s1).view(2, -1), ref, 1e-2)
+    _close(HP.stats_collapse(s2).view(2, -1), ref, 1e-2)
+    assert torch.equal(y1, y2)
+    _close(dx1, dx0, 1e-2)
+    _close(dw1, dw0, 1e-3)
+
+
 @pytest.mark.parametrize("mode", ["plain", "res", "two", "norelu"])
 @pytest.mark.parametrize("C", [64, 256, 2048])
 def test_bn_family(mode, C):
@@ -346,9 +414,20 @@ def test_resnet50_trains_on_gpu():
                                    (256, 28, 256, 3, 2), (512, 7, 2048, 1, 1)],
                          ids=lambda s: "C%d_H%d_K%d_R%d_s%d" % s)
 @pytest.mark.parametrize("two", [False, True])
-def test_dgrad_fused_bn_reduce(shape, two):
+@pytest.mark.parametrize("tile", [1, 2, 3])
+def test_dgrad_fused_bn_reduce(shape, two, tile):
     """BN-backward reduce fused into the dgrad epilogue (one or two BN sets
-    sharing the ReLU mask, with a residual addend) == dgrad then bn_bwd_reduce."""
+    sharing the ReLU mask, with a residual addend) == dgrad then bn_bwd_reduce,
+    on the 4-wave 128-row tiles and the 8-wave 256-row tiles."""
+    from pytorch_multiprocessing_distributed_amd.ops.native import C as _C
+    _C.conv_set_tile(tile)
+    try:
+        _dgrad_fused_bn_reduce(shape, two)
+    finally:
+        _C.conv_set_tile(0)
+
+
+def _dgrad_fused_bn_reduce(shape, two):
     HP = _hp()
     torch.manual_seed(3)
     C, H, K, R, st = shape
