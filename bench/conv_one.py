@@ -1,0 +1,49 @@
+"""Run ONE conv layer configuration repeatedly (for rocprofv3 --pmc passes).
+
+    python bench/conv_one.py C H K R stride [--tile T] [--pipe P] [--impl I] [--pass fwd|dgrad]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pytorch_multiprocessing_distributed_amd.ops import hip_prims as HP  # noqa: E402
+from pytorch_multiprocessing_distributed_amd.ops.native import C as _C  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    for k in ("C", "H", "K", "R", "stride"):
+        ap.add_argument(k, type=int)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--tile", type=int, default=1)
+    ap.add_argument("--pipe", type=int, default=0)
+    ap.add_argument("--impl", type=int, default=5)
+    ap.add_argument("--pass", dest="which", default="fwd")
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    _C.conv_set_autotune(0)
+    _C.conv_set_tile(a.tile)
+    _C.conv_set_big_pipe(a.pipe)
+    _C.conv_set_impl(a.impl)
+    pad = a.R // 2
+    x = torch.randn(a.batch, a.H, a.H, a.C, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(a.K, a.C, a.R, a.R, device="cuda") / (a.C * a.R * a.R) ** 0.5).contiguous(
+        memory_format=torch.channels_last)
+    wp = HP.conv_weight(w, torch.bfloat16, a.C, True)
+    y, s = HP.conv_fwd(x, wp, a.stride, pad, True)
+    dy = torch.randn_like(y)
+    for _ in range(a.iters):
+        if a.which == "fwd":
+            y, s = HP.conv_fwd(x, wp, a.stride, pad, True)
+            HP._release(s)
+        else:
+            HP.conv_dgrad(dy, wp, tuple(x.shape), a.stride, pad)
+    torch.cuda.synchronize()
+    print("done")
+
+
+if __name__ == "__main__":
+    main()

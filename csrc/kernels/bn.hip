@@ -264,29 +264,50 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(
 // ready for the next conv epilogue / reduce -- no memset launch).
 // acc_a/acc_b: optional [2][C] fp32 gradient targets (d_beta | d_gamma rows)
 // that receive += the collapsed local sums (direct-to-arena BN param grads).
-__global__ void stats_collapse_kernel(float* __restrict__ a, int Ca, float* __restrict__ b, int Cb,
-                                      float count, float* __restrict__ out, int with_count, int clear,
-                                      float* __restrict__ acc_a0, float* __restrict__ acc_a1,
-                                      float* __restrict__ acc_b0, float* __restrict__ acc_b1) {
+// The slot buffers were filled by memory-side fp32 atomics, so nothing of them
+// is in L2: every read is a full HBM/MALL round trip.  A thread therefore sums
+// only kStatSlots/4 slots of one output with all its loads in flight at once,
+// and the 4 slot groups of an output are combined through LDS -- one memory
+// latency per kernel instead of kStatSlots/8 dependent batches.
+constexpr int kSlotGroups = 4;
+constexpr int kSlotsPerGroup = kStatSlots / kSlotGroups;
+
+__global__ __launch_bounds__(256) void stats_collapse_kernel(
+    float* __restrict__ a, int Ca, float* __restrict__ b, int Cb, float count, float* __restrict__ out,
+    int with_count, int clear, float* __restrict__ acc_a0, float* __restrict__ acc_a1,
+    float* __restrict__ acc_b0, float* __restrict__ acc_b1) {
+  __shared__ float part[kSlotGroups][64];
   const int na = 2 * Ca, nb = b ? 2 * Cb : 0;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int li = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + li;
+  float s = 0.f;
   if (i < na + nb) {
     float* src = i < na ? a + i : b + (i - na);
     const int n = i < na ? na : nb;
-    float s = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < kStatSlots; ++k) s += src[(size_t)k * n];
+    float v[kSlotsPerGroup];
+#pragma unroll
+    for (int k = 0; k < kSlotsPerGroup; ++k) v[k] = src[(size_t)(g * kSlotsPerGroup + k) * n];
+#pragma unroll
+    for (int k = 0; k < kSlotsPerGroup; ++k) s += v[k];
     if (clear) {
-#pragma unroll 8
-      for (int k = 0; k < kStatSlots; ++k) src[(size_t)k * n] = 0.f;
+#pragma unroll
+      for (int k = 0; k < kSlotsPerGroup; ++k) src[(size_t)(g * kSlotsPerGroup + k) * n] = 0.f;
     }
-    out[i] = s;
-    const int j = i < na ? i : i - na;
-    const int C = i < na ? Ca : Cb;
-    float* acc = i < na ? (j < C ? acc_a0 : acc_a1) : (j < C ? acc_b0 : acc_b1);
-    if (acc) acc[j < C ? j : j - C] += s;
-  } else if (with_count && i == na + nb) {
-    out[i] = count;
+  }
+  part[g][li] = s;
+  __syncthreads();
+  if (g == 0) {
+    if (i < na + nb) {
+      // fixed order: bitwise identical to a sequential sum over the groups
+      s = ((part[0][li] + part[1][li]) + part[2][li]) + part[3][li];
+      out[i] = s;
+      const int j = i < na ? i : i - na;
+      const int C = i < na ? Ca : Cb;
+      float* acc = i < na ? (j < C ? acc_a0 : acc_a1) : (j < C ? acc_b0 : acc_b1);
+      if (acc) acc[j < C ? j : j - C] += s;
+    } else if (with_count && i == na + nb) {
+      out[i] = count;
+    }
   }
 }
 
@@ -294,29 +315,44 @@ int stats_collapse_launch(float* a, int Ca, float* b, int Cb, float count, float
                           bool with_count, bool clear, float* acc_a0, float* acc_a1, float* acc_b0,
                           float* acc_b1, hipStream_t st) {
   const int n = 2 * Ca + (b ? 2 * Cb : 0) + (with_count ? 1 : 0);
-  hipLaunchKernelGGL(stats_collapse_kernel, dim3((n + 255) / 256), dim3(256), 0, st, a, Ca, b, Cb,
+  hipLaunchKernelGGL(stats_collapse_kernel, dim3((n + 63) / 64), dim3(256), 0, st, a, Ca, b, Cb,
                      count, out, with_count ? 1 : 0, clear ? 1 : 0, acc_a0, acc_a1, acc_b0, acc_b1);
   return 0;
 }
 
 // Single-replica BN statistics: collapse (and clear) the slots and finalize
 // in one launch -- used when there is no SyncBN all-reduce between the two.
-__global__ void stats_finalize_local_kernel(float* __restrict__ slots, float count,
-                                            const float* __restrict__ gamma,
-                                            const float* __restrict__ beta, float* __restrict__ params,
-                                            float* running_mean, float* running_var, long long* nbt,
-                                            int C, float eps, float momentum) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void stats_finalize_local_kernel(
+    float* __restrict__ slots, float count, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ params, float* running_mean,
+    float* running_var, long long* nbt, int C, float eps, float momentum) {
+  __shared__ float part[2][kSlotGroups][64];
+  const int li = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + li;
+  float s1 = 0.f, s2 = 0.f;
   if (c < C) {
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < kStatSlots; ++k) {
-      float* p = slots + (size_t)k * 2 * C;
-      s1 += p[c];
-      s2 += p[C + c];
+    float v1[kSlotsPerGroup], v2[kSlotsPerGroup];
+#pragma unroll
+    for (int k = 0; k < kSlotsPerGroup; ++k) {
+      const float* p = slots + (size_t)(g * kSlotsPerGroup + k) * 2 * C;
+      v1[k] = p[c];
+      v2[k] = p[C + c];
+    }
+#pragma unroll
+    for (int k = 0; k < kSlotsPerGroup; ++k) {
+      s1 += v1[k];
+      s2 += v2[k];
+      float* p = slots + (size_t)(g * kSlotsPerGroup + k) * 2 * C;
       p[c] = 0.f;
       p[C + c] = 0.f;
     }
+  }
+  part[0][g][li] = s1;
+  part[1][g][li] = s2;
+  __syncthreads();
+  if (g == 0 && c < C) {
+    s1 = ((part[0][0][li] + part[0][1][li]) + part[0][2][li]) + part[0][3][li];
+    s2 = ((part[1][0][li] + part[1][1][li]) + part[1][2][li]) + part[1][3][li];
     const float mean = s1 / count;
     const float var = fmaxf(s2 / count - mean * mean, 0.f);
     const float invstd = rsqrtf(var + eps);
@@ -337,7 +373,7 @@ __global__ void stats_finalize_local_kernel(float* __restrict__ slots, float cou
 int stats_finalize_local_launch(float* slots, float count, const float* gamma, const float* beta,
                                 float* params, float* rm, float* rv, long long* nbt, int C, float eps,
                                 float momentum, hipStream_t st) {
-  hipLaunchKernelGGL(stats_finalize_local_kernel, dim3((C + 255) / 256), dim3(256), 0, st, slots, count,
+  hipLaunchKernelGGL(stats_finalize_local_kernel, dim3((C + 63) / 64), dim3(256), 0, st, slots, count,
                      gamma, beta, params, rm, rv, nbt, C, eps, momentum);
   return 0;
 }

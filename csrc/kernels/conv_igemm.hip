@@ -650,14 +650,23 @@ __global__ void conv_weight_prep_grouped_kernel(const WeightPrepDesc* __restrict
   const int lb = blockIdx.x - block_start[e_sh];
   const int nb = block_start[e_sh + 1] - block_start[e_sh];
   const int total = d.K * d.RS * d.Cp;
-  for (int i = lb * blockDim.x + threadIdx.x; i < total; i += nb * blockDim.x) {
-    const int c = i % d.Cp;
-    const int rs = (i / d.Cp) % d.RS;
-    const int k = i / (d.Cp * d.RS);
-    const float v = c < d.C ? d.w[((size_t)k * d.RS + rs) * d.C + c] : 0.f;
-    const bf16_t h = f2bf(v);
-    d.wk[i] = h;
-    if (d.wkt) d.wkt[((size_t)c * d.RS + rs) * d.K + k] = h;
+  // pass 1: wk [K][RS][Cp] in its own order (coalesced reads and writes);
+  // pass 2: wkt [Cp][RS][K] in ITS order -- coalesced writes, strided reads of the
+  // (L2-resident, <= 9 MB) fp32 weight instead of a scattered 2-byte write stream
+  const int work = d.wkt ? 2 * total : total;
+  for (int i = lb * blockDim.x + threadIdx.x; i < work; i += nb * blockDim.x) {
+    if (i < total) {
+      const int c = i % d.Cp;
+      const int rs = (i / d.Cp) % d.RS;
+      const int k = i / (d.Cp * d.RS);
+      d.wk[i] = f2bf(c < d.C ? d.w[((size_t)k * d.RS + rs) * d.C + c] : 0.f);
+    } else {
+      const int j = i - total;
+      const int k = j % d.K;
+      const int rs = (j / d.K) % d.RS;
+      const int c = j / (d.K * d.RS);
+      d.wkt[j] = f2bf(c < d.C ? d.w[((size_t)k * d.RS + rs) * d.C + c] : 0.f);
+    }
   }
 }
 

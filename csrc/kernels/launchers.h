@@ -99,8 +99,9 @@ int conv_fp8_fwd_launch(const uint8_t* x, const uint8_t* w, bf16_t* out, float* 
 // flags [kXgmiMaxRanks][kXgmiMaxBlocks] uint32 (kXgmiFlagBytes), then data
 // [2 parities][world][kXgmiCap] fp32.
 constexpr int kXgmiMaxRanks = 16;
-constexpr int kXgmiChunk = 2048;       // floats per block
-constexpr int kXgmiMaxBlocks = 16;
+constexpr int kXgmiChunk = 512;        // floats per block of the fused SyncBN kernel (small:
+constexpr int kXgmiMaxBlocks = 64;     // its slot collapse is latency-bound, so spread it out)
+constexpr int kXgmiArChunk = 2048;     // floats per block of the plain all-reduce
 constexpr int kXgmiCap = kXgmiChunk * kXgmiMaxBlocks;  // max floats per call
 constexpr int kXgmiFlagBytes = 4096;
 int xgmi_allreduce_launch(float* const* data, uint32_t* const* flags, float* x, int n, int rank,
@@ -131,7 +132,10 @@ struct XgmiBnArgs {
   float* accB1;
   float* outA;              // backward: global [2][CA]
   float* outB;
+  int pairs;  // channel pairs per block (set by the launcher)
 };
+// fused SyncBN kernel: channel pairs per block (1..kBnPairs); default kBnPairs
+void xgmi_set_bn_pairs(int pairs);
 int xgmi_bn_launch(float* const* data, uint32_t* const* flags, const XgmiBnArgs& args, int rank, int world,
                    uint32_t* epochs, uint32_t* err, long long spin_limit, hipStream_t st);
 }  // namespace pmd

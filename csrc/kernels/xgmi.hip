@@ -40,8 +40,8 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(XgmiPeers peers, fl
   __syncthreads();
   const uint32_t e = e_sh;
   const int p = e & 1;
-  const int lo = b * kXgmiChunk;
-  const int len = min(kXgmiChunk, n - lo);
+  const int lo = b * kXgmiArChunk;
+  const int len = min(kXgmiArChunk, n - lo);
   // 1) push my chunk into slot [p][rank] of every rank's receive buffer
   const size_t my_slot = ((size_t)p * world + rank) * kXgmiCap + lo;
   const bool vec = ((len & 3) == 0) && ((reinterpret_cast<uintptr_t>(x + lo) & 15) == 0);
@@ -93,7 +93,7 @@ int xgmi_allreduce_launch(float* const* data, uint32_t* const* flags, float* x, 
     p.data[r] = data[r];
     p.flags[r] = flags[r];
   }
-  const int nb = (n + kXgmiChunk - 1) / kXgmiChunk;
+  const int nb = (n + kXgmiArChunk - 1) / kXgmiArChunk;
   hipLaunchKernelGGL(xgmi_allreduce_kernel, dim3(nb), dim3(256), 0, st, p, x, n, rank, world, epochs,
                      err, spin_limit);
   return 0;
@@ -114,7 +114,9 @@ namespace pmd {
 //   4) forward: BatchNorm finalize from the global sums (params [4][C],
 //      running stats, num_batches_tracked, global count); backward: writes the
 //      global (sum dz, sum dz*xhat) as [2][C] for bn_bwd_elemt.
-constexpr int kBnPairs = (kXgmiChunk - 2) / 2;  // 1023 channels per block; [2*kBnPairs] = count
+constexpr int kBnPairs = (kXgmiChunk - 2) / 2;  // 255 channels per block; [2*kBnPairs] = count
+static int g_bn_pairs = 128;  // measured best of {255,128,64,32} (tests/test_xgmi_gpu.py)
+void xgmi_set_bn_pairs(int pairs) { g_bn_pairs = pairs < 1 ? 1 : (pairs > kBnPairs ? kBnPairs : pairs); }
 
 __global__ __launch_bounds__(256) void xgmi_bn_kernel(XgmiPeers peers, XgmiBnArgs a, int rank, int world,
                                                      uint32_t* __restrict__ epochs,
@@ -127,25 +129,38 @@ __global__ __launch_bounds__(256) void xgmi_bn_kernel(XgmiPeers peers, XgmiBnArg
     epochs[b] = e_sh;
   }
   const int P = a.CA + a.CB;
-  const int p0 = b * kBnPairs;
-  const int np = min(kBnPairs, P - p0);
-  // 0) collapse my channels' slots
-  for (int j = tid; j < np; j += 256) {
-    const int pi = p0 + j;
+  const int p0 = b * a.pairs;
+  const int np = min(a.pairs, P - p0);
+  // 0) collapse my channels' slots: one channel per thread (np <= kBnPairs < 256), all
+  //    2 * kStatSlots slot loads issued before the first add -- the slots were filled
+  //    by memory-side atomics, so each read is a full memory round trip and a
+  //    dependent chain would cost kStatSlots of them
+  static_assert(kBnPairs <= 256, "one channel per thread");
+  if (tid < np) {
+    const int pi = p0 + tid;
     const bool isA = pi < a.CA;
     float* slots = isA ? a.slotsA : a.slotsB;
     const int C = isA ? a.CA : a.CB;
     const int c = isA ? pi : pi - a.CA;
-    float s0 = 0.f, s1 = 0.f;
+    float v0[kStatSlots], v1[kStatSlots];
+#pragma unroll
     for (int k = 0; k < kStatSlots; ++k) {
-      float* q = slots + (size_t)k * 2 * C;
-      s0 += q[c];
-      s1 += q[C + c];
-      q[c] = 0.f;
-      q[C + c] = 0.f;
+      v0[k] = slots[(size_t)k * 2 * C + c];
+      v1[k] = slots[(size_t)k * 2 * C + C + c];
     }
-    loc[2 * j] = s0;
-    loc[2 * j + 1] = s1;
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int k = 0; k < kStatSlots; ++k) {
+      s0 += v0[k];
+      s1 += v1[k];
+    }
+#pragma unroll
+    for (int k = 0; k < kStatSlots; ++k) {
+      slots[(size_t)k * 2 * C + c] = 0.f;
+      slots[(size_t)k * 2 * C + C + c] = 0.f;
+    }
+    loc[2 * tid] = s0;
+    loc[2 * tid + 1] = s1;
     if (a.mode == 1) {
       float* acc0 = isA ? a.accA0 : a.accB0;
       float* acc1 = isA ? a.accA1 : a.accB1;
@@ -225,14 +240,20 @@ int xgmi_bn_launch(float* const* data, uint32_t* const* flags, const XgmiBnArgs&
                    uint32_t* epochs, uint32_t* err, long long spin_limit, hipStream_t st) {
   if (world < 1 || world > kXgmiMaxRanks) return 1;
   const int P = args.CA + args.CB;
-  const int nb = (P + kBnPairs - 1) / kBnPairs;
+  XgmiBnArgs a = args;
+  a.pairs = g_bn_pairs;
+  int nb = (P + a.pairs - 1) / a.pairs;
+  if (nb > kXgmiMaxBlocks) {  // too many blocks for the flag table: use fuller ones
+    a.pairs = kBnPairs;
+    nb = (P + a.pairs - 1) / a.pairs;
+  }
   if (P <= 0 || nb > kXgmiMaxBlocks) return 2;
   XgmiPeers p{};
   for (int r = 0; r < world; ++r) {
     p.data[r] = data[r];
     p.flags[r] = flags[r];
   }
-  hipLaunchKernelGGL(xgmi_bn_kernel, dim3(nb), dim3(256), 0, st, p, args, rank, world, epochs, err,
+  hipLaunchKernelGGL(xgmi_bn_kernel, dim3(nb), dim3(256), 0, st, p, a, rank, world, epochs, err,
                      spin_limit);
   return 0;
 }

@@ -196,6 +196,8 @@ class XgmiComm {
 };
 
 void register_xgmi(pybind11::module& m) {
+  m.def("xgmi_set_bn_pairs", &pmd::xgmi_set_bn_pairs,
+        "fused SyncBN kernel: channel pairs per block (1..255)");
   namespace py = pybind11;
   py::class_<XgmiComm>(m, "XgmiComm")
       .def(py::init<int64_t, int64_t, int64_t, double>(), py::arg("rank"), py::arg("world"),

@@ -218,7 +218,7 @@ class ResNet(nn.Module):
         if ws is None or self.__dict__.get("_pmd_wset_key") != key:
             entries = [(self.conv1, x.shape[-1], False)]
             for mod in self.modules():
-                if isinstance(mod, nn.Conv2d) and mod is not self.conv1:
+                if isinstance(mod, (nn.Conv2d, Conv2d)) and mod is not self.conv1:
                     entries.append((mod, mod.in_channels, True))
             ws = OF.WeightImageSet(entries)
             self.__dict__["_pmd_wset"] = ws

@@ -186,3 +186,40 @@ def test_checkpoint_loads_into_reference_model_class(tmp_path):
         want = rm(x)
         got = m.module(x.permute(0, 2, 3, 1).contiguous())
     torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-5)
+
+
+def test_weight_image_set_covers_every_conv(monkeypatch):
+    """The grouped weight-image refresh must serve EVERY conv of the model (one
+    prep launch per forward); a conv whose lookup misses falls back to its own
+    per-conv prep launch.  Simulated on CPU with a stand-in for the native
+    image table (the lookup keys are what is under test)."""
+    from pytorch_multiprocessing_distributed_amd.ops import torch_prims as TP
+    from pytorch_multiprocessing_distributed_amd.ops.native import C
+
+    class FakeImages:
+        def __init__(self, ws, cps, wts):
+            self.e = list(zip(ws, cps, wts))
+
+        def refresh(self):
+            pass
+
+        def get(self, i):
+            w, cp, wt = self.e[i]
+            return list(TP.conv_weight(w, torch.float32, cp, wt))
+
+    monkeypatch.setattr(C, "WeightImages", FakeImages, raising=False)
+    monkeypatch.setattr(TP, "SUPPORTS_FP8", True, raising=False)
+    calls = {"hit": 0, "miss": 0}
+    orig = OF.WeightImageSet.lookup
+
+    def lookup(self, w, cin, want_t):
+        r = orig(self, w, cin, want_t)
+        calls["hit" if r is not None else "miss"] += 1
+        return r
+    monkeypatch.setattr(OF.WeightImageSet, "lookup", lookup)
+    for name, stem, hw in [("resnet50", "imagenet", 64), ("res", "cifar", 32)]:
+        calls.update(hit=0, miss=0)
+        m = build_model(name, num_classes=10, stem=stem)
+        m(torch.randn(2, hw, hw, 8 if stem == "imagenet" else 3)).sum().backward()
+        nconv = sum(1 for mod in m.modules() if hasattr(mod, "kernel_size"))
+        assert calls == {"hit": nconv, "miss": 0}, (name, calls, nconv)
