@@ -201,6 +201,25 @@ def _bn_acc(bn):
     return (tb, tg)
 
 
+class _Pre(list):
+    """BN-backward reduce slot buffers produced by a fused dgrad epilogue, plus
+    the HIP event recorded right after that dgrad (None on CPU)."""
+    __slots__ = ("event",)
+
+    def __init__(self, bufs, event=None):
+        super().__init__(bufs)
+        self.event = event
+
+
+def _after_dgrad_event(t, sync):
+    if sync is None or not t.is_cuda or not getattr(sync, "overlap_bn_bwd", False) \
+            or getattr(sync, "xgmi", None) is None:
+        return None
+    ev = torch.cuda.Event()
+    ev.record()
+    return ev
+
+
 # ---------------------------------------------------------------- BN pieces
 def _bn_forward_params(P, y, st, bn, training, sync, y2=None, st2=None, bn2=None):
     """-> (p1, p2, count); count is a host float (local) or device scalar (SyncBN)."""
@@ -267,7 +286,21 @@ def _bn_backward(P, dout, mask, relu, training, sync, count, y1, p1, bn1, y2=Non
         # collapse (+= local gamma/beta grads) + one-shot exchange in ONE kernel
         c2 = y2.shape[-1] if y2 is not None else 0
         red = torch.empty(2 * c1 + 2 * c2, dtype=torch.float32, device=dout.device)
-        sync.bn_stats_bwd(r1, r2, acc1, acc2, red[:2 * c1], red[2 * c1:] if c2 else None)
+        ev = getattr(pre, "event", None) if pre is not None else None
+        if ev is not None and getattr(sync, "overlap_bn_bwd", False):
+            # the reduce slots were complete right after the dgrad that produced them
+            # (event); run the exchange on the side stream from there, so it overlaps
+            # the weight-gradient kernel(s) issued since, and join before bn_bwd_elemt
+            # (and before the gamma/beta grads are marked ready for the reducer)
+            side = sync.side_stream()
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                sync.bn_stats_bwd(r1, r2, acc1, acc2, red[:2 * c1], red[2 * c1:] if c2 else None)
+            done = torch.cuda.Event()
+            done.record(side)
+            torch.cuda.current_stream().wait_event(done)
+        else:
+            sync.bn_stats_bwd(r1, r2, acc1, acc2, red[:2 * c1], red[2 * c1:] if c2 else None)
         P._release(r1, r2)
         _ready(bn1.bias, bn1.weight)
         if bn2 is not None:
@@ -555,7 +588,8 @@ class _ResidualBlockFn(torch.autograd.Function):
             if not fuse:
                 return P.conv_dgrad(dy_, wp_, shape, stride, pad, addend), None
             _hin, _wp, y_, p_, z_ = rec
-            return P.conv_dgrad(dy_, wp_, shape, stride, pad, addend, bnred=(z_, [(y_, p_)]))
+            dx_, red_ = P.conv_dgrad(dy_, wp_, shape, stride, pad, addend, bnred=(z_, [(y_, p_)]))
+            return dx_, _Pre(red_, _after_dgrad_event(dx_, sync if training else None))
         chk("dyf", dyf)
         # --- final conv
         dh, pre_k = dgrad_fused(dyf, wpf, tuple(hlast.shape), fconv.stride, fconv.padding, recs[-1])
@@ -587,7 +621,7 @@ class _ResidualBlockFn(torch.autograd.Function):
                     dx, site_red = P.conv_dgrad(dy, wp, tuple(x.shape), conv_m.stride,
                                                 conv_m.padding, addend, bnred=(site.mask, site.sets),
                                                 addend_mask=amask)
-                    site.put(dx, site_red)
+                    site.put(dx, _Pre(site_red, _after_dgrad_event(dx, sync if training else None)))
                 else:
                     dx = P.conv_dgrad(dy, wp, tuple(x.shape), conv_m.stride, conv_m.padding, addend,
                                       addend_mask=amask)

@@ -36,6 +36,18 @@ class Comm:
         self.order_check_every = int(os.environ.get("PMD_CHECK_ORDER", "0"))
         self._seq = 0
         self._ncoll = 0
+        # backward SyncBN exchanges run on a high-priority side stream so they
+        # overlap the weight-gradient GEMM issued between the producing dgrad
+        # and the BN backward (see ops/functional.py::_bn_backward)
+        self.overlap_bn_bwd = os.environ.get("PMD_SYNCBN_OVERLAP", "1") != "0"
+        self._side = None
+
+    def side_stream(self):
+        """High-priority HIP stream for latency-bound SyncBN exchanges (GPU only)."""
+        if self._side is None:
+            import torch
+            self._side = torch.cuda.Stream(priority=-1)
+        return self._side
 
     def _record(self, op, t):
         key = f"{op}:{t.numel()}:{t.dtype}".encode()
