@@ -44,7 +44,9 @@ constexpr int BR = 64;  // reduction rows per stage
 
 template <int ROWB>
 __device__ __forceinline__ int swz(int row) {
-  if (ROWB == 256) return (row & 3) | (((row >> 3) & 1) << 2);
+  // 256-B and 512-B rows: both put every row at the same bank offset, so the same
+  // 3-bit window XOR spreads the 8 rows of a transposed read over 8 windows
+  if (ROWB >= 256) return (row & 3) | (((row >> 3) & 1) << 2);
   return ((row >> 1) & 1) | ((row >> 2) & 2);  // 128-byte rows
 }
 
@@ -238,15 +240,16 @@ __device__ __forceinline__ void wg_wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN, int BRD, int NST>
-__global__ __launch_bounds__(256, 2) void conv_wgrad_dma_kernel(WgradArgs a) {
-  constexpr int MI = BM / 32, NI = BN / 32;
+template <int BM, int BN, int BRD, int NST, int WM = 2, int WN = 2>
+__global__ __launch_bounds__(64 * WM * WN, 2) void conv_wgrad_dma_kernel(WgradArgs a) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int MI = BM / (16 * WM), NI = BN / (16 * WN);
   constexpr int A_BYTES = BRD * BM * 2, B_BYTES = BRD * BN * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WN, wn = wid % WN;
   const int tilesM = a.K / BM + (a.K % BM != 0);
   const int tilesN = (a.Kg + BN - 1) / BN;
   const int tiles = tilesM * tilesN;
@@ -261,9 +264,10 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_dma_kernel(WgradArgs a) {
   if (mend > a.M) mend = a.M;
   const int nchunks = (mend - mbeg + BRD - 1) / BRD;
 
-  constexpr int CA = BM / 8, RA = 256 / CA, PA = BRD / RA;
-  constexpr int CB = BN / 8, RB = 256 / CB, PB = BRD / RB;
+  constexpr int CA = BM / 8, RA = NT / CA, PA = BRD / RA;
+  constexpr int CB = BN / 8, RB = NT / CB, PB = BRD / RB;
   static_assert(PA >= 1 && PB >= 1 && RA % 16 == 0 && RB % 16 == 0, "DMA wgrad tile shape");
+  static_assert(NST * STAGE <= 160 * 1024, "exceeds the 160 KiB LDS of a CU");
   constexpr int LPT = PA + PB;  // DMA instructions per thread per stage
   const int a_row = tid / CA, b_row = tid / CB;
   const int a_pc = tid % CA, b_pc = tid % CB;  // physical 16-B chunk in the row
@@ -339,7 +343,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_dma_kernel(WgradArgs a) {
       typedef __attribute__((ext_vector_type(8))) short s16x8;
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        const int col = wm * (BM / 2) + i * 16 + 4 * p4;
+        const int col = wm * (BM / WM) + i * 16 + 4 * p4;
         s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
             (__attribute__((address_space(3))) s16x4*)(As + toff<BM>(r0, col)));
         s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -349,7 +353,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_dma_kernel(WgradArgs a) {
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        const int col = wn * (BN / 2) + j * 16 + 4 * p4;
+        const int col = wn * (BN / WN) + j * 16 + 4 * p4;
         s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
             (__attribute__((address_space(3))) s16x4*)(Bs + toff<BN>(r0, col)));
         s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -392,8 +396,8 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_dma_kernel(WgradArgs a) {
     for (int j = 0; j < NI; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int k = k0 + wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + e;
-        const int gg = g0 + wn * (BN / 2) + j * 16 + (lane & 15);
+        const int k = k0 + wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + e;
+        const int gg = g0 + wn * (BN / WN) + j * 16 + (lane & 15);
         if (k < a.K && gg < a.Kg) {
           float* p = dst + (size_t)k * a.Kg + gg;
           if (a.ws)
@@ -462,38 +466,18 @@ static int wgrad_target_blocks(int R) {
   return R == 1 ? t1 : (R <= 3 ? t3 : t7);
 }
 
-// Staging variant (conv_wgrad_set_impl or PMD_WGRAD_IMPL): 0 register staging
-// (2 stages), 1 LDS-DMA 64-row stages x2, 2 LDS-DMA 32-row x4, 3 LDS-DMA 64-row x3.
+// Variant (conv_wgrad_set_impl or PMD_WGRAD_IMPL): 0 register staging
+// (2 stages), 1 LDS-DMA 64-row stages x2 (default: autotuned per shape over
+// {0, 1, 4, 5}), 2 LDS-DMA 32-row x4, 3 LDS-DMA 64-row x3, 4 8-wave 256x256
+// LDS-DMA 64-row x2, 5 8-wave 256x128 (4/5 need K >= 256; else 1 is used).
 static int g_wgrad_impl = -1;
 void conv_wgrad_set_impl(int impl) { g_wgrad_impl = impl; }
 static int wgrad_impl() {
   if (g_wgrad_impl < 0) {
     const char* e = getenv("PMD_WGRAD_IMPL");
-    g_wgrad_impl = (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 1;
+    g_wgrad_impl = (e && e[0] >= '0' && e[0] <= '5') ? e[0] - '0' : 1;
   }
   return g_wgrad_impl;
-}
-
-static void wgrad_dispatch(int impl, const WgradArgs& a, dim3 grid, hipStream_t st) {
-  const bool k64 = a.K == 64;
-  switch (impl) {
-    case 0:
-      if (k64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128>), grid, dim3(256), 0, st, a);
-      else hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), grid, dim3(256), 0, st, a);
-      break;
-    case 2:  // DMA, 32-row stages, 4-deep ring
-      if (k64) hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 128, 32, 4>), grid, dim3(256), 0, st, a);
-      else hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 32, 4>), grid, dim3(256), 0, st, a);
-      break;
-    case 3:  // DMA, 64-row stages, 3-deep ring (1 block/CU at BM=128)
-      if (k64) hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 128, 64, 3>), grid, dim3(256), 0, st, a);
-      else hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 64, 3>), grid, dim3(256), 0, st, a);
-      break;
-    default:  // 1: DMA, 64-row stages, 2-deep ring
-      if (k64) hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 128, 64, 2>), grid, dim3(256), 0, st, a);
-      else hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 64, 2>), grid, dim3(256), 0, st, a);
-      break;
-  }
 }
 
 // Per-shape autotuning of the staging variant (register staging vs LDS-DMA),
@@ -519,7 +503,86 @@ static bool wgrad_autotune_on() {
   return on == 1;
 }
 
-static int wgrad_tune(const WgradArgs& a0, dim3 grid, int splits, hipStream_t st) {
+// Output tile of a staging variant: 4-wave 128-row tiles (BM 64 for K = 64),
+// 8-wave 256x256 / 256x128 tiles (K >= 256).  The split-K plan aims at
+// target blocks; an 8-wave block is one per CU and does 2-4x the work of a
+// 128-row one, so it aims at a quarter / half as many (but >= 256).
+struct WgradCfg {
+  int impl, BM, BN, target;
+};
+
+static bool wgrad_cfg_ok(int impl, const WgradArgs& a) {
+  if (impl == 4) return a.K >= 256 && a.Kg >= 256;
+  if (impl == 5) return a.K >= 256;
+  return true;
+}
+
+static WgradCfg wgrad_cfg(int impl, const WgradArgs& a) {
+  const int t = wgrad_target_blocks(a.R);
+  if (impl == 4) return {4, 256, 256, t / 4 > 256 ? t / 4 : 256};
+  if (impl == 5) return {5, 256, 128, t / 2 > 256 ? t / 2 : 256};
+  return {impl, a.K == 64 ? 64 : 128, 128, t};
+}
+
+static void plan(const WgradArgs& a, const WgradCfg& cfg, int* splits_out, int* cps_out) {
+  const int tiles = ((a.K + cfg.BM - 1) / cfg.BM) * ((a.Kg + cfg.BN - 1) / cfg.BN);
+  const int chunks = (a.M + BR - 1) / BR;
+  int splits = (cfg.target + tiles - 1) / tiles;
+  const int max_splits = (chunks + 3) / 4;
+  if (splits > max_splits) splits = max_splits;
+  // keep the partial workspace bounded (<= 96 MiB)
+  const long long per = (long long)a.K * a.Kg * 4;
+  while (splits > 1 && per * splits > (96ll << 20)) --splits;
+  if (splits < 1) splits = 1;
+  const int cps = (chunks + splits - 1) / splits;
+  *cps_out = cps;
+  *splits_out = (chunks + cps - 1) / cps;
+}
+
+// One full weight gradient with variant `impl`: split-K plan, kernel, split reduce.
+static void wgrad_run(int impl, WgradArgs a, float* ws, hipStream_t st) {
+  const WgradCfg cfg = wgrad_cfg(impl, a);
+  int splits, cps;
+  plan(a, cfg, &splits, &cps);
+  a.chunks_per_split = cps;
+  a.ws = splits > 1 ? ws : nullptr;
+  const int tiles = ((a.K + cfg.BM - 1) / cfg.BM) * ((a.Kg + cfg.BN - 1) / cfg.BN);
+  const dim3 grid(tiles * splits);
+  const bool k64 = a.K == 64;
+  switch (impl) {
+    case 0:
+      if (k64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), grid, dim3(256), 0, st, a);
+      break;
+    case 2:  // DMA, 32-row stages, 4-deep ring
+      if (k64) hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 128, 32, 4>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 32, 4>), grid, dim3(256), 0, st, a);
+      break;
+    case 3:  // DMA, 64-row stages, 3-deep ring (1 block/CU at BM=128)
+      if (k64) hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 128, 64, 3>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 64, 3>), grid, dim3(256), 0, st, a);
+      break;
+    case 4:  // 8 waves, 256x256, DMA 64-row x2
+      hipLaunchKernelGGL((conv_wgrad_dma_kernel<256, 256, 64, 2, 2, 4>), grid, dim3(512), 0, st, a);
+      break;
+    case 5:  // 8 waves, 256x128, DMA 64-row x2
+      hipLaunchKernelGGL((conv_wgrad_dma_kernel<256, 128, 64, 2, 4, 2>), grid, dim3(512), 0, st, a);
+      break;
+    default:  // 1: DMA, 64-row stages, 2-deep ring
+      if (k64) hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 128, 64, 2>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 64, 2>), grid, dim3(256), 0, st, a);
+      break;
+  }
+  if (splits > 1) {
+    const long long n4 = (long long)a.K * a.Kg / 4;
+    const int groups = (splits + kSplitGroup - 1) / kSplitGroup;
+    long long b = (n4 + 255) / 256;
+    if (b > 4096) b = 4096;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)b, groups), dim3(256), 0, st, a.ws, a.dw, splits, n4);
+  }
+}
+
+static int wgrad_tune(const WgradArgs& a0, float* ws, hipStream_t st) {
   WgradArgs a = a0;
   static float* scratch = nullptr;
   static size_t scratch_n = 0;
@@ -529,22 +592,21 @@ static int wgrad_tune(const WgradArgs& a0, dim3 grid, int splits, hipStream_t st
     if (hipMalloc(&scratch, sizeof(float) * need) != hipSuccess) return -1;
     scratch_n = need;
   }
-  a.dw = scratch;  // splits == 1 accumulates into dw; otherwise dw is untouched here
-  (void)splits;
+  a.dw = scratch;  // kernel (+ split reduce) accumulate into a scratch dW, not the caller's
   static hipEvent_t e0 = nullptr, e1 = nullptr;
   if (!e0) {
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
   }
-  const int cands[2] = {0, 1};
   int best = -1;
   float best_ms = 1e30f;
-  for (int c : cands) {
-    wgrad_dispatch(c, a, grid, st);
+  for (int c : {0, 1, 4, 5}) {
+    if (!wgrad_cfg_ok(c, a)) continue;
+    wgrad_run(c, a, ws, st);
     float t = 1e30f;
     for (int r = 0; r < 3; ++r) {
       (void)hipEventRecord(e0, st);
-      wgrad_dispatch(c, a, grid, st);
+      wgrad_run(c, a, ws, st);
       (void)hipEventRecord(e1, st);
       if (hipEventSynchronize(e1) != hipSuccess) return -1;
       float ms = 0.f;
@@ -561,23 +623,6 @@ static int wgrad_tune(const WgradArgs& a0, dim3 grid, int splits, hipStream_t st
     fprintf(stderr, "[pmd autotune] wgrad N=%d H=%d W=%d C=%d K=%d R=%d s=%d: impl %d (%.1f us)\n", a.N,
             a.H, a.W, a.C, a.K, a.R, a.stride, best, best_ms * 1e3f);
   return best;
-}
-
-template <int BM>
-static void plan(const WgradArgs& a, int* splits_out, int* cps_out) {
-  constexpr int BN = 128;
-  const int tiles = ((a.K + BM - 1) / BM) * ((a.Kg + BN - 1) / BN);
-  const int chunks = (a.M + BR - 1) / BR;
-  int splits = (wgrad_target_blocks(a.R) + tiles - 1) / tiles;
-  const int max_splits = (chunks + 3) / 4;
-  if (splits > max_splits) splits = max_splits;
-  // keep the partial workspace bounded (<= 96 MiB)
-  const long long per = (long long)a.K * a.Kg * 4;
-  while (splits > 1 && per * splits > (96ll << 20)) --splits;
-  if (splits < 1) splits = 1;
-  const int cps = (chunks + splits - 1) / splits;
-  *cps_out = cps;
-  *splits_out = (chunks + cps - 1) / cps;
 }
 
 static void fill_args(WgradArgs& a, int N, int H, int W, int C, int P, int Q, int K, int R, int S,
@@ -598,16 +643,20 @@ static void fill_args(WgradArgs& a, int N, int H, int W, int C, int P, int Q, in
   a.Kg = R * S * C;
 }
 
+// workspace slices the caller must provide: the max over every variant the
+// launcher may pick (the autotuner chooses at launch time)
 int conv_wgrad_splits(int N, int H, int W, int C, int P, int Q, int K, int R, int S, int stride,
                       int pad) {
   WgradArgs a;
   fill_args(a, N, H, W, C, P, Q, K, R, S, stride, pad);
-  int splits, cps;
-  if (K == 64)
-    plan<64>(a, &splits, &cps);
-  else
-    plan<128>(a, &splits, &cps);
-  return splits;
+  int best = 1;
+  for (int impl : {0, 1, 4, 5}) {
+    if (!wgrad_cfg_ok(impl, a)) continue;
+    int splits, cps;
+    plan(a, wgrad_cfg(impl, a), &splits, &cps);
+    best = splits > best ? splits : best;
+  }
+  return best;
 }
 
 int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, float* ws, int N, int H, int W,
@@ -620,18 +669,9 @@ int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, float* ws, i
   a.x = x;
   a.dw = dw;
   fill_args(a, N, H, W, C, P, Q, K, R, S, stride, pad);
-  int splits, cps;
-  if (K == 64)
-    plan<64>(a, &splits, &cps);
-  else
-    plan<128>(a, &splits, &cps);
-  a.chunks_per_split = cps;
-  a.ws = splits > 1 ? ws : nullptr;
-  if (splits > 1 && !ws) return 5;
-  const int BM = K == 64 ? 64 : 128;
-  const int tiles = ((a.K + BM - 1) / BM) * ((a.Kg + 127) / 128);
-  const dim3 grid(tiles * splits);
+  if (!ws && conv_wgrad_splits(N, H, W, C, P, Q, K, R, S, stride, pad) > 1) return 5;
   int impl = wgrad_impl();
+  if (!wgrad_cfg_ok(impl, a)) impl = 1;
   if (impl == 1 && wgrad_autotune_on()) {
     const WgradKey key{{N, H, W, C, P, Q, K, R, S, stride, pad}};
     int c = -1;
@@ -644,7 +684,7 @@ int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, float* ws, i
       hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
       (void)hipStreamIsCapturing(st, &cs);
       if (cs == hipStreamCaptureStatusNone) {
-        c = wgrad_tune(a, grid, splits, st);
+        c = wgrad_tune(a, ws, st);
         if (c >= 0) {
           std::lock_guard<std::mutex> lk(g_wtune_mu);
           g_wtune[key] = c;
@@ -653,14 +693,7 @@ int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, float* ws, i
     }
     if (c >= 0) impl = c;
   }
-  wgrad_dispatch(impl, a, grid, st);
-  if (splits > 1) {
-    const long long n4 = (long long)a.K * a.Kg / 4;
-    const int groups = (splits + kSplitGroup - 1) / kSplitGroup;
-    long long b = (n4 + 255) / 256;
-    if (b > 4096) b = 4096;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)b, groups), dim3(256), 0, st, ws, dw, splits, n4);
-  }
+  wgrad_run(impl, a, ws, st);
   return 0;
 }
 
