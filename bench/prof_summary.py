@@ -20,15 +20,36 @@ def main():
     ap.add_argument("db")
     ap.add_argument("--steps", type=int, default=0, help="training steps in the trace")
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--skip", type=int, default=0,
+                    help="ignore everything before the (skip+1)-th --marker dispatch (warm-up / "
+                         "autotuning steps); then --steps defaults to the markers counted after it")
+    ap.add_argument("--marker", default="synth_images_kernel", help="one dispatch per training step")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
-    rows = c.execute("select name, total_calls, total_duration, average from top_kernels").fetchall()
     agg = {}
-    for n, calls, tot, _ in rows:
-        k = short(n)
-        e = agg.setdefault(k, [0, 0.0])
-        e[0] += calls
-        e[1] += tot
+    if a.skip:
+        ks = c.execute("select name, start, end from kernels order by start").fetchall()
+        marks = [i for i, (n, _, _) in enumerate(ks) if a.marker in n]
+        if len(marks) <= a.skip:
+            raise SystemExit(f"only {len(marks)} '{a.marker}' dispatches in the trace")
+        ks = ks[marks[a.skip]:]
+        if not a.steps:
+            a.steps = len(marks) - a.skip
+        span = (ks[-1][2] - ks[0][1]) / 1e6
+        busy = sum(e - s for _, s, e in ks) / 1e6
+        print(f"# window: {a.steps} steps, wall {span:.2f} ms ({span / a.steps:.2f} ms/step), "
+              f"kernels busy {busy:.2f} ms ({100 * busy / span:.1f}% of wall)")
+        for n, s_, e_ in ks:
+            e = agg.setdefault(short(n), [0, 0.0])
+            e[0] += 1
+            e[1] += (e_ - s_) / 1e3
+    else:
+        rows = c.execute("select name, total_calls, total_duration, average from top_kernels").fetchall()
+        for n, calls, tot, _ in rows:
+            k = short(n)
+            e = agg.setdefault(k, [0, 0.0])
+            e[0] += calls
+            e[1] += tot
     total = sum(v[1] for v in agg.values())
     print(f"# total kernel time {total / 1e3:.2f} ms over {sum(v[0] for v in agg.values())} dispatches"
           + (f"; {total / 1e3 / a.steps:.2f} ms per step ({a.steps} steps)" if a.steps else ""))

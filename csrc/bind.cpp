@@ -385,6 +385,60 @@ Tensor maxpool_bwd(Tensor dout, Tensor arg, int64_t H, int64_t W) {
   return dx;
 }
 
+// fused stem tail: y (conv1 output) + BN params -> pooled activation + argmax taps
+std::vector<Tensor> stem_pool_fwd(Tensor y, Tensor params) {
+  CHECK_DEV(y); CHECK_BF16(y); CHECK_CONT(y); CHECK_CONT(params);
+  const int N = y.size(0), H = y.size(1), W = y.size(2), C = y.size(3);
+  TORCH_CHECK(params.numel() == 4 * C, "stem_pool_fwd: params [4][C]");
+  const int P = (H + 2 - 3) / 2 + 1, Q = (W + 2 - 3) / 2 + 1;
+  c10::DeviceGuard g(y.device());
+  Tensor out = torch::empty({N, P, Q, C}, y.options());
+  Tensor arg = torch::empty({N, P, Q, C}, y.options().dtype(torch::kUInt8));
+  CHECK_RC(pmd::stem_pool_fwd_launch(bfp(y), params.data_ptr<float>(), bfp_mut(out), arg.data_ptr<uint8_t>(),
+                                     N, H, W, C, P, Q, cur_stream()), "stem_pool_fwd");
+  return {out, arg};
+}
+
+// pass 1 of the fused stem backward: sum(dz), sum(dz*xhat) into `red` slots [S][2][C]
+Tensor stem_pool_bwd_reduce(Tensor dout, Tensor arg, Tensor y, Tensor params, Tensor red) {
+  CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONT(dout); CHECK_CONT(arg);
+  CHECK_BF16(y); CHECK_CONT(y); CHECK_CONT(params); CHECK_CONT(red);
+  const int N = y.size(0), H = y.size(1), W = y.size(2), C = y.size(3);
+  const int P = dout.size(1), Q = dout.size(2);
+  TORCH_CHECK(dout.size(0) == N && dout.size(3) == C && arg.sizes() == dout.sizes(), "stem_pool_bwd: shapes");
+  TORCH_CHECK(red.numel() == 64 * 2 * C && red.scalar_type() == torch::kFloat32, "stem_pool_bwd: slots");
+  c10::DeviceGuard g(y.device());
+  CHECK_RC(pmd::stem_pool_bwd_reduce_launch(bfp(dout), arg.data_ptr<uint8_t>(), bfp(y), params.data_ptr<float>(),
+                                            red.data_ptr<float>(), N, H, W, C, P, Q, cur_stream()),
+           "stem_pool_bwd_reduce");
+  return red;
+}
+
+// pass 2: dy (gradient of the conv1 output)
+Tensor stem_pool_bwd_elemt(Tensor dout, Tensor arg, Tensor y, Tensor params, Tensor gamma,
+                           c10::optional<Tensor> red, c10::optional<Tensor> count, double count_h,
+                           bool eval_mode) {
+  CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONT(dout); CHECK_CONT(arg);
+  CHECK_BF16(y); CHECK_CONT(y); CHECK_CONT(params);
+  const int N = y.size(0), H = y.size(1), W = y.size(2), C = y.size(3);
+  const int P = dout.size(1), Q = dout.size(2);
+  TORCH_CHECK(dout.size(0) == N && dout.size(3) == C && arg.sizes() == dout.sizes(), "stem_pool_bwd: shapes");
+  Tensor gm = gamma.contiguous(), rr, cc;
+  if (!eval_mode) {
+    TORCH_CHECK(red && red->defined() && red->numel() == 2 * C, "stem_pool_bwd: train backward needs [2][C] sums");
+    rr = red->contiguous();
+    if (count && count->defined()) cc = count->contiguous();
+  }
+  c10::DeviceGuard g(y.device());
+  Tensor dy = torch::empty_like(y);
+  CHECK_RC(pmd::stem_pool_bwd_elemt_launch(bfp(dout), arg.data_ptr<uint8_t>(), bfp(y), params.data_ptr<float>(),
+                                           gm.data_ptr<float>(), eval_mode ? nullptr : rr.data_ptr<float>(),
+                                           cc.defined() ? cc.data_ptr<float>() : nullptr, (float)count_h,
+                                           bfp_mut(dy), N, H, W, C, P, Q, eval_mode, cur_stream()),
+           "stem_pool_bwd_elemt");
+  return dy;
+}
+
 Tensor avgpool_fwd(Tensor x) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_CONT(x);
   const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
@@ -585,6 +639,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd_elemt", &bn_bwd_elemt);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("stem_pool_fwd", &stem_pool_fwd);
+  m.def("stem_pool_bwd_reduce", &stem_pool_bwd_reduce);
+  m.def("stem_pool_bwd_elemt", &stem_pool_bwd_elemt);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("xent_fwd", &xent_fwd);

@@ -64,6 +64,16 @@ int bn_bwd_elemt_launch(const bf16_t* dout, const uint8_t* mask, const bf16_t* y
                         bf16_t* dy, bf16_t* dzm, long long M, int C, bool relu, bool eval_mode,
                         hipStream_t st);
 
+// fused stem tail (kernels/stem.hip): BN + ReLU + 3x3/s2 max-pool, and its backward
+int stem_pool_fwd_launch(const bf16_t* y, const float* params, bf16_t* out, uint8_t* arg, int N, int H,
+                         int W, int C, int P, int Q, hipStream_t st);
+int stem_pool_bwd_reduce_launch(const bf16_t* dout, const uint8_t* arg, const bf16_t* y,
+                                const float* params, float* red, int N, int H, int W, int C, int P, int Q,
+                                hipStream_t st);
+int stem_pool_bwd_elemt_launch(const bf16_t* dout, const uint8_t* arg, const bf16_t* y, const float* params,
+                               const float* gamma, const float* red, const float* count, float count_h,
+                               bf16_t* dy, int N, int H, int W, int C, int P, int Q, bool eval_mode,
+                               hipStream_t st);
 int maxpool_fwd_launch(const bf16_t* x, bf16_t* out, uint8_t* arg, int N, int H, int W, int C, int P,
                        int Q, hipStream_t st);
 int maxpool_bwd_launch(const bf16_t* dout, const uint8_t* arg, bf16_t* dx, int N, int H, int W, int C,

@@ -1,0 +1,246 @@
+// Fused ImageNet stem tail: BatchNorm + ReLU + 3x3/s2 max-pool in ONE pass
+// forward, and max-pool backward + BatchNorm(+ReLU) backward in two passes
+// (reduce, elementwise) -- the [N,112,112,64] stem activation is never
+// materialised (forward: it was written by bn_apply and re-read by the pool;
+// backward: the pool gradient was written and re-read twice by the BN
+// backward).  Same arithmetic and tie-breaking as the composite path
+// (bn_apply -> maxpool_fwd; maxpool_bwd -> bn_bwd_reduce -> bn_bwd_elemt):
+//   a = bf16(relu(y*scale + shift)), window max = first strictly greater a,
+//   ReLU mask bit = (y*scale + shift > 0), pool gradient rounded to bf16.
+// Reference: model/resnet.py:97 (conv -> SyncBN -> relu) followed by the
+// ImageNet max-pool this framework adds for 224x224 inputs.
+#include "common.h"
+
+namespace pmd {
+
+__device__ __forceinline__ void ld8(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// y [N,H,W,C] bf16 (conv output), params [4][C] (mean, invstd, scale, shift)
+// -> out [N,P,Q,C] bf16, arg [N,P,Q,C] uint8 tap (0..8) of the window max.
+// grid.y = output row (n, p); x covers Q * C/8 chunks.
+__global__ __launch_bounds__(256) void stem_pool_fwd_kernel(const bf16_t* __restrict__ y,
+                                                            const float* __restrict__ params,
+                                                            bf16_t* __restrict__ out,
+                                                            uint8_t* __restrict__ arg, int H, int W,
+                                                            int C, int P, int Q, int log2C8) {
+  const int C8 = C >> 3;
+  const int row = blockIdx.y;
+  const int n = row / P, p = row - (row / P) * P;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= Q * C8) return;
+  const int q = j >> log2C8, cc = j & (C8 - 1);
+  float sc[8], sh[8];
+  ld8(params + 2 * C + cc * 8, sc);
+  ld8(params + 3 * C + cc * 8, sh);
+  float best[8];
+  int bi[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    best[k] = -INFINITY;
+    bi[k] = 0;
+  }
+  const bf16_t* yb = y + (size_t)n * H * W * C + cc * 8;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int ih = p * 2 - 1 + t / 3, iw = q * 2 - 1 + t % 3;
+    if ((unsigned)ih >= (unsigned)H || (unsigned)iw >= (unsigned)W) continue;
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(yb + ((size_t)ih * W + iw) * C), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float a = round_bf(fmaxf(v[k] * sc[k] + sh[k], 0.f));
+      if (a > best[k]) {
+        best[k] = a;
+        bi[k] = t;
+      }
+    }
+  }
+  const size_t o = (size_t)row * Q * C8 + j;
+  reinterpret_cast<uint4*>(out)[o] = pack8(best);
+  uint2 packed;
+  packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
+  packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
+  reinterpret_cast<uint2*>(arg)[o] = packed;
+}
+
+// dz of one 8-channel input chunk (n, h, w, cc): the bf16-rounded sum of the
+// dout of the (<= 4) windows whose argmax is this pixel, gated by the ReLU.
+__device__ __forceinline__ void stem_dz(const bf16_t* __restrict__ dout, const uint8_t* __restrict__ arg,
+                                        int n, int h, int w, int cc, int C8, int P, int Q,
+                                        const float (&v)[8], const float (&sc)[8], const float (&sh)[8],
+                                        float (&dz)[8]) {
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  const int p_lo = h > 0 ? h >> 1 : 0;
+  const int p_hi = min((h + 1) >> 1, P - 1);
+  const int q_lo = w > 0 ? w >> 1 : 0;
+  const int q_hi = min((w + 1) >> 1, Q - 1);
+  for (int p = p_lo; p <= p_hi; ++p)
+    for (int q = q_lo; q <= q_hi; ++q) {
+      const int dh = h - (p * 2 - 1), dw = w - (q * 2 - 1);
+      if (dh < 0 || dh > 2 || dw < 0 || dw > 2) continue;
+      const int tap = dh * 3 + dw;
+      const size_t o = (((size_t)n * P + p) * Q + q) * C8 + cc;
+      const uint2 a = reinterpret_cast<const uint2*>(arg)[o];
+      float g[8];
+      unpack8(reinterpret_cast<const uint4*>(dout)[o], g);
+      const uint32_t aw[2] = {a.x, a.y};
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if ((int)((aw[k >> 2] >> ((k & 3) * 8)) & 0xff) == tap) acc[k] += g[k];
+    }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) dz[k] = (v[k] * sc[k] + sh[k] > 0.f) ? round_bf(acc[k]) : 0.f;
+}
+
+// Pass 1: per-channel sum(dz), sum(dz * xhat) into kStatSlots slot copies.
+// Block = a run of input rows (n, h); thread tid keeps channel chunk tid % C8
+// for the whole block (256 % C8 == 0), partials combined in LDS, one atomic
+// per channel per block.
+__global__ __launch_bounds__(256) void stem_pool_bwd_reduce_kernel(
+    const bf16_t* __restrict__ dout, const uint8_t* __restrict__ arg, const bf16_t* __restrict__ y,
+    const float* __restrict__ params, float* __restrict__ red, int N, int H, int W, int C, int P, int Q,
+    int rows_per_block) {
+  __shared__ float part[256 * 17];
+  const int C8 = C >> 3;
+  const int tid = threadIdx.x;
+  const int cc = tid % C8;
+  float mean[8], inv[8], sc[8], sh[8];
+  ld8(params + cc * 8, mean);
+  ld8(params + C + cc * 8, inv);
+  ld8(params + 2 * C + cc * 8, sc);
+  ld8(params + 3 * C + cc * 8, sh);
+  float s1[8], s2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(r0 + rows_per_block, N * H);
+  for (int row = r0; row < r1; ++row) {
+    const int n = row / H, h = row - (row / H) * H;
+    for (int j = tid; j < W * C8; j += 256) {
+      const int w = j / C8;
+      float v[8], dz[8];
+      unpack8(reinterpret_cast<const uint4*>(y)[(size_t)row * W * C8 + j], v);
+      stem_dz(dout, arg, n, h, w, cc, C8, P, Q, v, sc, sh, dz);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s1[k] += dz[k];
+        s2[k] += dz[k] * (v[k] - mean[k]) * inv[k];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    part[tid * 17 + k] = s1[k];
+    part[tid * 17 + 8 + k] = s2[k];
+  }
+  __syncthreads();
+  for (int e = tid; e < C8 * 16; e += 256) {
+    const int col = e >> 4, k = e & 15;
+    float a = 0.f;
+    for (int r = col; r < 256; r += C8) a += part[r * 17 + k];
+    float* slot = red + (size_t)(blockIdx.x % kStatSlots) * 2 * C;
+    atomicAdd(slot + (k < 8 ? 0 : C) + col * 8 + (k & 7), a);
+  }
+}
+
+// Pass 2: dy = a*dz + b*y + c with the globally reduced sums (train), or
+// dy = scale*dz (eval: running statistics, no batch dependence).
+template <bool EVAL>
+__global__ __launch_bounds__(256) void stem_pool_bwd_elemt_kernel(
+    const bf16_t* __restrict__ dout, const uint8_t* __restrict__ arg, const bf16_t* __restrict__ y,
+    const float* __restrict__ params, const float* __restrict__ gamma, const float* __restrict__ red,
+    const float* __restrict__ count, float count_h, bf16_t* __restrict__ dy, int H, int W, int C, int P,
+    int Q) {
+  const int C8 = C >> 3;
+  const int row = blockIdx.y;  // n * H + h
+  const int n = row / H, h = row - (row / H) * H;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= W * C8) return;
+  const int w = j / C8, cc = j - (j / C8) * C8;
+  const int c0 = cc * 8;
+  float sc[8], sh[8], ca[8], cb[8], ccf[8];
+  ld8(params + 2 * C + c0, sc);
+  ld8(params + 3 * C + c0, sh);
+  if (EVAL) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      ca[k] = sc[k];
+      cb[k] = ccf[k] = 0.f;
+    }
+  } else {
+    const float inv_cnt = 1.f / (count ? count[0] : count_h);
+    float mean[8], inv[8], g[8], q0[8], q1[8];
+    ld8(params + c0, mean);
+    ld8(params + C + c0, inv);
+    ld8(gamma + c0, g);
+    ld8(red + c0, q0);
+    ld8(red + C + c0, q1);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float a = g[k] * inv[k];
+      const float mdy = q0[k] * inv_cnt, mdyx = q1[k] * inv_cnt;
+      ca[k] = a;
+      cb[k] = -a * inv[k] * mdyx;
+      ccf[k] = a * (mean[k] * inv[k] * mdyx - mdy);
+    }
+  }
+  const size_t i = (size_t)row * W * C8 + j;
+  float v[8], dz[8], o[8];
+  unpack8(reinterpret_cast<const uint4*>(y)[i], v);
+  stem_dz(dout, arg, n, h, w, cc, C8, P, Q, v, sc, sh, dz);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o[k] = EVAL ? ca[k] * dz[k] : ca[k] * dz[k] + cb[k] * v[k] + ccf[k];
+  reinterpret_cast<uint4*>(dy)[i] = pack8(o);
+}
+
+static int l2e(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return (1 << l) == v ? l : -1;
+}
+
+int stem_pool_fwd_launch(const bf16_t* y, const float* params, bf16_t* out, uint8_t* arg, int N, int H,
+                         int W, int C, int P, int Q, hipStream_t st) {
+  const int l = l2e(C / 8);
+  if (C % 8 || l < 0 || (C / 8) > 256 || N * P > 65535) return 1;
+  const dim3 grid((Q * (C / 8) + 255) / 256, N * P);
+  hipLaunchKernelGGL(stem_pool_fwd_kernel, grid, dim3(256), 0, st, y, params, out, arg, H, W, C, P, Q, l);
+  return 0;
+}
+
+int stem_pool_bwd_reduce_launch(const bf16_t* dout, const uint8_t* arg, const bf16_t* y,
+                                const float* params, float* red, int N, int H, int W, int C, int P, int Q,
+                                hipStream_t st) {
+  if (C % 8 || l2e(C / 8) < 0 || (C / 8) > 256) return 1;
+  const int rows = N * H;
+  int blocks = 1024;
+  int rpb = (rows + blocks - 1) / blocks;
+  blocks = (rows + rpb - 1) / rpb;
+  hipLaunchKernelGGL(stem_pool_bwd_reduce_kernel, dim3(blocks), dim3(256), 0, st, dout, arg, y, params, red,
+                     N, H, W, C, P, Q, rpb);
+  return 0;
+}
+
+int stem_pool_bwd_elemt_launch(const bf16_t* dout, const uint8_t* arg, const bf16_t* y, const float* params,
+                               const float* gamma, const float* red, const float* count, float count_h,
+                               bf16_t* dy, int N, int H, int W, int C, int P, int Q, bool eval_mode,
+                               hipStream_t st) {
+  if (C % 8 || l2e(C / 8) < 0 || N * H > 65535) return 1;
+  const dim3 grid((W * (C / 8) + 255) / 256, N * H);
+  if (eval_mode)
+    hipLaunchKernelGGL(stem_pool_bwd_elemt_kernel<true>, grid, dim3(256), 0, st, dout, arg, y, params, gamma,
+                       red, count, count_h, dy, H, W, C, P, Q);
+  else
+    hipLaunchKernelGGL(stem_pool_bwd_elemt_kernel<false>, grid, dim3(256), 0, st, dout, arg, y, params,
+                       gamma, red, count, count_h, dy, H, W, C, P, Q);
+  return 0;
+}
+
+}  // namespace pmd

@@ -201,9 +201,14 @@ class ResNet(nn.Module):
         if f8 is not None and self.training and torch.is_grad_enabled():
             f8.update()                          # delayed scaling: one device op per step
         with OF.weight_images(self._weight_set(x)):
-            out = OF.conv_bn_act(x, self.conv1, self.bn1, relu=True)
-            if self.stem == "imagenet":
-                out = OF.max_pool3x3s2(out)
+            if self.stem == "imagenet" and OF.fused_stem_enabled():
+                # conv1 -> BN -> ReLU -> 3x3/s2 max-pool; the activation is never stored
+                y, s = OF.conv(x, self.conv1, want_stats=self.bn1.training)
+                out = OF.bn_relu_maxpool(y, s, self.bn1)
+            else:
+                out = OF.conv_bn_act(x, self.conv1, self.bn1, relu=True)
+                if self.stem == "imagenet":
+                    out = OF.max_pool3x3s2(out)
             out = self.layer4(self.layer3(self.layer2(self.layer1(out))))
         out = OF.global_avg_pool(out)            # [N, C] fp32
         return OF.linear(out, self.linear)

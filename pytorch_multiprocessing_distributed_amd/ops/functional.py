@@ -46,6 +46,8 @@ _state = {"bn_sync": None, "force_torch": os.environ.get("PMD_PRIMS", "") == "to
           # fuse each BN-backward reduce into the dgrad epilogue that produces its input
           "fuse_bnred": os.environ.get("PMD_FUSE_BNRED", "1") != "0",
           "fused_site_hits": 0,
+          "fused_site_misses": 0,
+          "fused_stem": os.environ.get("PMD_FUSED_STEM", "1") != "0",
           "fp8": None,          # Fp8Scaling when the block convs run in fp8 (config 5)
           "wimg": None}         # WeightImageSet of the running forward (grouped weight prep)
 
@@ -266,11 +268,13 @@ def _bn_forward_params(P, y, st, bn, training, sync, y2=None, st2=None, bn2=None
 
 
 def _bn_backward(P, dout, mask, relu, training, sync, count, y1, p1, bn1, y2=None, p2=None,
-                 bn2=None, want_dzm=False, pre=None):
+                 bn2=None, want_dzm=False, pre=None, elemt_fn=None):
     """BN(+second BN)(+ReLU) backward. Returns (dy1, dy2, dzm, grads) with
     grads = [d_g1, d_b1, d_g2, d_b2] for params that were NOT written directly.
     ``pre``: the reduce results already produced by the dgrad that computed
-    ``dout`` (fused epilogue), in the order (bn1[, bn2])."""
+    ``dout`` (fused epilogue), in the order (bn1[, bn2]).  ``elemt_fn(red, count)``
+    replaces the elementwise pass of BN 1 (fused stem: it re-derives dz itself;
+    red/count are None in eval mode)."""
     if pre is not None:
         r1 = pre[0]
         r2 = pre[1] if y2 is not None else None
@@ -305,8 +309,11 @@ def _bn_backward(P, dout, mask, relu, training, sync, count, y1, p1, bn1, y2=Non
         _ready(bn1.bias, bn1.weight)
         if bn2 is not None:
             _ready(bn2.bias, bn2.weight)
-        dy1, dzm = P.bn_bwd_elemt(dout, mask, y1, p1, bn1.weight, red[:2 * c1].view(2, c1), count,
-                                  relu, want_dzm=want_dzm)
+        if elemt_fn is not None:
+            dy1, dzm = elemt_fn(red[:2 * c1].view(2, c1), count), None
+        else:
+            dy1, dzm = P.bn_bwd_elemt(dout, mask, y1, p1, bn1.weight, red[:2 * c1].view(2, c1), count,
+                                      relu, want_dzm=want_dzm)
         dy2 = None
         if y2 is not None:
             dy2, _ = P.bn_bwd_elemt(dout, mask, y2, p2, bn2.weight, red[2 * c1:].view(2, -1), count,
@@ -328,12 +335,17 @@ def _bn_backward(P, dout, mask, relu, training, sync, count, y1, p1, bn1, y2=Non
         if sync is not None:
             red = red.clone()
             sync.all_reduce_stats_(red)
-        dy1, dzm = P.bn_bwd_elemt(dout, mask, y1, p1, bn1.weight, red[:2 * c1].view(2, c1), count,
-                                  relu, want_dzm=want_dzm)
+        if elemt_fn is not None:
+            dy1, dzm = elemt_fn(red[:2 * c1].view(2, c1), count), None
+        else:
+            dy1, dzm = P.bn_bwd_elemt(dout, mask, y1, p1, bn1.weight, red[:2 * c1].view(2, c1),
+                                      count, relu, want_dzm=want_dzm)
         dy2 = None
         if y2 is not None:
             dy2, _ = P.bn_bwd_elemt(dout, mask, y2, p2, bn2.weight, red[2 * c1:].view(2, -1), count,
                                     relu)
+    elif elemt_fn is not None:
+        dy1, dy2, dzm = elemt_fn(None, None), None, None
     else:
         dy1, dzm = P.bn_bwd_elemt_eval(dout, mask, p1, relu, want_dzm=want_dzm)
         dy2 = P.bn_bwd_elemt_eval(dout, mask, p2, relu)[0] if y2 is not None else None
@@ -418,6 +430,57 @@ def conv_bn_act(x, conv_mod, bn, relu=True):
     return bn_add_act(y, s, bn, relu=relu)
 
 
+# ------------------------------------------------------------- stem tail
+class _StemPoolFn(torch.autograd.Function):
+    """ImageNet stem tail as one node: out = maxpool3x3s2(relu(BN(y))), y = conv1(x)
+    (reference resnet.py:97 + the ImageNet max-pool).  On the gfx950 path the
+    activation is never materialised: one kernel forward (kernels/stem.hip),
+    and the backward recomputes dz = pool-gradient * ReLU-mask from y in its
+    reduce and elementwise passes."""
+
+    @staticmethod
+    def forward(ctx, cfg, y, st, g, b):
+        bn, training = cfg
+        P = prims_for(y)
+        sync = _state["bn_sync"] if training else None
+        p, _, count = _bn_forward_params(P, y, st, bn, training, sync)
+        out, arg = P.stem_pool_fwd(y, p)
+        ctx.cfg = (bn, training, sync, count)
+        ctx.arg = arg
+        ctx.save_for_backward(y, p)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        bn, training, sync, count = ctx.cfg
+        y, p = ctx.saved_tensors
+        arg = ctx.arg
+        P = prims_for(y)
+        dout = dout.contiguous()
+        red = P.stem_pool_bwd_reduce(dout, arg, y, p)
+
+        def elemt(r, cnt):
+            return P.stem_pool_bwd_elemt(dout, arg, y, p, bn.weight, r, cnt, eval_mode=not training)
+        dy, _, _, g = _bn_backward(P, dout, None, True, training, sync, count, y, p, bn, pre=[red],
+                                   elemt_fn=elemt)
+        ctx.arg = None
+        return None, dy, None, g[0], g[1]
+
+
+def fused_stem_enabled():
+    return _state["fused_stem"]
+
+
+def set_fused_stem(flag: bool):
+    """ImageNet stem tail as one fused node (default) or conv_bn_act + max-pool."""
+    _state["fused_stem"] = bool(flag)
+
+
+def bn_relu_maxpool(y, stats, bn):
+    """maxpool3x3s2(relu(BN(y))) for the ImageNet stem (fused on the gfx950 path)."""
+    return _StemPoolFn.apply((bn, bn.training), y, stats, bn.weight, bn.bias)
+
+
 # ------------------------------------------------------------ residual block
 class _BnSite:
     """Hand-off between two consecutive residual blocks for the fused BN reduce:
@@ -448,8 +511,11 @@ class _BnSite:
         if dout.data_ptr() == self.dx_ptr and tuple(dout.shape) == self.dx_shape:
             _state["fused_site_hits"] += 1
             return red
+        _state["fused_site_misses"] += 1
         rel = getattr(P, "_release", None)
         if rel is not None:
+            for b in red:          # the pool hands out zeroed slot buffers only
+                b.zero_()
             rel(*red)
         return None
 

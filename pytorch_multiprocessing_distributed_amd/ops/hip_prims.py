@@ -166,6 +166,23 @@ def maxpool_bwd(dout, arg, x_shape):
     return _C.maxpool_bwd(dout, arg, int(x_shape[1]), int(x_shape[2]))
 
 
+def stem_pool_fwd(y, p):
+    """BN + ReLU + 3x3/s2 max-pool of the conv1 output in one pass -> (out, argmax taps)."""
+    return tuple(_C.stem_pool_fwd(y, p))
+
+
+def stem_pool_bwd_reduce(dout, arg, y, p):
+    buf = _acquire(y.shape[-1], y.device)
+    return _C.stem_pool_bwd_reduce(dout, arg, y, p, buf)
+
+
+def stem_pool_bwd_elemt(dout, arg, y, p, gamma, red, count, eval_mode=False):
+    if torch.is_tensor(count):
+        return _C.stem_pool_bwd_elemt(dout, arg, y, p, gamma.detach(), red, count, 0.0, bool(eval_mode))
+    return _C.stem_pool_bwd_elemt(dout, arg, y, p, gamma.detach(), red, None,
+                                  float(count or 1.0), bool(eval_mode))
+
+
 def avgpool_fwd(x):
     return _C.avgpool_fwd(x)
 

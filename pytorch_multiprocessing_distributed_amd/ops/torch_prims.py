@@ -192,6 +192,28 @@ def maxpool_bwd(dout, x, x_shape):
     return _nhwc(dx).to(dout.dtype)
 
 
+def stem_pool_fwd(y, p):
+    """Composite reference of the fused stem tail: bn_apply(+ReLU) then max-pool.
+    The auxiliary output carries (activation, ReLU mask) for the backward."""
+    a, mask = bn_apply(y, p, relu=True)
+    out, _ = maxpool_fwd(a)
+    return out, (a, mask)
+
+
+def stem_pool_bwd_reduce(dout, arg, y, p):
+    a, mask = arg
+    da = maxpool_bwd(dout, a, tuple(a.shape))
+    return bn_bwd_reduce(da, mask, y, p, True)
+
+
+def stem_pool_bwd_elemt(dout, arg, y, p, gamma, red, count, eval_mode=False):
+    a, mask = arg
+    da = maxpool_bwd(dout, a, tuple(a.shape))
+    if eval_mode:
+        return bn_bwd_elemt_eval(da, mask, p, True)[0]
+    return bn_bwd_elemt(da, mask, y, p, gamma, red, count, True)[0]
+
+
 def avgpool_fwd(x):
     return _f(x).mean(dim=(1, 2))
 

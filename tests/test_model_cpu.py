@@ -75,12 +75,14 @@ def test_fused_matches_stock_train_step(name, stem, hw):
                                    atol=1e-8)
 
 
-def test_eval_mode_backward_matches_stock():
+@pytest.mark.parametrize("name,stem,hw", [("res", "cifar", 32), ("resnet50", "imagenet", 64)])
+def test_eval_mode_backward_matches_stock(name, stem, hw):
     torch.manual_seed(1)
-    f = build_model("res").double().eval()
-    s = build_model("res", impl="stock").double().eval()
+    nc = 1000 if stem == "imagenet" else 10
+    f = build_model(name, num_classes=nc, stem=stem).double().eval()
+    s = build_model(name, num_classes=nc, stem=stem, impl="stock").double().eval()
     _copy_into_stock(f, s)
-    x = torch.randn(2, 3, 32, 32, dtype=torch.float64)
+    x = torch.randn(2, 3, hw, hw, dtype=torch.float64)
     f(x.permute(0, 2, 3, 1).contiguous()).sum().backward()
     s(x).sum().backward()
     for (n, pf), ps in zip(f.named_parameters(), s.parameters()):
