@@ -45,16 +45,25 @@ __global__ __launch_bounds__(256) void stem_pool_fwd_kernel(const bf16_t* __rest
     bi[k] = 0;
   }
   const bf16_t* yb = y + (size_t)n * H * W * C + cc * 8;
+  // branch-free taps: out-of-range taps load a clamped (valid) pixel and are
+  // masked out, so all 9 loads are independent and can be in flight together
+  uint4 raw[9];
+  bool ok[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
     const int ih = p * 2 - 1 + t / 3, iw = q * 2 - 1 + t % 3;
-    if ((unsigned)ih >= (unsigned)H || (unsigned)iw >= (unsigned)W) continue;
+    ok[t] = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+    const int ch = min(max(ih, 0), H - 1), cw = min(max(iw, 0), W - 1);
+    raw[t] = *reinterpret_cast<const uint4*>(yb + ((size_t)ch * W + cw) * C);
+  }
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
     float v[8];
-    unpack8(*reinterpret_cast<const uint4*>(yb + ((size_t)ih * W + iw) * C), v);
+    unpack8(raw[t], v);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const float a = round_bf(fmaxf(v[k] * sc[k] + sh[k], 0.f));
-      if (a > best[k]) {
+      if (ok[t] && a > best[k]) {
         best[k] = a;
         bi[k] = t;
       }
@@ -77,24 +86,32 @@ __device__ __forceinline__ void stem_dz(const bf16_t* __restrict__ dout, const u
   float acc[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-  const int p_lo = h > 0 ? h >> 1 : 0;
-  const int p_hi = min((h + 1) >> 1, P - 1);
-  const int q_lo = w > 0 ? w >> 1 : 0;
-  const int q_hi = min((w + 1) >> 1, Q - 1);
-  for (int p = p_lo; p <= p_hi; ++p)
-    for (int q = q_lo; q <= q_hi; ++q) {
-      const int dh = h - (p * 2 - 1), dw = w - (q * 2 - 1);
-      if (dh < 0 || dh > 2 || dw < 0 || dw > 2) continue;
-      const int tap = dh * 3 + dw;
-      const size_t o = (((size_t)n * P + p) * Q + q) * C8 + cc;
-      const uint2 a = reinterpret_cast<const uint2*>(arg)[o];
-      float g[8];
-      unpack8(reinterpret_cast<const uint4*>(dout)[o], g);
-      const uint32_t aw[2] = {a.x, a.y};
+  // windows p with 2p-1 <= h <= 2p+1: p in {h>>1, (h+1)>>1} (one or two of them);
+  // always visit the 2x2 candidates with clamped indices and mask the invalid
+  // ones, so the (up to) 4 gathers are independent loads
+  const int pa = h >> 1, qa = w >> 1;
+  uint2 av[4];
+  uint4 gv[4];
+  int tp[4];
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if ((int)((aw[k >> 2] >> ((k & 3) * 8)) & 0xff) == tap) acc[k] += g[k];
-    }
+  for (int u = 0; u < 4; ++u) {
+    const int p = pa + (u >> 1), q = qa + (u & 1);
+    const int dh = h - (p * 2 - 1), dw = w - (q * 2 - 1);
+    const bool ok = p < P && q < Q && dh >= 0 && dh <= 2 && dw >= 0 && dw <= 2;
+    tp[u] = ok ? dh * 3 + dw : -1;
+    const size_t o = (((size_t)n * P + min(p, P - 1)) * Q + min(q, Q - 1)) * C8 + cc;
+    av[u] = reinterpret_cast<const uint2*>(arg)[o];
+    gv[u] = reinterpret_cast<const uint4*>(dout)[o];
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    float g[8];
+    unpack8(gv[u], g);
+    const uint32_t aw[2] = {av[u].x, av[u].y};
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if ((int)((aw[k >> 2] >> ((k & 3) * 8)) & 0xff) == tp[u]) acc[k] += g[k];
+  }
 #pragma unroll
   for (int k = 0; k < 8; ++k) dz[k] = (v[k] * sc[k] + sh[k] > 0.f) ? round_bf(acc[k]) : 0.f;
 }
@@ -106,7 +123,7 @@ __device__ __forceinline__ void stem_dz(const bf16_t* __restrict__ dout, const u
 __global__ __launch_bounds__(256) void stem_pool_bwd_reduce_kernel(
     const bf16_t* __restrict__ dout, const uint8_t* __restrict__ arg, const bf16_t* __restrict__ y,
     const float* __restrict__ params, float* __restrict__ red, int N, int H, int W, int C, int P, int Q,
-    int rows_per_block) {
+    int rows_per_block, int log2C8) {
   __shared__ float part[256 * 17];
   const int C8 = C >> 3;
   const int tid = threadIdx.x;
@@ -124,7 +141,7 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_reduce_kernel(
   for (int row = r0; row < r1; ++row) {
     const int n = row / H, h = row - (row / H) * H;
     for (int j = tid; j < W * C8; j += 256) {
-      const int w = j / C8;
+      const int w = j >> log2C8;
       float v[8], dz[8];
       unpack8(reinterpret_cast<const uint4*>(y)[(size_t)row * W * C8 + j], v);
       stem_dz(dout, arg, n, h, w, cc, C8, P, Q, v, sc, sh, dz);
@@ -156,14 +173,13 @@ template <bool EVAL>
 __global__ __launch_bounds__(256) void stem_pool_bwd_elemt_kernel(
     const bf16_t* __restrict__ dout, const uint8_t* __restrict__ arg, const bf16_t* __restrict__ y,
     const float* __restrict__ params, const float* __restrict__ gamma, const float* __restrict__ red,
-    const float* __restrict__ count, float count_h, bf16_t* __restrict__ dy, int H, int W, int C, int P,
-    int Q) {
+    const float* __restrict__ count, float count_h, bf16_t* __restrict__ dy, int N, int H, int W, int C,
+    int P, int Q, int rows_per_block, int log2C8) {
+  // same traversal as the reduce: a run of input rows per block, channel chunk
+  // tid % C8 fixed per thread, so the per-channel coefficients are computed once
   const int C8 = C >> 3;
-  const int row = blockIdx.y;  // n * H + h
-  const int n = row / H, h = row - (row / H) * H;
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= W * C8) return;
-  const int w = j / C8, cc = j - (j / C8) * C8;
+  const int tid = threadIdx.x;
+  const int cc = tid & (C8 - 1);
   const int c0 = cc * 8;
   float sc[8], sh[8], ca[8], cb[8], ccf[8];
   ld8(params + 2 * C + c0, sc);
@@ -191,13 +207,21 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_elemt_kernel(
       ccf[k] = a * (mean[k] * inv[k] * mdyx - mdy);
     }
   }
-  const size_t i = (size_t)row * W * C8 + j;
-  float v[8], dz[8], o[8];
-  unpack8(reinterpret_cast<const uint4*>(y)[i], v);
-  stem_dz(dout, arg, n, h, w, cc, C8, P, Q, v, sc, sh, dz);
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(r0 + rows_per_block, N * H);
+  for (int row = r0; row < r1; ++row) {
+    const int n = row / H, h = row - (row / H) * H;
+    for (int j = tid; j < W * C8; j += 256) {
+      const int w = j >> log2C8;
+      const size_t i = (size_t)row * W * C8 + j;
+      float v[8], dz[8], o[8];
+      unpack8(reinterpret_cast<const uint4*>(y)[i], v);
+      stem_dz(dout, arg, n, h, w, cc, C8, P, Q, v, sc, sh, dz);
 #pragma unroll
-  for (int k = 0; k < 8; ++k) o[k] = EVAL ? ca[k] * dz[k] : ca[k] * dz[k] + cb[k] * v[k] + ccf[k];
-  reinterpret_cast<uint4*>(dy)[i] = pack8(o);
+      for (int k = 0; k < 8; ++k) o[k] = EVAL ? ca[k] * dz[k] : ca[k] * dz[k] + cb[k] * v[k] + ccf[k];
+      reinterpret_cast<uint4*>(dy)[i] = pack8(o);
+    }
+  }
 }
 
 static int l2e(int v) {
@@ -218,13 +242,14 @@ int stem_pool_fwd_launch(const bf16_t* y, const float* params, bf16_t* out, uint
 int stem_pool_bwd_reduce_launch(const bf16_t* dout, const uint8_t* arg, const bf16_t* y,
                                 const float* params, float* red, int N, int H, int W, int C, int P, int Q,
                                 hipStream_t st) {
-  if (C % 8 || l2e(C / 8) < 0 || (C / 8) > 256) return 1;
-  const int rows = N * H;
-  int blocks = 1024;
-  int rpb = (rows + blocks - 1) / blocks;
-  blocks = (rows + rpb - 1) / rpb;
+  const int l = l2e(C / 8);
+  if (C % 8 || l < 0 || (C / 8) > 256) return 1;
+  // ~4 input rows per block: thousands of blocks keep many rows' gathers in
+  // flight (the per-block atomics stay far below the streaming cost)
+  const int rpb = 4;
+  const int blocks = (N * H + rpb - 1) / rpb;
   hipLaunchKernelGGL(stem_pool_bwd_reduce_kernel, dim3(blocks), dim3(256), 0, st, dout, arg, y, params, red,
-                     N, H, W, C, P, Q, rpb);
+                     N, H, W, C, P, Q, rpb, l);
   return 0;
 }
 
@@ -232,14 +257,16 @@ int stem_pool_bwd_elemt_launch(const bf16_t* dout, const uint8_t* arg, const bf1
                                const float* gamma, const float* red, const float* count, float count_h,
                                bf16_t* dy, int N, int H, int W, int C, int P, int Q, bool eval_mode,
                                hipStream_t st) {
-  if (C % 8 || l2e(C / 8) < 0 || N * H > 65535) return 1;
-  const dim3 grid((W * (C / 8) + 255) / 256, N * H);
+  const int l = l2e(C / 8);
+  if (C % 8 || l < 0 || (C / 8) > 256) return 1;
+  const int rpb = 4;
+  const dim3 grid((N * H + rpb - 1) / rpb);
   if (eval_mode)
     hipLaunchKernelGGL(stem_pool_bwd_elemt_kernel<true>, grid, dim3(256), 0, st, dout, arg, y, params, gamma,
-                       red, count, count_h, dy, H, W, C, P, Q);
+                       red, count, count_h, dy, N, H, W, C, P, Q, rpb, l);
   else
     hipLaunchKernelGGL(stem_pool_bwd_elemt_kernel<false>, grid, dim3(256), 0, st, dout, arg, y, params,
-                       gamma, red, count, count_h, dy, H, W, C, P, Q);
+                       gamma, red, count, count_h, dy, N, H, W, C, P, Q, rpb, l);
   return 0;
 }
 
