@@ -216,46 +216,64 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
   uint4 ra[DMA ? 1 : PA], rb[DMA ? 1 : PB];
   const int nk = (Kgp + BK - 1) / BK;
 
+  // Tap state of the NEXT K-tile the uniform loader issues.  K-tiles are issued
+  // strictly in order (prologue 0..NST-2, then kt+NST-1), and with Cs >= BK a
+  // K-tile lies inside one filter tap, so (channel block, tap row, tap col) is
+  // advanced incrementally in scalar registers -- no per-tile integer division.
+  int u_cb = 0, u_tr = 0, u_ts = 0, u_kt = 0;
+  // per-row source pointers at tap (0,0) channel 0 (+ this lane's chunk); a tile
+  // then only adds the wave-uniform offset (dr*W + ds)*Cs + cb
+  const bf16_t* a_ptr[PA];
+  const int lane_ci = (lane % CH ^ swz<BK>(lane / CH)) * 8;
+#pragma unroll
+  for (int i = 0; i < PA; ++i) {
+    const int ci = MF32 ? lane_c32[i & 1] : lane_ci;
+    // signed: u_p is -1.. at padded borders (never dereferenced there: `ok` masks it)
+    a_ptr[i] = a.src + ((long long)u_p[i] << a.log2Cs) + ci;
+  }
   auto load_tile_uni = [&](int kt, int dbuf) {
-    const int k0 = kt * BK;                       // all scalar until lane_c
-    const bool kok = k0 < Kgp;
-    const int tap = k0 >> a.log2Cs;
-    const int tr = tap / ns;
-    const int ts = tap - tr * ns;
-    const int r = r0 + rstep * tr, sx = s0 + rstep * ts;
+    (void)kt;
+    const bool kok = u_kt < nk;
+    const int r = r0 + rstep * u_tr, sx = s0 + rstep * u_ts;
     int dr, ds;
     if (!DGRAD) {
       dr = r;
       ds = sx;
     } else if (a.stride == 2) {
-      dr = -tr;
-      ds = -ts;
+      dr = -u_tr;
+      ds = -u_ts;
     } else {
       dr = -r;
       ds = -sx;
     }
-    const int dpix = dr * a.W + ds;
-    const int cb = k0 & (a.Cs - 1);
-    const int c = cb + lane_c;
-    const int tapo = (r * a.S + sx) << a.log2Cs;
+    const long long aoff = ((long long)(dr * a.W + ds) << a.log2Cs) + u_cb;  // scalar
+    const int tapo = ((r * a.S + sx) << a.log2Cs) + u_cb;
 #pragma unroll
     for (int i = 0; i < PA; ++i) {
       const bool ok = kok && a_ok[i] && (unsigned)(u_h[i] + dr) < (unsigned)a.H &&
                       (unsigned)(u_w[i] + ds) < (unsigned)a.W;
-      const int ci = MF32 ? cb + lane_c32[i & 1] : c;
-      const bf16_t* real = a.src + ((size_t)(unsigned)(u_p[i] + dpix) << a.log2Cs) + ci;
-      const void* src = ok ? (const void*)real : (const void*)g_zero16;
+      const void* src = ok ? (const void*)(a_ptr[i] + aoff) : (const void*)g_zero16;
       bf16_t* dst = lds + dbuf * STAGE + (wid_s * (BM / NW) + RPI * i) * LDR;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
-      const int boff = tapo + (MF32 ? cb + lane_c32[i & 1] : c);
+      const int boff = tapo + (MF32 ? lane_c32[i & 1] : lane_ci);
       const void* src = (b_ok[i] && kok) ? (const void*)(b_row[i] + boff) : (const void*)g_zero16;
       bf16_t* dst = lds + dbuf * STAGE + A_ELEMS + (wid_s * (BN / NW) + RPI * i) * LDR;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+    // advance to the next K-tile: channel block, then tap column, then tap row
+    ++u_kt;
+    u_cb += BK;
+    if (u_cb == a.Cs) {
+      u_cb = 0;
+      if (++u_ts == ns) {
+        u_ts = 0;
+        ++u_tr;
+      }
     }
   };
 
@@ -393,10 +411,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
   };
 
   if constexpr (DMA) {
-    auto load = [&](int kt, int buf) {
-      if (uni) load_tile_uni(kt, buf);
-      else load_tile(kt, buf);
-    };
+    // the loader choice is hoisted out of the K loop: one loop instance per loader
+    auto pipeline = [&](auto&& load) {
     // prologue: tiles 0 .. NST-2 in flight
 #pragma unroll
     for (int t = 0; t < NST - 1; ++t)
@@ -420,6 +436,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
       if (kt + NST - 1 < nk) load(kt + NST - 1, (kt + NST - 1) % NST);
       compute(kt % NST);
     }
+    };
+    if (uni) pipeline(load_tile_uni);
+    else pipeline(load_tile);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   } else {
     if (nk > 0) {
