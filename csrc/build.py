@@ -58,7 +58,8 @@ def build(force=False, jobs=None, debug=False, verbose=True):
     headers = glob.glob(os.path.join(CSRC, "kernels", "*.h"))
     opt = ["-O1", "-g"] if debug else ["-O3"]
     common = [HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", *opt,
-              "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1"]
+              "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+              *os.environ.get("PMD_EXTRA_CFLAGS", "").split()]  # A/B variant macros
     jobs_ = []
     objs = []
     for src in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))):

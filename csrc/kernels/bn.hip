@@ -18,6 +18,10 @@
 // per-channel coefficients are loaded once per thread.
 #include "common.h"
 
+#ifndef PMD_EW_U
+#define PMD_EW_U 1
+#endif
+
 namespace pmd {
 
 __device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
@@ -86,39 +90,58 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
     load8f(p2 + 2 * C + c0, s2);
     load8f(p2 + 3 * C + c0, b2);
   }
-  for (long long i = start; i < nchunk; i += step) {
-    float v[8], w[8];
-    unpack8(reinterpret_cast<const uint4*>(y1)[i], v);
-    if (MODE >= 1) unpack8(reinterpret_cast<const uint4*>(r)[i], w);
-    uint32_t bits = 0;
+  // U chunks per thread per trip, all loads issued before any store.  Measured
+  // (bench/ab_so.sh, full R50 step): U=2 is 0.4% SLOWER than U=1 -- the
+  // 2048x256-thread grid at full occupancy already covers HBM latency -- so the
+  // default stays 1; the knob is kept for A/B builds (PMD_EXTRA_CFLAGS).
+  constexpr int U = PMD_EW_U;
+  for (long long i0 = start; i0 < nchunk; i0 += U * step) {
+    uint4 yv[U], rv[U];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float o = v[k] * s1[k] + b1[k];
-      if (MODE == 1) o += w[k];
-      if (MODE == 2) o += w[k] * s2[k] + b2[k];
-      if (RELU) {
-        bits |= (uint32_t)(o > 0.f) << k;
-        o = fmaxf(o, 0.f);
+    for (int u = 0; u < U; ++u) {
+      const long long i = i0 + u * step;
+      if (i < nchunk) {
+        yv[u] = reinterpret_cast<const uint4*>(y1)[i];
+        if (MODE >= 1) rv[u] = reinterpret_cast<const uint4*>(r)[i];
       }
-      v[k] = o;
     }
-    const uint4 pk = pack8(v);
-    reinterpret_cast<uint4*>(out)[i] = pk;
-    if (RELU && mask_out) mask_out[i] = (uint8_t)bits;
-    if (Q8) {
-      float o[8];
-      unpack8(pk, o);  // quantise the bf16 value the bf16 consumers see
-      // the convert does not saturate (|v| > 448 -> NaN code): clamp with v_med3
-      float c[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) c[k] = __builtin_amdgcn_fmed3f(o[k] * qs, -448.f, 448.f);
-      int w0 = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
-      w0 = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], w0, true);
-      int w1 = __builtin_amdgcn_cvt_pk_fp8_f32(c[4], c[5], 0, false);
-      w1 = __builtin_amdgcn_cvt_pk_fp8_f32(c[6], c[7], w1, true);
-      reinterpret_cast<uint2*>(q_out)[i] = make_uint2((uint32_t)w0, (uint32_t)w1);
+    for (int u = 0; u < U; ++u) {
+      const long long i = i0 + u * step;
+      if (i >= nchunk) break;
+      float v[8], w[8];
+      unpack8(yv[u], v);
+      if (MODE >= 1) unpack8(rv[u], w);
+      uint32_t bits = 0;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) qm = fmaxf(qm, fabsf(o[k]));
+      for (int k = 0; k < 8; ++k) {
+        float o = v[k] * s1[k] + b1[k];
+        if (MODE == 1) o += w[k];
+        if (MODE == 2) o += w[k] * s2[k] + b2[k];
+        if (RELU) {
+          bits |= (uint32_t)(o > 0.f) << k;
+          o = fmaxf(o, 0.f);
+        }
+        v[k] = o;
+      }
+      const uint4 pk = pack8(v);
+      reinterpret_cast<uint4*>(out)[i] = pk;
+      if (RELU && mask_out) mask_out[i] = (uint8_t)bits;
+      if (Q8) {
+        float o[8];
+        unpack8(pk, o);  // quantise the bf16 value the bf16 consumers see
+        // the convert does not saturate (|v| > 448 -> NaN code): clamp with v_med3
+        float c[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) c[k] = __builtin_amdgcn_fmed3f(o[k] * qs, -448.f, 448.f);
+        int w0 = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
+        w0 = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], w0, true);
+        int w1 = __builtin_amdgcn_cvt_pk_fp8_f32(c[4], c[5], 0, false);
+        w1 = __builtin_amdgcn_cvt_pk_fp8_f32(c[6], c[7], w1, true);
+        reinterpret_cast<uint2*>(q_out)[i] = make_uint2((uint32_t)w0, (uint32_t)w1);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) qm = fmaxf(qm, fabsf(o[k]));
+      }
     }
   }
   if (Q8) block_amax_update(qamax, qm);
@@ -243,19 +266,36 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(
       cc[k] = a * (mean[k] * inv[k] * mdyx - mdy);
     }
   }
-  for (long long i = start; i < nchunk; i += step) {
-    float d[8], o[8], v[8];
-    unpack8(reinterpret_cast<const uint4*>(dout)[i], d);
-    const uint32_t mb = RELU ? mask[i] : 0xffu;
-    if (!EVAL) unpack8(reinterpret_cast<const uint4*>(y)[i], v);
+  constexpr int U = PMD_EW_U;  // chunks in flight per thread (see bn_apply_kernel)
+  for (long long i0 = start; i0 < nchunk; i0 += U * step) {
+    uint4 dv[U], yv[U];
+    uint32_t mv[U];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float dz = ((mb >> k) & 1u) ? d[k] : 0.f;
-      d[k] = dz;
-      o[k] = EVAL ? ca[k] * dz : ca[k] * dz + cb[k] * v[k] + cc[k];
+    for (int u = 0; u < U; ++u) {
+      const long long i = i0 + u * step;
+      if (i < nchunk) {
+        dv[u] = reinterpret_cast<const uint4*>(dout)[i];
+        mv[u] = RELU ? mask[i] : 0xffu;
+        if (!EVAL) yv[u] = reinterpret_cast<const uint4*>(y)[i];
+      }
     }
-    reinterpret_cast<uint4*>(dy)[i] = pack8(o);
-    if (DZM) reinterpret_cast<uint4*>(dzm_out)[i] = pack8(d);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = i0 + u * step;
+      if (i >= nchunk) break;
+      float d[8], o[8], v[8];
+      unpack8(dv[u], d);
+      const uint32_t mb = mv[u];
+      if (!EVAL) unpack8(yv[u], v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float dz = ((mb >> k) & 1u) ? d[k] : 0.f;
+        d[k] = dz;
+        o[k] = EVAL ? ca[k] * dz : ca[k] * dz + cb[k] * v[k] + cc[k];
+      }
+      reinterpret_cast<uint4*>(dy)[i] = pack8(o);
+      if (DZM) reinterpret_cast<uint4*>(dzm_out)[i] = pack8(d);
+    }
   }
 }
 

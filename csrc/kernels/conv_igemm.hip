@@ -565,42 +565,74 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
           }
     }
   }
-  for (int idx = tid; idx < BM * CPR; idx += NT) {
-    const int row = idx / CPR, cc = idx % CPR;
-    const int m = m0 + row, n = n0 + cc * 8;
-    if (m < Mp && n < a.Nout) {
-      size_t orow = m;
-      if (DGRAD && a.stride == 2) {
+  // Output rows in groups of G per thread: every global load of a group (addend,
+  // masks, BN inputs) is issued before the group's first store (the stores may
+  // alias nothing the group reads), so a thread has G x (1-3) HBM reads in
+  // flight instead of one dependent load->store chain per row.  Full-step A/B
+  // (bench/ab_so.sh): G=2 +0.6% over the serial loop, G=4 -3.6% (the 4-deep
+  // register tile of activation chunks costs more than the extra latency hiding).
+  constexpr int ITERS = BM * CPR / NT;
+  static_assert((BM * CPR) % NT == 0, "whole epilogue iterations");
+#ifndef PMD_EPI_G
+#define PMD_EPI_G 2
+#endif
+  constexpr int G = ITERS < PMD_EPI_G ? ITERS : PMD_EPI_G;
+  static_assert(ITERS % G == 0, "epilogue groups");
+  const bool has_add = DGRAD && a.addend, has_amask = DGRAD && a.addend_mask;
+  for (int it0 = 0; it0 < ITERS; it0 += G) {
+    size_t orow[G];
+    bool ok[G];
+    uint4 v[G], ad[G], yy[2][G];
+    uint32_t am[G], mb[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int idx = tid + (it0 + g) * NT;
+      const int row = idx / CPR, cc = idx % CPR;
+      const int m = m0 + row, n = n0 + cc * 8;
+      ok[g] = m < Mp && n < a.Nout;
+      orow[g] = ok[g] ? m : 0;
+      if (DGRAD && a.stride == 2 && ok[g]) {
         const int nb = m / ohw, rem = m - nb * ohw;
         const int hh = rem / OWp, ww = rem - hh * OWp;
-        orow = ((size_t)nb * a.OH + 2 * hh + ph) * a.OW + 2 * ww + pw;
+        orow[g] = ((size_t)nb * a.OH + 2 * hh + ph) * a.OW + 2 * ww + pw;
       }
-      uint4 v = *reinterpret_cast<const uint4*>(Cs + row * LDC + cc * 8);
-      if (a.addend) {
-        float f[8], g[8];
-        unpack8(v, f);
-        unpack8(*reinterpret_cast<const uint4*>(a.addend + orow * a.Nout + n), g);
-        if (a.addend_mask) {
-          const uint32_t am = a.addend_mask[orow * (a.Nout >> 3) + (n >> 3)];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) g[e] = ((am >> e) & 1u) ? g[e] : 0.f;
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] += g[e];
-        v = pack8(f);
+      v[g] = *reinterpret_cast<const uint4*>(Cs + row * LDC + cc * 8);
+      const size_t off = orow[g] * a.Nout + (ok[g] ? n : 0);
+      if (has_add && ok[g]) {
+        ad[g] = *reinterpret_cast<const uint4*>(a.addend + off);
+        am[g] = has_amask ? a.addend_mask[off >> 3] : 0xffu;
       }
-      *reinterpret_cast<uint4*>(a.out + orow * a.Nout + n) = v;
+      if (nbn && ok[g]) {
+        mb[g] = a.bn_mask ? a.bn_mask[off >> 3] : 0xffu;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          if (t < nbn) yy[t][g] = *reinterpret_cast<const uint4*>(a.bn_y[t] + off);
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (!ok[g]) continue;
+      const int n = n0 + ((tid + (it0 + g) * NT) % CPR) * 8;
+      uint4 o = v[g];
+      if (has_add) {
+        float f[8], ga[8];
+        unpack8(o, f);
+        unpack8(ad[g], ga);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] += ((am[g] >> e) & 1u) ? ga[e] : 0.f;
+        o = pack8(f);
+      }
+      *reinterpret_cast<uint4*>(a.out + orow[g] * a.Nout + n) = o;
       if (nbn) {
         float d[8];
-        unpack8(v, d);
-        const uint32_t mb = a.bn_mask ? a.bn_mask[orow * (a.Nout >> 3) + (n >> 3)] : 0xffu;
+        unpack8(o, d);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) d[e] = ((mb >> e) & 1u) ? d[e] : 0.f;
+        for (int e = 0; e < 8; ++e) d[e] = ((mb[g] >> e) & 1u) ? d[e] : 0.f;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           if (t < nbn) {
             float yv[8];
-            unpack8(*reinterpret_cast<const uint4*>(a.bn_y[t] + orow * a.Nout + n), yv);
+            unpack8(yy[t][g], yv);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               bsum[t][e] += d[e];
