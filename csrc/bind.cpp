@@ -84,6 +84,56 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor wk, int64_t stride, int64_t pad, b
   return {y};
 }
 
+// ------------------------------------------------------------- winograd
+// F(2x2,3x3) for stride-1 pad-1 3x3 convs: U = filter transform of the forward
+// weight image wk [K,3,3,Cp] (flip: the dgrad filter, [16,Cp,K]); the 16 GEMMs
+// between the input and output transforms are torch.bmm (hipBLASLt).
+Tensor winograd_filter(Tensor wk, bool flip) {
+  CHECK_DEV(wk); CHECK_BF16(wk); CHECK_CONT(wk);
+  TORCH_CHECK(wk.dim() == 4 && wk.size(1) == 3 && wk.size(2) == 3, "wk must be [K,3,3,Cp]");
+  const int K = wk.size(0), Cp = wk.size(3);
+  c10::DeviceGuard g(wk.device());
+  Tensor U = flip ? torch::empty({16, Cp, K}, wk.options()) : torch::empty({16, K, Cp}, wk.options());
+  CHECK_RC(pmd::winograd_filter_launch(bfp(wk), bfp_mut(U), K, Cp, flip, cur_stream()), "winograd_filter");
+  return U;
+}
+
+Tensor winograd_input(Tensor x) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONT(x);
+  TORCH_CHECK(x.dim() == 4, "x must be [N,H,W,C]");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int64_t T = (int64_t)N * ((H + 1) / 2) * ((W + 1) / 2);
+  c10::DeviceGuard g(x.device());
+  Tensor V = torch::empty({16, T, C}, x.options());
+  CHECK_RC(pmd::winograd_input_launch(bfp(x), bfp_mut(V), N, H, W, C, cur_stream()), "winograd_input");
+  return V;
+}
+
+std::vector<Tensor> winograd_output(Tensor M, int64_t N, int64_t H, int64_t W, bool want_stats,
+                                    c10::optional<Tensor> stats_buf) {
+  CHECK_DEV(M); CHECK_BF16(M); CHECK_CONT(M);
+  const int64_t T = N * ((H + 1) / 2) * ((W + 1) / 2);
+  TORCH_CHECK(M.dim() == 3 && M.size(0) == 16 && M.size(1) == T, "M must be [16, tiles, K]");
+  const int K = M.size(2);
+  c10::DeviceGuard g(M.device());
+  Tensor y = torch::empty({N, H, W, K}, M.options());
+  Tensor stats;
+  if (want_stats) {
+    if (stats_buf && stats_buf->defined()) {
+      TORCH_CHECK(stats_buf->numel() == pmd_slots() * 2 * K, "stats buffer must be [S,2,K]");
+      opt_f32(stats_buf, "stats_buf");
+      stats = *stats_buf;
+    } else {
+      stats = torch::zeros({pmd_slots(), 2, K}, M.options().dtype(torch::kFloat32));
+    }
+  }
+  CHECK_RC(pmd::winograd_output_launch(bfp(M), bfp_mut(y), want_stats ? stats.data_ptr<float>() : nullptr,
+                                       (int)N, (int)H, (int)W, K, cur_stream()),
+           "winograd_output");
+  if (want_stats) return {y, stats};
+  return {y};
+}
+
 // dx[N,H,W,Cp] from dy[N,P,Q,K] and wkt[Cp,R,S,K]
 // addend: optional [N,H,W,Cp] bf16 added in the epilogue (dx = dgrad + addend)
 // bn_*: optional fused BN-backward reduce of the output (see pmd::BnReduceArgs);
@@ -629,6 +679,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad_set_impl", &pmd::conv_wgrad_set_impl,
         "wgrad staging variant: 0 registers, 1 LDS-DMA 64x2 (default), 2 LDS-DMA 32x4, 3 LDS-DMA 64x3");
   m.def("conv_fwd", &conv_fwd);
+  m.def("winograd_filter", &winograd_filter);
+  m.def("winograd_input", &winograd_input);
+  m.def("winograd_output", &winograd_output);
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("bn_finalize", &bn_finalize);

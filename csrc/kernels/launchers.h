@@ -18,6 +18,11 @@ int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* s
                       int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
                       bool dgrad, const bf16_t* addend, const uint8_t* addend_mask,
                       const BnReduceArgs* bnr, hipStream_t st);
+// Winograd F(2x2,3x3) transforms (stride-1 pad-1 3x3; the 16 GEMMs run on hipBLASLt)
+int winograd_filter_launch(const bf16_t* wk, bf16_t* U, int K, int Cp, bool flip, hipStream_t st);
+int winograd_input_launch(const bf16_t* x, bf16_t* V, int N, int H, int W, int C, hipStream_t st);
+int winograd_output_launch(const bf16_t* M, bf16_t* y, float* stats, int N, int H, int W, int K,
+                           hipStream_t st);
 void conv_set_impl(int impl);
 void conv_wgrad_set_impl(int impl);
 void conv_set_tile(int t);

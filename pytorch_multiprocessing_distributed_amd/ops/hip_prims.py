@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import torch
 
+from . import winograd as _WG
 from .native import C as _C
 
 SLOTS = 64
@@ -62,6 +63,9 @@ def conv_weight(w, dtype, cin, want_t=True):
 
 
 def conv_fwd(x, wpack, stride, pad, want_stats):
+    if _WG.get_algo() == "winograd" and _WG.eligible(tuple(wpack[0].shape), stride, pad, x.shape[-1]):
+        return _WG.conv_fwd(x, wpack[0], want_stats,
+                            _acquire(wpack[0].shape[0], x.device) if want_stats else None)
     if want_stats:
         buf = _acquire(wpack[0].shape[0], x.device)
         y, st = _C.conv_fwd(x, wpack[0], int(stride), int(pad), True, buf)
@@ -75,6 +79,9 @@ def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None, bnred=None, addend_
     and returns ``(dx, [slot buffers])`` (same contract as :func:`bn_bwd_reduce`)."""
     if len(wpack) < 2:
         raise RuntimeError("dgrad image was not prepared (input did not require grad)")
+    if (bnred is None and addend is None and _WG.get_algo() == "winograd"
+            and _WG.eligible(tuple(wpack[0].shape), stride, pad)):
+        return _WG.conv_dgrad(dy, wpack[0], x_shape)
     if bnred is None:
         return _C.conv_dgrad(dy, wpack[1], int(x_shape[1]), int(x_shape[2]), int(stride), int(pad),
                              addend, None, None, None, None, None, None, None, addend_mask)
