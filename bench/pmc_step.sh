@@ -1,0 +1,16 @@
+# PMC counters of one full ResNet-50 bs256 training step (every kernel of the
+# step, last-step dispatches only in the summary).  Each pass stays within the
+# per-block counter limits (<= 8 SQ, <= 4 TCC, <= 2 GRBM) and runs alone.
+set -o pipefail
+mkdir -p gpurun_out/pmc
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+export PMD_NO_AUTOBUILD=1
+PA="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"
+PB="FETCH_SIZE TCC_HIT_sum GRBM_GUI_ACTIVE"
+PC="WRITE_SIZE TCC_MISS_sum GRBM_GUI_ACTIVE"
+for p in A B C; do
+  eval cnt=\$P$p
+  timeout -s KILL 150 rocprofv3 --kernel-trace --pmc $cnt --output-format csv -d gpurun_out/pmc/pass$p -o run -- \
+    python3 bench.py --steps 2 --warmup 1 > gpurun_out/pmc/pass$p.log 2>&1 || exit 1
+done
+echo all-ok
