@@ -757,6 +757,7 @@ static int ilog2(int v) {
 //   1 LDS-DMA BK=64, 2 stages      2 LDS-DMA BK=32, 4 stages
 //   3 LDS-DMA BK=64, 3 stages      4 LDS-DMA BK=32, 3 stages
 //   6 LDS-DMA BK=64, 2 stages, 32x32x16 MFMA
+//   7 LDS-DMA BK=32, 2 stages (128x128 tiles; 128x64 -> 4)
 //   5 (default) per shape: BK=32/3 stages for short reductions (Kg <= 512: the
 //     prologue/epilogue dominate, a shallower K-tile fills the pipe sooner),
 //     BK=64/2 stages otherwise (fewer barriers per MFMA) -- measured on all 23
@@ -768,7 +769,7 @@ void conv_set_impl(int impl) { g_conv_impl = impl; }
 static int conv_impl() {
   if (g_conv_impl < 0) {
     const char* e = getenv("PMD_CONV_IMPL");
-    g_conv_impl = (e && e[0] >= '0' && e[0] <= '6') ? e[0] - '0' : 5;
+    g_conv_impl = (e && e[0] >= '0' && e[0] <= '7') ? e[0] - '0' : 5;
   }
   return g_conv_impl;
 }
@@ -792,6 +793,10 @@ static void launch_t(const ConvArgs& a, hipStream_t st, int impl) {
     case 1: launch_k<BM, BN, 64, 2, DGRAD, STATS, true>(a, st); break;
     case 2: launch_k<BM, BN, 32, 4, DGRAD, STATS, true>(a, st); break;
     case 3: launch_k<BM, BN, 64, 3, DGRAD, STATS, true>(a, st); break;
+    case 7:  // BK=32 x2 stages (4 blocks/CU); the 64-column tile is too small for it
+      if constexpr (BN >= 128) launch_k<BM, BN, 32, 2, DGRAD, STATS, true>(a, st);
+      else launch_k<BM, BN, 32, 3, DGRAD, STATS, true>(a, st);
+      break;
     case 6:  // 32x32x16 MFMA: needs the uniform-tap loader (Cs % 64 == 0)
       if (a.Cs % 64 == 0) launch_k<BM, BN, 64, 2, DGRAD, STATS, true, true>(a, st);
       else launch_k<BM, BN, 64, 2, DGRAD, STATS, true>(a, st);
@@ -845,9 +850,15 @@ static bool big_ok(const ConvArgs& a) {
 // One candidate kernel configuration of the autotuner:
 //   0  128-row tile, LDS-DMA BK=32 x3 stages      1  128-row tile, LDS-DMA BK=64 x2
 //   2  256x256 tile (8 waves), BK=64 x2            3  256x128 tile (8 waves), BK=64 x2
+//   4  128x128 tile, LDS-DMA BK=32 x2 stages: 34 KB of LDS -> 4 blocks (16 waves) per
+//      CU, for the short-reduction dgrads whose fused epilogue (addend, BN-backward
+//      reduce over 1-2 BN inputs) streams 3-4 activation tensors and needs the
+//      extra waves to hide HBM latency
 template <bool DGRAD, bool STATS>
 static void launch_choice(int c, const ConvArgs& a, hipStream_t st) {
-  if (c == 2 && big_ok(a) && a.Nout >= 256) {
+  if (c == 4 && a.Nout > 64) {
+    launch_k<128, 128, 32, 2, DGRAD, STATS, true>(a, st);
+  } else if (c == 2 && big_ok(a) && a.Nout >= 256) {
     launch_k<256, 256, 64, 2, DGRAD, STATS, true, false, 2, 4>(a, st);
   } else if (c == 3 && big_ok(a)) {
     launch_k<256, 128, 64, 2, DGRAD, STATS, true, false, 4, 2>(a, st);
@@ -864,8 +875,8 @@ static void launch_choice(int c, const ConvArgs& a, hipStream_t st) {
 // events on the caller's stream) and caches the winner; later launches go
 // straight to it.  Candidates write the real output (every candidate overwrites
 // all of it, and the chosen kernel runs last), but BN statistics go to a
-// scratch slot buffer and the fused BN-backward reduce is left out of the
-// timing runs, so nothing accumulates twice.  PMD_CONV_AUTOTUNE=0 disables it
+// scratch slot buffer and the fused BN-backward reduce into scratch sums, so
+// nothing accumulates twice.  PMD_CONV_AUTOTUNE=0 disables it
 // (then: 128-row tiles, BK by reduction depth); PMD_CONV_AUTOTUNE_LOG=1 prints
 // every decision.
 struct TuneKey {
@@ -899,7 +910,20 @@ void conv_autotune_clear() {
 template <bool DGRAD, bool STATS>
 static int tune(const ConvArgs& a0, hipStream_t st) {
   ConvArgs a = a0;
-  a.bn_red[0] = a.bn_red[1] = nullptr;  // no fused reduce in the timing runs
+  // the fused BN-backward reduce is part of the cost being compared (it decides
+  // the epilogue-bound dgrads), so the timing runs keep it, aimed at scratch sums
+  static float* scratch_red = nullptr;
+  static int scratch_red_n = 0;
+  if (a.bn_red[0]) {
+    const int need = 2 * kStatSlots * 2 * a.Nout;
+    if (need > scratch_red_n) {
+      if (scratch_red) (void)hipFree(scratch_red);
+      if (hipMalloc(&scratch_red, sizeof(float) * need) != hipSuccess) return -1;
+      scratch_red_n = need;
+    }
+    a.bn_red[0] = scratch_red;
+    if (a.bn_red[1]) a.bn_red[1] = scratch_red + kStatSlots * 2 * a.Nout;
+  }
   static float* scratch_stats = nullptr;
   static int scratch_n = 0;
   if (STATS) {
@@ -918,9 +942,10 @@ static int tune(const ConvArgs& a0, hipStream_t st) {
   }
   int best = -1;
   float best_ms = 1e30f;
-  const int ncand = 4;
+  const int ncand = 5;
   for (int c = 0; c < ncand; ++c) {
-    if ((c == 2 && !(big_ok(a) && a.Nout >= 256)) || (c == 3 && !big_ok(a))) continue;
+    if ((c == 2 && !(big_ok(a) && a.Nout >= 256)) || (c == 3 && !big_ok(a)) || (c == 4 && a.Nout <= 64))
+      continue;
     launch_choice<DGRAD, STATS>(c, a, st);  // warm (code object load, caches)
     float t = 1e30f;
     for (int r = 0; r < 3; ++r) {

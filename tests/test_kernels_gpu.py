@@ -106,7 +106,7 @@ def test_wgrad_variants(shape, impl):
     _close(dw, dwr, 2e-3)
 
 
-@pytest.mark.parametrize("impl", [0, 1, 3, 4, 6])
+@pytest.mark.parametrize("impl", [0, 1, 3, 4, 6, 7])
 @pytest.mark.parametrize("shape", R50_SHAPES + CIFAR_SHAPES, ids=lambda s: "C%d_H%d_K%d_R%d_s%d" % s)
 def test_conv_pipeline_variants(shape, impl):
     """Every operand-staging / pipeline variant of the implicit-GEMM kernel
