@@ -54,15 +54,20 @@ float* opt_f32(const c10::optional<Tensor>& t, const char* what) {
 }
 
 // stats_buf: optional pre-zeroed [S,2,K] slot buffer (pool); allocated zeroed otherwise
-std::vector<Tensor> conv_fwd(Tensor x, Tensor wk, int64_t stride, int64_t pad, bool want_stats,
-                             c10::optional<Tensor> stats_buf) {
+// out_h/out_w < 0: the usual (H + 2 pad - R) / stride + 1; otherwise an explicit
+// (cropped) output extent -- the space-to-depth stem's 4x4 conv pads 2 rows on
+// the top but only 1 at the bottom, i.e. the last full-pad output row is dropped
+static std::vector<Tensor> conv_fwd_impl(Tensor x, Tensor wk, int64_t stride, int64_t pad, bool want_stats,
+                                         c10::optional<Tensor> stats_buf, int64_t out_h, int64_t out_w) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_CONT(x);
   CHECK_DEV(wk); CHECK_BF16(wk); CHECK_CONT(wk);
   TORCH_CHECK(x.dim() == 4 && wk.dim() == 4, "x [N,H,W,C], wk [K,R,S,C]");
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   const int K = wk.size(0), R = wk.size(1), S = wk.size(2);
   TORCH_CHECK(wk.size(3) == C, "channel mismatch: x has ", C, ", weight has ", wk.size(3));
-  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
+  const int Pf = (H + 2 * pad - R) / stride + 1, Qf = (W + 2 * pad - S) / stride + 1;
+  const int P = out_h < 0 ? Pf : (int)out_h, Q = out_w < 0 ? Qf : (int)out_w;
+  TORCH_CHECK(P >= 1 && Q >= 1 && P <= Pf && Q <= Qf, "conv_fwd: output extent beyond the padded input");
   c10::DeviceGuard g(x.device());
   Tensor y = torch::empty({N, P, Q, K}, x.options());
   Tensor stats;
@@ -82,6 +87,63 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor wk, int64_t stride, int64_t pad, b
   CHECK_RC(rc, "conv_fwd");
   if (want_stats) return {y, stats};
   return {y};
+}
+
+std::vector<Tensor> conv_fwd(Tensor x, Tensor wk, int64_t stride, int64_t pad, bool want_stats,
+                             c10::optional<Tensor> stats_buf) {
+  return conv_fwd_impl(x, wk, stride, pad, want_stats, stats_buf, -1, -1);
+}
+
+std::vector<Tensor> conv_fwd_hw(Tensor x, Tensor wk, int64_t stride, int64_t pad, int64_t out_h,
+                                int64_t out_w, bool want_stats, c10::optional<Tensor> stats_buf) {
+  return conv_fwd_impl(x, wk, stride, pad, want_stats, stats_buf, out_h, out_w);
+}
+
+// ----------------------------------------------------------- s2d stem
+Tensor stem_s2d_input(Tensor x) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONT(x);
+  TORCH_CHECK(x.dim() == 4 && x.size(3) == 8, "stem input must be [N,H,W,8] (3 channels zero-padded)");
+  TORCH_CHECK(x.size(1) % 2 == 0 && x.size(2) % 2 == 0, "space-to-depth needs even H, W");
+  c10::DeviceGuard g(x.device());
+  Tensor xs = torch::empty({x.size(0), x.size(1) / 2, x.size(2) / 2, 16}, x.options());
+  CHECK_RC(pmd::stem_s2d_input_launch(bfp(x), bfp_mut(xs), x.size(0), x.size(1), x.size(2), cur_stream()),
+           "stem_s2d_input");
+  return xs;
+}
+
+Tensor stem_s2d_weight(Tensor w) {
+  CHECK_DEV(w); CHECK_F32(w);
+  TORCH_CHECK(w.dim() == 4 && w.size(2) == 7 && w.size(3) == 7 && w.size(1) <= 4, "w must be [K,C<=4,7,7]");
+  const int K = w.size(0), C = w.size(1);
+  c10::DeviceGuard g(w.device());
+  Tensor wphys = w.permute({0, 2, 3, 1}).contiguous();  // no-op for channels_last params
+  Tensor ws = torch::empty({K, 4, 4, 16}, w.options().dtype(torch::kBFloat16));
+  CHECK_RC(pmd::stem_s2d_weight_launch(wphys.data_ptr<float>(), bfp_mut(ws), K, C, cur_stream()),
+           "stem_s2d_weight");
+  return ws;
+}
+
+// dws [K,4,4,16] -> dw [K,7,7,C]; with `out` (a contiguous [K,7,7,C] fp32 view,
+// e.g. the gradient arena) the folded gradient is accumulated into it
+Tensor stem_s2d_wgrad_fold(Tensor dws, int64_t C, c10::optional<Tensor> out) {
+  CHECK_DEV(dws); CHECK_F32(dws); CHECK_CONT(dws);
+  TORCH_CHECK(dws.dim() == 4 && dws.size(1) == 4 && dws.size(2) == 4 && dws.size(3) == 16, "dws [K,4,4,16]");
+  TORCH_CHECK(C >= 1 && C <= 4, "C <= 4");
+  const int K = dws.size(0);
+  c10::DeviceGuard g(dws.device());
+  Tensor dw;
+  const bool acc = out && out->defined();
+  if (acc) {
+    TORCH_CHECK(out->sizes() == torch::IntArrayRef({K, 7, 7, C}) && out->is_contiguous(), "fold out [K,7,7,C]");
+    opt_f32(out, "fold out");
+    dw = *out;
+  } else {
+    dw = torch::empty({K, 7, 7, C}, dws.options());
+  }
+  CHECK_RC(pmd::stem_s2d_wgrad_fold_launch(dws.data_ptr<float>(), dw.data_ptr<float>(), K, (int)C, acc,
+                                           cur_stream()),
+           "stem_s2d_wgrad_fold");
+  return dw;
 }
 
 // ------------------------------------------------------------- winograd
@@ -204,7 +266,8 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int64_t R, int64_t S, int64_t stride, int
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   const int P = dy.size(1), Q = dy.size(2), K = dy.size(3);
   TORCH_CHECK(dy.size(0) == N, "batch mismatch");
-  TORCH_CHECK((H + 2 * pad - R) / stride + 1 == P && (W + 2 * pad - S) / stride + 1 == Q,
+  // P, Q may crop the last rows/cols of the padded extent (s2d stem, see conv_fwd_hw)
+  TORCH_CHECK((H + 2 * pad - R) / stride + 1 >= P && (W + 2 * pad - S) / stride + 1 >= Q && P >= 1 && Q >= 1,
               "wgrad spatial mismatch");
   c10::DeviceGuard g(x.device());
   Tensor dw;
@@ -679,6 +742,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad_set_impl", &pmd::conv_wgrad_set_impl,
         "wgrad staging variant: 0 registers, 1 LDS-DMA 64x2 (default), 2 LDS-DMA 32x4, 3 LDS-DMA 64x3");
   m.def("conv_fwd", &conv_fwd);
+  m.def("conv_fwd_hw", &conv_fwd_hw);
+  m.def("stem_s2d_input", &stem_s2d_input);
+  m.def("stem_s2d_weight", &stem_s2d_weight);
+  m.def("stem_s2d_wgrad_fold", &stem_s2d_wgrad_fold);
   m.def("winograd_filter", &winograd_filter);
   m.def("winograd_input", &winograd_input);
   m.def("winograd_output", &winograd_output);

@@ -70,6 +70,10 @@ int bn_bwd_elemt_launch(const bf16_t* dout, const uint8_t* mask, const bf16_t* y
                         hipStream_t st);
 
 // fused stem tail (kernels/stem.hip): BN + ReLU + 3x3/s2 max-pool, and its backward
+// space-to-depth stem (7x7/s2 over 3 channels as 4x4/s1 over 16)
+int stem_s2d_input_launch(const bf16_t* x, bf16_t* xs, int N, int H, int W, hipStream_t st);
+int stem_s2d_weight_launch(const float* w, bf16_t* ws, int K, int C, hipStream_t st);
+int stem_s2d_wgrad_fold_launch(const float* dws, float* dw, int K, int C, bool accumulate, hipStream_t st);
 int stem_pool_fwd_launch(const bf16_t* y, const float* params, bf16_t* out, uint8_t* arg, int N, int H,
                          int W, int C, int P, int Q, hipStream_t st);
 int stem_pool_bwd_reduce_launch(const bf16_t* dout, const uint8_t* arg, const bf16_t* y,

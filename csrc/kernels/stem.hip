@@ -270,4 +270,83 @@ int stem_pool_bwd_elemt_launch(const bf16_t* dout, const uint8_t* arg, const bf1
   return 0;
 }
 
+// ---------------------------------------------------------------------------
+// Space-to-depth ImageNet stem.  The 7x7/s2/pad-3 conv over 3 channels is
+// re-expressed on the 2x2-blocked image xs[n][u][v][(dy*2+dx)*4 + c] =
+// x[n][2u+dy][2v+dx][c] (c < 4; the 3-channel input is zero-padded to 8, so
+// c = 3 is already 0) as a 4x4/s1 conv over 16 channels with pad 2 on the
+// top/left and 1 on the bottom/right (the launcher passes OH = H/2 explicitly):
+//   output p reads input rows 2p-3 .. 2p+3 = blocks u = p-2 .. p+1, i.e.
+//   tap i = 2 r + dy - 1 of the 7x7 filter (zero where i = -1 or 7).
+// The reduction shrinks from 7*7*8 = 392 (62% zero padding, a 128-wide wgrad
+// tile left 23% empty) to 4*4*16 = 256 (25% padding, exactly 2 wgrad tiles).
+__global__ __launch_bounds__(256) void stem_s2d_input_kernel(const bf16_t* __restrict__ x,
+                                                             bf16_t* __restrict__ xs, int N, int H,
+                                                             int W) {
+  const int Hs = H >> 1, Ws = W >> 1;
+  const long long total = (long long)N * Hs * Ws;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int v = (int)(i % Ws), u = (int)((i / Ws) % Hs), n = (int)(i / ((long long)Ws * Hs));
+    uint2 q[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int h = 2 * u + (d >> 1), w = 2 * v + (d & 1);
+      q[d] = *reinterpret_cast<const uint2*>(x + (((size_t)n * H + h) * W + w) * 8);  // channels 0..3
+    }
+    uint4* o = reinterpret_cast<uint4*>(xs + (size_t)i * 16);
+    o[0] = make_uint4(q[0].x, q[0].y, q[1].x, q[1].y);
+    o[1] = make_uint4(q[2].x, q[2].y, q[3].x, q[3].y);
+  }
+}
+
+// bf16 forward image ws[k][r][s][(dy*2+dx)*4 + c] of the fp32 7x7 weight
+// w[k][i][j][c] (channels_last parameter storage, C input channels <= 4).
+__global__ __launch_bounds__(256) void stem_s2d_weight_kernel(const float* __restrict__ w,
+                                                              bf16_t* __restrict__ ws, int K, int C) {
+  const int total = K * 4 * 4 * 16;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int ch = t & 15, s = (t >> 4) & 3, r = (t >> 6) & 3, k = t >> 8;
+    const int q = ch >> 2, c = ch & 3, dy = q >> 1, dx = q & 1;
+    const int i = 2 * r + dy - 1, j = 2 * s + dx - 1;
+    const bool ok = c < C && i >= 0 && i < 7 && j >= 0 && j < 7;
+    ws[t] = f2bf(ok ? w[(((size_t)k * 7 + i) * 7 + j) * C + c] : 0.f);
+  }
+}
+
+// dw[k][i][j][c] (+)= dws[k][r][s][(dy*2+dx)*4 + c] -- every 7x7 tap has exactly
+// one (r, dy) / (s, dx) preimage; dw is the [K][7][7][C] fp32 gradient (arena view).
+__global__ __launch_bounds__(256) void stem_s2d_wgrad_fold_kernel(const float* __restrict__ dws,
+                                                                  float* __restrict__ dw, int K, int C,
+                                                                  int accumulate) {
+  const int total = K * 49 * C;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int c = t % C, j = (t / C) % 7, i = (t / (7 * C)) % 7, k = t / (49 * C);
+    const int r = (i + 1) >> 1, dy = (i + 1) & 1, s = (j + 1) >> 1, dx = (j + 1) & 1;
+    const float g = dws[(((size_t)k * 4 + r) * 4 + s) * 16 + (dy * 2 + dx) * 4 + c];
+    dw[t] = accumulate ? dw[t] + g : g;
+  }
+}
+
+int stem_s2d_input_launch(const bf16_t* x, bf16_t* xs, int N, int H, int W, hipStream_t st) {
+  if ((H | W) & 1) return 1;
+  long long b = ((long long)N * (H / 2) * (W / 2) + 255) / 256;
+  if (b > 8192) b = 8192;
+  hipLaunchKernelGGL(stem_s2d_input_kernel, dim3((int)b), dim3(256), 0, st, x, xs, N, H, W);
+  return 0;
+}
+
+int stem_s2d_weight_launch(const float* w, bf16_t* ws, int K, int C, hipStream_t st) {
+  if (C > 4) return 1;
+  hipLaunchKernelGGL(stem_s2d_weight_kernel, dim3((K * 256 + 255) / 256), dim3(256), 0, st, w, ws, K, C);
+  return 0;
+}
+
+int stem_s2d_wgrad_fold_launch(const float* dws, float* dw, int K, int C, bool accumulate, hipStream_t st) {
+  if (C > 4) return 1;
+  hipLaunchKernelGGL(stem_s2d_wgrad_fold_kernel, dim3((K * 49 * C + 255) / 256), dim3(256), 0, st, dws, dw,
+                     K, C, accumulate ? 1 : 0);
+  return 0;
+}
+
 }  // namespace pmd

@@ -379,11 +379,73 @@ class _ConvFn(torch.autograd.Function):
         return dx, dw, None, None, None
 
 
+class _StemS2DConvFn(torch.autograd.Function):
+    """ImageNet stem conv (7x7/s2/pad 3 over 3 channels, reference
+    model/resnet.py:79 with the ImageNet stem) as a space-to-depth 4x4/s1 conv
+    over 16 channels on the gfx950 kernels (csrc/kernels/stem.hip): 256-deep
+    reduction instead of 392 (of which 62% was channel padding).  Same output,
+    same BN statistics contract; the weight gradient is folded back to 7x7x3."""
+
+    @staticmethod
+    def forward(ctx, x, w, want_stats):
+        from . import hip_prims as HP
+        from .native import C
+        xs = C.stem_s2d_input(x)                       # [N, H/2, W/2, 16]
+        ws = C.stem_s2d_weight(w.detach())             # [K, 4, 4, 16] bf16
+        oh, ow = x.shape[1] // 2, x.shape[2] // 2
+        buf = HP._acquire(w.shape[0], x.device) if want_stats else None
+        out = C.conv_fwd_hw(xs, ws, 1, 2, oh, ow, bool(want_stats), buf)
+        y = out[0]
+        stats = out[1] if want_stats else _empty(x.device)
+        ctx.save_for_backward(xs)
+        ctx.w = w
+        ctx.mark_non_differentiable(stats)
+        return y, stats
+
+    @staticmethod
+    def backward(ctx, dy, _dstats):
+        from .native import C
+        (xs,) = ctx.saved_tensors
+        w = ctx.w
+        if not ctx.needs_input_grad[1] or not w.requires_grad:
+            return None, None, None
+        dws = C.conv_wgrad(dy.contiguous(), xs, 4, 4, 1, 2, None)   # fp32 [K, 4, 4, 16]
+        tgt = _grad_target(w)
+        if tgt is not None:
+            C.stem_s2d_wgrad_fold(dws, w.shape[1], tgt.permute(0, 2, 3, 1))
+            _ready(w)
+            return None, None, None
+        dw = C.stem_s2d_wgrad_fold(dws, w.shape[1], None)            # [K, 7, 7, C]
+        return None, dw.permute(0, 3, 1, 2), None
+
+
+_S2D_STEM = os.environ.get("PMD_STEM_S2D", "1") != "0"
+
+
+def set_s2d_stem(flag: bool):
+    global _S2D_STEM
+    _S2D_STEM = bool(flag)
+
+
+def _pair(v):
+    return tuple(v) if isinstance(v, (tuple, list)) else (v, v)
+
+
+def _s2d_stem_ok(x, conv_mod):
+    w = conv_mod.weight
+    return (_S2D_STEM and x.is_cuda and not _state["force_torch"] and x.dim() == 4 and x.shape[-1] == 8
+            and x.shape[1] % 2 == 0 and x.shape[2] % 2 == 0 and tuple(w.shape[2:]) == (7, 7)
+            and w.shape[1] <= 4 and _pair(conv_mod.stride) == (2, 2) and _pair(conv_mod.padding) == (3, 3)
+            and not x.requires_grad)
+
+
 def conv(x, conv_mod, want_stats=None):
     """Returns ``(y, stats)``; ``stats`` = per-channel (sum, sum^2) of y in the
     backend's layout (consumed by :func:`bn_add_act`)."""
     if want_stats is None:
         want_stats = conv_mod.training
+    if _s2d_stem_ok(x, conv_mod):
+        return _StemS2DConvFn.apply(x, conv_mod.weight, bool(want_stats))
     return _ConvFn.apply(x, conv_mod.weight, conv_mod.stride, conv_mod.padding, bool(want_stats))
 
 
