@@ -148,14 +148,14 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_reduce_kernel(
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         s1[k] += dz[k];
-        s2[k] += dz[k] * (v[k] - mean[k]) * inv[k];
+        s2[k] += dz[k] * (v[k] - mean[k]);  // * invstd once, below
       }
     }
   }
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     part[tid * 17 + k] = s1[k];
-    part[tid * 17 + 8 + k] = s2[k];
+    part[tid * 17 + 8 + k] = s2[k] * inv[k];
   }
   __syncthreads();
   for (int e = tid; e < C8 * 16; e += 256) {
@@ -246,7 +246,10 @@ int stem_pool_bwd_reduce_launch(const bf16_t* dout, const uint8_t* arg, const bf
   if (C % 8 || l < 0 || (C / 8) > 256) return 1;
   // ~4 input rows per block: thousands of blocks keep many rows' gathers in
   // flight (the per-block atomics stay far below the streaming cost)
-  const int rpb = 4;
+#ifndef PMD_STEM_RPB
+#define PMD_STEM_RPB 4
+#endif
+  const int rpb = PMD_STEM_RPB;
   const int blocks = (N * H + rpb - 1) / rpb;
   hipLaunchKernelGGL(stem_pool_bwd_reduce_kernel, dim3(blocks), dim3(256), 0, st, dout, arg, y, params, red,
                      N, H, W, C, P, Q, rpb, l);
@@ -259,7 +262,10 @@ int stem_pool_bwd_elemt_launch(const bf16_t* dout, const uint8_t* arg, const bf1
                                hipStream_t st) {
   const int l = l2e(C / 8);
   if (C % 8 || l < 0 || (C / 8) > 256) return 1;
-  const int rpb = 4;
+#ifndef PMD_STEM_RPB
+#define PMD_STEM_RPB 4
+#endif
+  const int rpb = PMD_STEM_RPB;
   const dim3 grid((N * H + rpb - 1) / rpb);
   if (eval_mode)
     hipLaunchKernelGGL(stem_pool_bwd_elemt_kernel<true>, grid, dim3(256), 0, st, dout, arg, y, params, gamma,
