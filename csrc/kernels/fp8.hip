@@ -71,6 +71,41 @@ __global__ void quant_weight_fp8_kernel(const float* __restrict__ w, uint8_t* __
   if (amax) block_amax_update(amax, m);
 }
 
+// Grouped form: block b finds its descriptor in the block-start table (a few
+// dozen entries), then grid-strides inside that weight; amax goes to the
+// weight's own slots (one atomicMax per block, every block of one weight).
+__global__ void quant_weight_fp8_grouped_kernel(const Fp8WeightDesc* __restrict__ descs,
+                                                const int* __restrict__ block_start, int n) {
+  __shared__ int e_sh;
+  if (threadIdx.x == 0) {
+    int e = 0;
+    while (e + 1 < n && block_start[e + 1] <= (int)blockIdx.x) ++e;
+    e_sh = e;
+  }
+  __syncthreads();
+  const Fp8WeightDesc d = descs[e_sh];
+  const int lb = blockIdx.x - block_start[e_sh];
+  const int nb = block_start[e_sh + 1] - block_start[e_sh];
+  const float s = d.scale[0];
+  float m = 0.f;
+  const int total = d.K * d.RS * d.Cp;
+  for (int i = lb * blockDim.x + threadIdx.x; i < total; i += nb * blockDim.x) {
+    const int c = i % d.Cp;
+    const int krs = i / d.Cp;
+    const float v = c < d.C ? d.w[(size_t)krs * d.C + c] : 0.f;
+    m = fmaxf(m, fabsf(v));
+    d.q[i] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(v * s), 0.f, 0, false) & 0xff);
+  }
+  // block_amax_update picks slot blockIdx % kAmaxSlots of the weight's own site
+  block_amax_update(d.amax, m);
+}
+
+void quant_weight_fp8_grouped_launch(const Fp8WeightDesc* d_descs, const int* d_block_start, int n,
+                                     int total_blocks, hipStream_t st) {
+  hipLaunchKernelGGL(quant_weight_fp8_grouped_kernel, dim3(total_blocks), dim3(256), 0, st, d_descs,
+                     d_block_start, n);
+}
+
 // e4m3 -> fp32 (tests / debugging)
 __global__ void dequant_fp8_kernel(const uint8_t* __restrict__ q, float* __restrict__ out,
                                    const float* __restrict__ inv_scale, long long n) {

@@ -105,6 +105,16 @@ int cifar_augment_launch(const uint8_t* data, const long long* idx, void* out, b
 // FP8 e4m3 (kernels/fp8.hip)
 int quant_bf16_fp8_launch(const bf16_t* x, uint8_t* q, const float* scale, float* amax, long long n,
                           hipStream_t st);
+// all fp8 weight images of a model in one launch (per-conv scale / amax sites)
+struct Fp8WeightDesc {
+  const float* w;      // fp32 [K][R][S][C]
+  uint8_t* q;          // e4m3 [K][R][S][Cp]
+  const float* scale;  // [1]
+  float* amax;         // [kAmaxSlots]
+  int K, RS, C, Cp;
+};
+void quant_weight_fp8_grouped_launch(const Fp8WeightDesc* d_descs, const int* d_block_start, int n,
+                                     int total_blocks, hipStream_t st);
 int quant_weight_fp8_launch(const float* w, uint8_t* q, const float* scale, float* amax, int K, int RS,
                             int C, int Cp, hipStream_t st);
 int dequant_fp8_launch(const uint8_t* q, float* out, const float* inv_scale, long long n, hipStream_t st);

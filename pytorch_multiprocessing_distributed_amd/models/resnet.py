@@ -219,13 +219,16 @@ class ResNet(nn.Module):
         if not getattr(P, "SUPPORTS_FP8", False):          # the gfx950 prims only
             return None
         ws = self.__dict__.get("_pmd_wset")
-        key = (x.shape[-1], self.conv1.weight.data_ptr(), self.linear.weight.data_ptr())
+        f8 = OF.get_fp8()
+        key = (x.shape[-1], self.conv1.weight.data_ptr(), self.linear.weight.data_ptr(), id(f8))
         if ws is None or self.__dict__.get("_pmd_wset_key") != key:
             entries = [(self.conv1, x.shape[-1], False)]
             for mod in self.modules():
                 if isinstance(mod, (nn.Conv2d, Conv2d)) and mod is not self.conv1:
                     entries.append((mod, mod.in_channels, True))
             ws = OF.WeightImageSet(entries)
+            if f8 is not None:   # config 5: every block conv's e4m3 image in the same per-step refresh
+                ws.fp8 = OF.Fp8WeightSet([(m, cp) for m, cp, _ in entries[1:]], f8)
             self.__dict__["_pmd_wset"] = ws
             self.__dict__["_pmd_wset_key"] = key
         return ws

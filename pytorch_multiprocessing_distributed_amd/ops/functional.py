@@ -75,12 +75,38 @@ class WeightImageSet:
 
     def refresh(self):
         self._c.refresh()
+        if self.fp8 is not None:
+            self.fp8.refresh()
+
+    fp8 = None   # Fp8WeightSet of the same model when fp8 (config 5) is active
 
     def lookup(self, w, cin, want_t):
         i = self.index.get((id(w), cin, want_t))
         if i is None and not want_t:
             i = self.index.get((id(w), cin, True))   # a superset of what was asked
         return None if i is None else tuple(self._c.get(i))
+
+
+class Fp8WeightSet:
+    """e4m3 images of the block convs' weights, quantised with their delayed-
+    scaling sites by ONE grouped launch per step (native ``_C.Fp8WeightImages``)
+    instead of one ``quant_weight_fp8`` launch per conv.  ``entries``:
+    [(conv module, input channels)]."""
+
+    def __init__(self, entries, f8):
+        from .native import C
+        self.f8 = f8
+        self.index = {id(m): i for i, (m, _) in enumerate(entries)}
+        sites = [f8.site(("w", id(m)), init_from=m.weight) for m, _ in entries]
+        self._c = C.Fp8WeightImages([m.weight for m, _ in entries], [cp for _, cp in entries],
+                                    [sc for sc, _ in sites], [am for _, am in sites])
+
+    def refresh(self):
+        self._c.refresh()
+
+    def lookup(self, conv_m, cin):
+        i = self.index.get(id(conv_m))
+        return None if i is None else self._c.get(i)
 
 
 def _weight_images(P, w, dtype, cin, want_t):
@@ -134,7 +160,11 @@ def _conv_fwd_any(P, f8, h, hq, wp, conv_m, want_stats):
     if f8 is None or hq is None:
         return P.conv_fwd(h, wp, conv_m.stride, conv_m.padding, want_stats)
     sw, aw = f8.site(("w", id(conv_m)), init_from=conv_m.weight)
-    wq = P.quant_weight_fp8(conv_m.weight, h.shape[-1], sw, aw)
+    wi = _state["wimg"]
+    wq = wi.fp8.lookup(conv_m, h.shape[-1]) if (wi is not None and wi.fp8 is not None
+                                                 and wi.fp8.f8 is f8) else None
+    if wq is None or wq.shape[-1] != h.shape[-1]:
+        wq = P.quant_weight_fp8(conv_m.weight, h.shape[-1], sw, aw)
     return P.conv_fp8_fwd(hq[0], wq, hq[1], sw, conv_m.stride, conv_m.padding, want_stats)
 
 

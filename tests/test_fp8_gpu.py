@@ -133,3 +133,27 @@ def test_resnet50_fp8_trains():
             n = len(f8.sites)
             assert torch.isfinite(f8.scale[:n]).all() and (f8.scale[:n] > 0).all()
     assert abs(first["fp8"] - first["bf16"]) < 0.05 * first["bf16"], first
+
+
+def test_grouped_fp8_weight_images_match_per_conv():
+    """Fp8WeightSet (one grouped launch for every block conv) == quant_weight_fp8
+    per conv: identical e4m3 bytes and amax, for every ResNet-50 block conv."""
+    from pytorch_multiprocessing_distributed_amd.models import ResNet50
+    from pytorch_multiprocessing_distributed_amd.models.resnet import Conv2d
+    from pytorch_multiprocessing_distributed_amd.ops import functional as OF
+    from pytorch_multiprocessing_distributed_amd.ops.fp8 import Fp8Scaling
+    C = _C()
+    torch.manual_seed(0)
+    m = ResNet50(num_classes=1000, stem="imagenet").to(DEV)
+    convs = [mod for mod in m.modules() if isinstance(mod, Conv2d) and mod is not m.conv1]
+    f8 = Fp8Scaling(DEV)
+    ws = OF.Fp8WeightSet([(c, c.in_channels) for c in convs], f8)
+    ws.refresh()
+    torch.cuda.synchronize()
+    for c in convs:
+        sw, aw = f8.site(("w", id(c)))
+        ref_amax = torch.zeros(64, device=DEV)
+        ref = C.quant_weight_fp8(c.weight.detach(), c.in_channels, sw, ref_amax)
+        got = ws.lookup(c, c.in_channels)
+        assert torch.equal(got, ref)
+        assert torch.equal(aw.max(), ref_amax.max())
