@@ -225,6 +225,58 @@ def _wgrad(P, dy, x, wpack, stride, pad, w):
     return dwk.permute(0, 3, 1, 2)                                   # [K,C,R,S] channels_last
 
 
+_WGRAD_STREAM = {"on": os.environ.get("PMD_WGRAD_STREAM", "1") != "0", "streams": {}}
+
+
+def set_wgrad_stream(flag: bool):
+    """Run the block weight gradients on a side HIP stream (default on)."""
+    _WGRAD_STREAM["on"] = bool(flag)
+
+
+class _WgradSide:
+    """Weight gradients of one block backward on a side HIP stream.
+
+    A wgrad only needs dY and the saved conv input, and nothing in the block
+    backward consumes its result, so it can run concurrently with the main
+    stream's BN-backward elementwise pass and the next dgrad (memory- / epilogue-
+    bound work next to the MFMA-heavy wgrad).  The side stream forks from the
+    main stream before each wgrad (dY is final), and the main stream joins it
+    once at the end of the block backward; only THEN are the weights marked
+    ready for the gradient all-reduce, so a bucket never launches on a
+    gradient still being written.  ``record_stream`` keeps dY / X alive for
+    the side stream in the caching allocator."""
+
+    def __init__(self, t):
+        self.on = _WGRAD_STREAM["on"] and t.is_cuda and not _state["force_torch"]
+        self.ready = []
+        if self.on:
+            dev = t.device
+            st = _WGRAD_STREAM["streams"].get(dev)
+            if st is None:
+                st = _WGRAD_STREAM["streams"][dev] = torch.cuda.Stream(device=dev)
+            self.side = st
+            self.main = torch.cuda.current_stream(dev)
+
+    def wgrad(self, P, dy, x, wpack, stride, pad, w):
+        if not self.on or _grad_target(w) is None:
+            return _wgrad(P, dy, x, wpack, stride, pad, w)
+        self.side.wait_stream(self.main)
+        with torch.cuda.stream(self.side):
+            tgt = _grad_target(w)
+            P.conv_wgrad(dy, x, tuple(wpack[0].shape), stride, pad, out=tgt.permute(0, 2, 3, 1))
+        dy.record_stream(self.side)
+        x.record_stream(self.side)
+        self.ready.append(w)
+        return None
+
+    def join(self):
+        if self.on and self.ready:
+            self.main.wait_stream(self.side)
+            for w in self.ready:
+                _ready(w)
+            self.ready = []
+
+
 def _bn_acc(bn):
     """(d_beta, d_gamma) arena targets for a BN module, or None."""
     tb, tg = _grad_target(bn.bias), _grad_target(bn.weight)
@@ -749,10 +801,11 @@ class _ResidualBlockFn(torch.autograd.Function):
             dx_, red_ = P.conv_dgrad(dy_, wp_, shape, stride, pad, addend, bnred=(z_, [(y_, p_)]))
             return dx_, _Pre(red_, _after_dgrad_event(dx_, sync if training else None))
         chk("dyf", dyf)
-        # --- final conv
+        side = _WgradSide(dout)
+        # --- final conv (its wgrad forks to the side stream first: it overlaps the dgrad)
+        put(fconv.weight, side.wgrad(P, dyf, hlast, wpf, fconv.stride, fconv.padding, fconv.weight))
         dh, pre_k = dgrad_fused(dyf, wpf, tuple(hlast.shape), fconv.stride, fconv.padding, recs[-1])
         chk("dh(final)", dh)
-        put(fconv.weight, _wgrad(P, dyf, hlast, wpf, fconv.stride, fconv.padding, fconv.weight))
         dx = None
         # --- conv->BN->ReLU stages in reverse; the block-input gradient of the
         #     residual/projection path is added in the first stage's dgrad epilogue
@@ -764,6 +817,8 @@ class _ResidualBlockFn(torch.autograd.Function):
             put(bn.weight, g[0])
             put(bn.bias, g[1])
             chk(f"dy(stage {k})", dy)
+            put(conv_m.weight, side.wgrad(P, dy, hin, wp, conv_m.stride, conv_m.padding,
+                                          conv_m.weight))
             if k > 0:
                 dh, pre_k = dgrad_fused(dy, wp, tuple(hin.shape), conv_m.stride, conv_m.padding,
                                         recs[k - 1])
@@ -783,10 +838,9 @@ class _ResidualBlockFn(torch.autograd.Function):
                 else:
                     dx = P.conv_dgrad(dy, wp, tuple(x.shape), conv_m.stride, conv_m.padding, addend,
                                       addend_mask=amask)
-            put(conv_m.weight, _wgrad(P, dy, hin, wp, conv_m.stride, conv_m.padding,
-                                      conv_m.weight))
         if shortcut is not None:
-            put(sconv.weight, _wgrad(P, dys, x, wps, sconv.stride, sconv.padding, sconv.weight))
+            put(sconv.weight, side.wgrad(P, dys, x, wps, sconv.stride, sconv.padding, sconv.weight))
+        side.join()
         return (None, dx, *[grads.get(id(p)) for p in _block_params(stages, final, shortcut)])
 
 
