@@ -225,7 +225,8 @@ def _wgrad(P, dy, x, wpack, stride, pad, w):
     return dwk.permute(0, 3, 1, 2)                                   # [K,C,R,S] channels_last
 
 
-_WGRAD_STREAM = {"on": os.environ.get("PMD_WGRAD_STREAM", "1") != "0", "streams": {}}
+_WGRAD_STREAM = {"on": os.environ.get("PMD_WGRAD_STREAM", "1") != "0", "streams": {},
+                 "defer": os.environ.get("PMD_WGRAD_DEFER", "1") != "0"}
 
 
 def set_wgrad_stream(flag: bool):
@@ -270,11 +271,43 @@ class _WgradSide:
         return None
 
     def join(self):
-        if self.on and self.ready:
+        """End of the block backward: the join is DEFERRED by one block -- the
+        main stream waits for the PREVIOUS block's side work (whose wgrads have
+        overlapped this block's backward) and marks those weights ready; this
+        block's side work is joined by the next block, or by the end-of-backward
+        engine callback queued with the first deferral (queued before the
+        reducer's own finalize callback, so every weight is ready before any
+        bucket is force-launched)."""
+        if not (self.on and self.ready):
+            return
+        if not _WGRAD_STREAM["defer"]:
             self.main.wait_stream(self.side)
             for w in self.ready:
                 _ready(w)
             self.ready = []
+            return
+        ev = torch.cuda.Event()
+        ev.record(self.side)
+        pend = _WGRAD_STREAM.get("pending")
+        if pend is None:
+            torch.autograd.Variable._execution_engine.queue_callback(_wgrad_flush)
+        else:
+            _join_pending(pend)
+        _WGRAD_STREAM["pending"] = (self.main, ev, self.ready)
+        self.ready = []
+
+
+def _join_pending(pend):
+    main, ev, ws = pend
+    main.wait_event(ev)
+    for w in ws:
+        _ready(w)
+
+
+def _wgrad_flush():
+    pend = _WGRAD_STREAM.pop("pending", None)
+    if pend is not None:
+        _join_pending(pend)
 
 
 def _bn_acc(bn):
