@@ -5,8 +5,8 @@ export PMD_NO_AUTOBUILD=1
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 && \
 for r in 1 2; do
   for v in 0 1; do
-    o=$(PMD_WGRAD_DEFER=$v timeout -k 10 200 python bench.py --steps 30 --warmup 10 2>/dev/null | tail -1) || exit 1
-    echo "$r defer=$v $(echo "$o" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')" >> gpurun_out/ab_defer.log
+    o=$(PMD_SHORTCUT_SIDE=$v timeout -k 10 200 python bench.py --steps 30 --warmup 10 2>/dev/null | tail -1) || exit 1
+    echo "$r scside=$v $(echo "$o" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')" >> gpurun_out/ab_scside.log
   done
 done
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && rm -rf gpurun_out/prof && \
