@@ -226,7 +226,7 @@ def _wgrad(P, dy, x, wpack, stride, pad, w):
 
 
 _WGRAD_STREAM = {"on": os.environ.get("PMD_WGRAD_STREAM", "1") != "0", "streams": {},
-                 "defer": os.environ.get("PMD_WGRAD_DEFER", "1") != "0"}
+                 "defer": int(os.environ.get("PMD_WGRAD_DEFER", "1") or 0)}  # join lag in blocks
 
 
 def set_wgrad_stream(flag: bool):
@@ -290,10 +290,11 @@ class _WgradSide:
         ev.record(self.side)
         pend = _WGRAD_STREAM.get("pending")
         if pend is None:
+            pend = _WGRAD_STREAM["pending"] = []
             torch.autograd.Variable._execution_engine.queue_callback(_wgrad_flush)
-        else:
-            _join_pending(pend)
-        _WGRAD_STREAM["pending"] = (self.main, ev, self.ready)
+        pend.append((self.main, ev, self.ready))
+        while len(pend) > _WGRAD_STREAM["defer"]:
+            _join_pending(pend.pop(0))
         self.ready = []
 
 
@@ -305,8 +306,7 @@ def _join_pending(pend):
 
 
 def _wgrad_flush():
-    pend = _WGRAD_STREAM.pop("pending", None)
-    if pend is not None:
+    for pend in _WGRAD_STREAM.pop("pending", None) or []:
         _join_pending(pend)
 
 
