@@ -420,7 +420,10 @@ int stats_finalize_local_launch(float* slots, float count, const float* gamma, c
 
 static int ew_grid(long long nchunk, int C8) {
   long long b = (nchunk + 255) / 256;
-  if (b > 2048) b = 2048;
+#ifndef PMD_EW_BLOCKS
+#define PMD_EW_BLOCKS 2048
+#endif
+  if (b > PMD_EW_BLOCKS) b = PMD_EW_BLOCKS;
   if (b < 1) b = 1;
   // keep grid*256 a multiple of C8 (C8 is a power of two <= 256, so always true)
   return (int)b;
