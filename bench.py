@@ -30,8 +30,10 @@ sys.path.insert(0, ROOT)
 METRIC = ("images/sec (whole node) ResNet-50 224×224 bf16 at 1/2/4/8 MI355X; "
           "DDP scaling efficiency")
 # stock PyTorch-ROCm reference path (DDP+SyncBN+MIOpen, bench/comparator_torch.py),
-# measured on one MI355X at per-GPU batch 256: profiles/comparator_r01.txt
-STOCK_IPS_PER_GPU = 6612.5
+# recorded on one MI355X at per-GPU batch 256 (profiles/comparator_r01.log); reported
+# as a RECORDED figure unless --with_stock measures it in the same run
+STOCK_IPS_PER_GPU_RECORDED = 6612.5
+STOCK_RECORDED_SOURCE = "profiles/comparator_r01.log (1x MI355X, round 1)"
 _MODEL_NAMES = {"resnet50": "ResNet-50", "resnet101": "ResNet-101", "resnet152": "ResNet-152",
                 "resnet34": "ResNet-34", "resnet18": "ResNet-18-ref", "res": "ResNet-18-ref"}
 
@@ -54,6 +56,19 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
                     help="fp8 = BASELINE config 5: block-conv forwards on the e4m3 scaled MFMA "
                          "(delayed per-tensor scaling), everything else bf16/fp32")
+    ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
+                    help="process-group backend for W>1 (auto: nccl = RCCL)")
+    ap.add_argument("--same_device", action="store_true",
+                    help="W>1 ranks all on GPU 0 (with --backend gloo: rehearses the exact "
+                         "multi-rank code path -- DataParallel, native reducer, xGMI SyncBN -- "
+                         "on a one-GPU box; not a throughput number)")
+    ap.add_argument("--comm", default="c10d", choices=["c10d", "rccl"],
+                    help="gradient-bucket transport: torch ProcessGroupNCCL or the native "
+                         "RCCL communicator (csrc/runtime/rccl_comm.cpp)")
+    ap.add_argument("--with_stock", action="store_true",
+                    help="also measure the stock PyTorch-ROCm comparator in this run (W=1)")
+    ap.add_argument("--timeline", action="store_true",
+                    help="print the gradient-bucket launch/overlap timeline of the last step")
     ap.add_argument("--profile", default="", help="write a torch.profiler table here (rank 0)")
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole training step (fwd+bwd+SGD) in a HIP graph and replay it "
@@ -72,7 +87,10 @@ def bench_rank(rank, world, a):
     from pytorch_multiprocessing_distributed_amd.parallel.dp import DataParallel
 
     if world > 1:
-        dev = launch.init_process(rank, world, "nccl", "cuda")
+        backend = "nccl" if a.backend == "auto" else a.backend
+        if a.same_device:
+            os.environ["LOCAL_RANK"] = "0"
+        dev = launch.init_process(rank, world, backend, "cuda")
     else:
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
@@ -81,7 +99,8 @@ def bench_rank(rank, world, a):
     comm = get_comm()
     setup_syncbn(comm, a.sync_bn, a.syncbn_comm, True)
     model = DataParallel(model, comm, bucket_mb=a.bucket_mb, first_bucket_mb=a.first_bucket_mb,
-                         compress=a.grad_compress)
+                         compress=a.grad_compress, transport=a.comm if comm is not None else "c10d",
+                         timeline=a.timeline)
     if a.dtype == "fp8":
         from pytorch_multiprocessing_distributed_amd.ops.fp8 import Fp8Scaling
         OF.set_fp8(Fp8Scaling(dev))
@@ -136,6 +155,8 @@ def bench_rank(rank, world, a):
     t0 = time.perf_counter()
     for i in range(a.steps):
         loss = step(a.warmup + i)
+        if comm is not None:
+            comm.raise_if_failed()          # host-mapped xGMI error word, no device sync
     torch.cuda.synchronize()
     if comm is not None:
         comm.barrier()
@@ -148,26 +169,47 @@ def bench_rank(rank, world, a):
     final_loss = float(loss.item())
     if comm is not None and comm.xgmi is not None:
         comm.xgmi.check()         # raises if any statistics exchange timed out
+    if a.timeline and rank == 0 and comm is not None:
+        for row in model.bucket_timeline():
+            print("[bench] bucket %d: host launch %.0f us after first grad, finalize at %.0f us; "
+                  "device all-reduce %.3f .. %.3f ms vs end of backward" % row, file=sys.stderr)
+    stock = None
+    if a.with_stock and world == 1 and a.dtype == "bf16":
+        sys.path.insert(0, os.path.join(ROOT, "bench"))
+        from comparator_torch import measure_stock
+        stock = measure_stock(a.model, a.batch, a.image, steps=max(a.steps, 10), warmup=5, dev=dev)
     if rank == 0:
         ips = a.batch * world * a.steps / dt
+        model_name = _MODEL_NAMES.get(a.model.lower(), a.model)
+        metric = METRIC if (model_name == "ResNet-50" and a.dtype == "bf16" and a.image == 224) else (
+            f"images/sec (whole node) {model_name} {a.image}×{a.image} {a.dtype} at 1/2/4/8 MI355X; "
+            "DDP scaling efficiency")
+        parallelism = f"dp{world}"
+        if world > 1 and a.same_device:
+            parallelism += f"-same-gpu-{dist.get_backend()}"
         rec = {
-            "metric": METRIC, "value": round(ips, 1), "unit": "images/sec",
+            "metric": metric, "value": round(ips, 1), "unit": "images/sec",
             "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(1000.0 * dt / a.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
             "data": "synthetic (on-device generated ImageNet-shaped batches, random-init weights)",
-            "config": {"model": _MODEL_NAMES.get(a.model.lower(), a.model), "global_batch": a.batch * world,
+            "config": {"model": model_name, "global_batch": a.batch * world,
                        "seq_len": None,
                        "image_size": a.image, "per_gpu_batch": a.batch,
-                       "parallelism": f"dp{world}", "sync_bn": a.sync_bn == "on" and world > 1,
+                       "parallelism": parallelism, "sync_bn": a.sync_bn == "on" and world > 1,
                        "bucket_mb": a.bucket_mb, "hip_graph": bool(a.graph and world == 1),
                        "syncbn_comm": ("xgmi" if comm is not None and comm.xgmi is not None
                                        else "rccl" if world > 1 else None),
-                       "grad_compress": a.grad_compress},
-            "vs_stock_pytorch_rocm": (round(ips / (STOCK_IPS_PER_GPU * world), 3)
-                                      if a.model.lower() == "resnet50" and a.dtype == "bf16" else None),
+                       "grad_compress": a.grad_compress,
+                       "grad_transport": model.transport},
             "final_loss": round(final_loss, 4),
         }
+        if stock is not None:
+            rec["stock_pytorch_rocm_ips_measured"] = round(stock, 1)
+            rec["vs_stock_pytorch_rocm_measured"] = round(ips / stock, 3)
+        elif model_name == "ResNet-50" and a.dtype == "bf16" and world == 1:
+            rec["vs_stock_pytorch_rocm_recorded"] = round(ips / STOCK_IPS_PER_GPU_RECORDED, 3)
+            rec["stock_recorded_source"] = STOCK_RECORDED_SOURCE
         print(json.dumps(rec), flush=True)
     if a.profile and rank == 0:
         from torch.profiler import ProfilerActivity, profile

@@ -23,6 +23,47 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pytorch_multiprocessing_distributed_amd.models import build_model  # noqa: E402
 
 
+def measure_stock(model_name="resnet50", batch=256, image=224, steps=20, warmup=10, dev=None,
+                  channels_last=True, ddp_device=None):
+    """Images/sec of the reference's code path on stock PyTorch-ROCm on ``dev``
+    (per process; DDP + SyncBN when torch.distributed is initialised with
+    ``ddp_device``).  Used by ``bench.py --with_stock`` so the comparator is
+    measured in the same run, on the same box, as the framework."""
+    dev = dev or torch.device("cuda", torch.cuda.current_device())
+    torch.backends.cudnn.benchmark = True
+    model = build_model(model_name, num_classes=1000, stem="imagenet", impl="stock").to(dev)
+    mf = torch.channels_last if channels_last else torch.contiguous_format
+    model = model.to(memory_format=mf)
+    if ddp_device is not None:
+        model = nn.SyncBatchNorm.convert_sync_batchnorm(model)
+        model = nn.parallel.DistributedDataParallel(model, device_ids=[ddp_device])
+    crit = nn.CrossEntropyLoss().to(dev)
+    opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4,
+                          nesterov=True, foreach=True)
+    x = torch.randn(batch, 3, image, image, device=dev).to(memory_format=mf)
+    y = torch.randint(0, 1000, (batch,), device=dev)
+
+    def step():
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = crit(model(x), y)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    del model, opt, x, y
+    torch.cuda.empty_cache()
+    return batch * steps / dt
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="resnet50")

@@ -91,7 +91,7 @@ def build(force=False, jobs=None, debug=False, verbose=True):
     if force or jobs_ or _newer(objs, out):
         link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs,
                 f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
-                "-ltorch_python", f"-Wl,-rpath,{lib}",
+                "-ltorch_python", "-l:librccl.so", f"-Wl,-rpath,{lib}",
                 "-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"]
         _run(link)
         if verbose:

@@ -134,8 +134,8 @@ constexpr int kXgmiArChunk = 2048;     // floats per block of the plain all-redu
 constexpr int kXgmiCap = kXgmiChunk * kXgmiMaxBlocks;  // max floats per call
 constexpr int kXgmiFlagBytes = 4096;
 int xgmi_allreduce_launch(float* const* data, uint32_t* const* flags, float* x, int n, int rank,
-                          int world, uint32_t* epochs, uint32_t* err, long long spin_limit,
-                          hipStream_t st);
+                          int world, uint32_t* epochs, uint32_t* err, uint32_t* err_host,
+                          unsigned long long timeout_ticks, hipStream_t st);
 
 // SyncBN collapse + one-shot exchange + finalize (fwd) / global sums (bwd) in one kernel
 struct BnFinalizeOut {
@@ -166,5 +166,6 @@ struct XgmiBnArgs {
 // fused SyncBN kernel: channel pairs per block (1..kBnPairs); default kBnPairs
 void xgmi_set_bn_pairs(int pairs);
 int xgmi_bn_launch(float* const* data, uint32_t* const* flags, const XgmiBnArgs& args, int rank, int world,
-                   uint32_t* epochs, uint32_t* err, long long spin_limit, hipStream_t st);
+                   uint32_t* epochs, uint32_t* err, uint32_t* err_host, unsigned long long timeout_ticks,
+                   hipStream_t st);
 }  // namespace pmd

@@ -14,9 +14,13 @@
 // only increases; slots are double-buffered by epoch parity, which is
 // enough because a rank can run at most one call ahead of any peer (it
 // cannot finish call e+1 before every peer has *started* e+1, i.e. finished
-// reading call e).  Spins are bounded: on timeout the kernel records an
-// error and returns garbage instead of hanging the GPU; the host checks the
-// error word (XgmiComm.check()).
+// reading call e).  Spins are bounded in WALL time (s_memrealtime, the
+// constant 100 MHz clock -- not an iteration count): on timeout the kernel
+// sets an error word in device memory AND a host-mapped word, then returns
+// instead of hanging the GPU.  The training loop reads the host-mapped word
+// after every step without any device sync (XgmiAllReduce.raise_if_failed)
+// and raises, so a timed-out exchange can never feed wrong statistics into
+// more than the step that produced them.
 #include "common.h"
 
 namespace pmd {
@@ -26,11 +30,28 @@ struct XgmiPeers {
   uint32_t* flags[kXgmiMaxRanks];
 };
 
+// Wait until the flag reaches epoch e; false (and both error words set) once
+// `ticks` of the constant wall clock have passed.
+__device__ __forceinline__ bool xgmi_wait_flag(const uint32_t* f, uint32_t e, unsigned long long ticks,
+                                               uint32_t* err, uint32_t* err_host) {
+  const unsigned long long t0 = (unsigned long long)wall_clock64();
+  while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+    if ((unsigned long long)wall_clock64() - t0 > ticks) {
+      atomicOr(err, 1u);
+      if (err_host) __hip_atomic_store(err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+
 __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(XgmiPeers peers, float* __restrict__ x,
                                                             int n, int rank, int world,
                                                             uint32_t* __restrict__ epochs,
                                                             uint32_t* __restrict__ err,
-                                                            long long spin_limit) {
+                                                            uint32_t* err_host,
+                                                            unsigned long long timeout_ticks) {
   __shared__ uint32_t e_sh;
   const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x;
   if (tid == 0) {
@@ -63,14 +84,7 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(XgmiPeers peers, fl
   // 3) wait until every rank's chunk for epoch e has landed in MY buffer
   if (tid < world) {
     const uint32_t* f = peers.flags[rank] + tid * kXgmiMaxBlocks + b;
-    long long it = 0;
-    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
-      if (++it > spin_limit) {
-        atomicOr(err, 1u);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
+    (void)xgmi_wait_flag(f, e, timeout_ticks, err, err_host);
   }
   __syncthreads();
   // 4) sum the W slots in rank order (identical on every rank)
@@ -84,8 +98,8 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(XgmiPeers peers, fl
 }
 
 int xgmi_allreduce_launch(float* const* data, uint32_t* const* flags, float* x, int n, int rank,
-                          int world, uint32_t* epochs, uint32_t* err, long long spin_limit,
-                          hipStream_t st) {
+                          int world, uint32_t* epochs, uint32_t* err, uint32_t* err_host,
+                          unsigned long long timeout_ticks, hipStream_t st) {
   if (world < 1 || world > kXgmiMaxRanks || n < 0 || n > kXgmiCap) return 1;
   if (n == 0) return 0;
   XgmiPeers p{};
@@ -95,7 +109,7 @@ int xgmi_allreduce_launch(float* const* data, uint32_t* const* flags, float* x, 
   }
   const int nb = (n + kXgmiArChunk - 1) / kXgmiArChunk;
   hipLaunchKernelGGL(xgmi_allreduce_kernel, dim3(nb), dim3(256), 0, st, p, x, n, rank, world, epochs,
-                     err, spin_limit);
+                     err, err_host, timeout_ticks);
   return 0;
 }
 
@@ -120,7 +134,8 @@ void xgmi_set_bn_pairs(int pairs) { g_bn_pairs = pairs < 1 ? 1 : (pairs > kBnPai
 
 __global__ __launch_bounds__(256) void xgmi_bn_kernel(XgmiPeers peers, XgmiBnArgs a, int rank, int world,
                                                      uint32_t* __restrict__ epochs,
-                                                     uint32_t* __restrict__ err, long long spin_limit) {
+                                                     uint32_t* __restrict__ err, uint32_t* err_host,
+                                                     unsigned long long timeout_ticks) {
   __shared__ float loc[kXgmiChunk];
   __shared__ uint32_t e_sh;
   const int b = blockIdx.x, tid = threadIdx.x;
@@ -187,14 +202,7 @@ __global__ __launch_bounds__(256) void xgmi_bn_kernel(XgmiPeers peers, XgmiBnArg
                        __HIP_MEMORY_SCOPE_SYSTEM);
   if (tid < world) {
     const uint32_t* f = peers.flags[rank] + tid * kXgmiMaxBlocks + b;
-    long long it = 0;
-    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
-      if (++it > spin_limit) {
-        atomicOr(err, 1u);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
+    (void)xgmi_wait_flag(f, e, timeout_ticks, err, err_host);
   }
   __syncthreads();
   // 4) global sums in rank order, then finalize / publish
@@ -237,7 +245,8 @@ __global__ __launch_bounds__(256) void xgmi_bn_kernel(XgmiPeers peers, XgmiBnArg
 }
 
 int xgmi_bn_launch(float* const* data, uint32_t* const* flags, const XgmiBnArgs& args, int rank, int world,
-                   uint32_t* epochs, uint32_t* err, long long spin_limit, hipStream_t st) {
+                   uint32_t* epochs, uint32_t* err, uint32_t* err_host, unsigned long long timeout_ticks,
+                   hipStream_t st) {
   if (world < 1 || world > kXgmiMaxRanks) return 1;
   const int P = args.CA + args.CB;
   XgmiBnArgs a = args;
@@ -254,7 +263,7 @@ int xgmi_bn_launch(float* const* data, uint32_t* const* flags, const XgmiBnArgs&
     p.flags[r] = flags[r];
   }
   hipLaunchKernelGGL(xgmi_bn_kernel, dim3(nb), dim3(256), 0, st, p, a, rank, world, epochs, err,
-                     spin_limit);
+                     err_host, timeout_ticks);
   return 0;
 }
 

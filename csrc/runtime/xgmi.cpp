@@ -38,12 +38,32 @@ class XgmiComm {
     HIP_OK(hipMalloc(reinterpret_cast<void**>(&epochs_), sizeof(uint32_t) * (kXgmiMaxBlocks + 1)));
     HIP_OK(hipMemset(epochs_, 0, sizeof(uint32_t) * (kXgmiMaxBlocks + 1)));
     err_ = epochs_ + kXgmiMaxBlocks;
+    // host-mapped error word: the kernels set it on a timeout, the training loop
+    // reads it after every step with no device synchronisation
+    HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&err_host_), sizeof(uint32_t),
+                         hipHostMallocMapped | hipHostMallocCoherent));
+    *err_host_ = 0;
+    HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_host_dev_), err_host_, 0));
     HIP_OK(hipDeviceSynchronize());
     peers_.assign(world, nullptr);
     peers_[rank] = buf_;
-    // ~timeout_s at roughly 64 polls per microsecond-ish s_sleep(1) granularity
-    spin_limit_ = static_cast<long long>(timeout_s * 1.0e6);
+    // the spin deadline is in ticks of the constant wall clock (s_memrealtime)
+    int khz = 0;
+    HIP_OK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, (int)device));
+    wall_khz_ = khz > 0 ? khz : 100000;
+    set_timeout(timeout_s);
   }
+
+  void set_timeout(double timeout_s) {
+    TORCH_CHECK(timeout_s > 0, "xgmi: timeout must be positive");
+    timeout_s_ = timeout_s;
+    timeout_ticks_ = static_cast<unsigned long long>(timeout_s * 1000.0 * wall_khz_);
+  }
+  double timeout() const { return timeout_s_; }
+  int64_t wall_clock_khz() const { return wall_khz_; }
+
+  // non-blocking: has any kernel (that finished so far) timed out on a peer?
+  bool failed() const { return __atomic_load_n(err_host_, __ATOMIC_ACQUIRE) != 0; }
 
   ~XgmiComm() {
     c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, device_));
@@ -51,6 +71,7 @@ class XgmiComm {
       if (r != rank_ && peers_[r]) (void)hipIpcCloseMemHandle(peers_[r]);
     if (buf_) (void)hipFree(buf_);
     if (epochs_) (void)hipFree(epochs_);
+    if (err_host_) (void)hipHostFree(err_host_);
   }
 
   pybind11::bytes handle() {
@@ -89,7 +110,7 @@ class XgmiComm {
     }
     c10::DeviceGuard g(x.device());
     const int rc = xgmi_allreduce_launch(data, flags, x.data_ptr<float>(), static_cast<int>(x.numel()),
-                                         rank_, world_, epochs_, err_, spin_limit_,
+                                         rank_, world_, epochs_, err_, err_host_dev_, timeout_ticks_,
                                          c10::hip::getCurrentHIPStream().stream());
     TORCH_CHECK(rc == 0, "xgmi: launch rejected");
     calls_++;
@@ -166,8 +187,8 @@ class XgmiComm {
       data[r] = reinterpret_cast<float*>(static_cast<char*>(peers_[r]) + kXgmiFlagBytes);
     }
     c10::DeviceGuard g(slots_a.device());
-    const int rc = xgmi_bn_launch(data, flags, a, rank_, world_, epochs_, err_, spin_limit_,
-                                  c10::hip::getCurrentHIPStream().stream());
+    const int rc = xgmi_bn_launch(data, flags, a, rank_, world_, epochs_, err_, err_host_dev_,
+                                  timeout_ticks_, c10::hip::getCurrentHIPStream().stream());
     TORCH_CHECK(rc == 0, "xgmi bn: launch rejected (", rc, ")");
     calls_++;
   }
@@ -190,7 +211,11 @@ class XgmiComm {
   uint32_t* epochs_ = nullptr;
   uint32_t* err_ = nullptr;
   std::vector<void*> peers_;
-  long long spin_limit_ = 0;
+  uint32_t* err_host_ = nullptr;      // host view of the mapped error word
+  uint32_t* err_host_dev_ = nullptr;  // device view of the same word
+  unsigned long long timeout_ticks_ = 0;
+  double timeout_s_ = 0.0;
+  int64_t wall_khz_ = 100000;
   bool opened_ = false;
   int64_t calls_ = 0;
 };
@@ -207,6 +232,10 @@ void register_xgmi(pybind11::module& m) {
       .def("all_reduce_", &XgmiComm::all_reduce_)
       .def("bn_", &XgmiComm::bn_)
       .def("check", &XgmiComm::check)
+      .def("failed", &XgmiComm::failed)
+      .def("set_timeout", &XgmiComm::set_timeout, py::arg("timeout_s"))
+      .def_property_readonly("timeout", &XgmiComm::timeout)
+      .def_property_readonly("wall_clock_khz", &XgmiComm::wall_clock_khz)
       .def_property_readonly("capacity", &XgmiComm::capacity)
       .def_property_readonly("calls", &XgmiComm::calls);
 }

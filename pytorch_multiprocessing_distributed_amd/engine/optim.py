@@ -32,6 +32,7 @@ class FusedSGD(torch.optim.Optimizer):
                         dampening=dampening)
         super().__init__(self.flat.params, defaults)
         self.momentum_arena = torch.zeros_like(self.flat.param_arena)
+        self.flat.companions.append(self.momentum_arena)   # follows arena relayouts
         self.steps = 0
         # device-resident learning rate: the SGD kernel reads it, so a captured
         # HIP graph of the step follows scheduler updates (see graph_safe())
@@ -71,12 +72,21 @@ class FusedSGD(torch.optim.Optimizer):
 
     # ------------------------------------------------------ resume state
     def state_dict(self):
-        return {"steps": self.steps, "momentum": self.momentum_arena.detach().cpu(),
+        # momentum per parameter name: independent of the arena layout (which the
+        # data-parallel wrapper re-orders after its first iteration)
+        mom = {n: self.momentum_arena[o: o + p.numel()].detach().cpu().clone()
+               for n, p, o in zip(self.flat.names, self.flat.params, self.flat.offsets)}
+        return {"steps": self.steps, "momentum": mom,
                 "param_groups": [{k: v for k, v in g.items() if k != "params"}
                                  for g in self.param_groups]}
 
     def load_state_dict(self, sd):
         self.steps = int(sd["steps"])
-        self.momentum_arena.copy_(sd["momentum"].to(self.momentum_arena.device))
+        mom = sd["momentum"]
+        if isinstance(mom, dict):
+            for n, p, o in zip(self.flat.names, self.flat.params, self.flat.offsets):
+                self.momentum_arena[o: o + p.numel()].copy_(mom[n].to(self.momentum_arena.device))
+        else:   # flat arena in construction order (older resume files)
+            self.momentum_arena.copy_(mom.to(self.momentum_arena.device))
         for g, s in zip(self.param_groups, sd["param_groups"]):
             g.update(s)

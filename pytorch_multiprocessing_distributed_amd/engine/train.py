@@ -77,6 +77,8 @@ def train_epoch(loader, model, optimizer, epoch, logger, args, rank, dev, comm=N
             loss.backward()
         with region("opt"):
             optimizer.step()
+        if comm is not None:
+            comm.raise_if_failed()      # xGMI SyncBN timeout of a finished step (no device sync)
         if comm is not None and comm.order_check_every and (step_offset + i) % comm.order_check_every == 0:
             comm.verify_order(model.collective_signature())
         bsz = inp.size(0)
@@ -86,6 +88,8 @@ def train_epoch(loader, model, optimizer, epoch, logger, args, rank, dev, comm=N
         top1.update(correct.float().squeeze(0) * (100.0 / bsz), bsz)
         if i % args.print_freq == 0 or i == n - 1:
             _sync(dev)
+            if comm is not None:
+                comm.raise_if_failed()
         batch_time.update(time.time() - end)
         end = time.time()
         if rank == 0 and i % args.print_freq == 0:
@@ -97,6 +101,8 @@ def train_epoch(loader, model, optimizer, epoch, logger, args, rank, dev, comm=N
                       epoch, i, n, batch_time=batch_time, data_time=data_time, loss=losses,
                       top1=top1), flush=True)
     _sync(dev)
+    if comm is not None:
+        comm.raise_if_failed()          # everything of this epoch has completed now
     elapsed = time.time() - t_epoch
     world = comm.world_size if comm is not None else 1
     ips = images * world / max(elapsed, 1e-9)

@@ -87,7 +87,17 @@ def run_model(main_fn, world_size, save_path=None, snapshot=None, args=()):
 
 
 def maybe_inject_fault(rank, step):
+    """Test hooks: ``PMD_FAULT_RANK``/``PMD_FAULT_STEP`` raise on
+    that rank at that step; ``PMD_FAULT_DELAY=rank:step:seconds`` makes that
+    rank a straggler (host sleep before the step), which drives its peers'
+    SyncBN exchanges into their timeout."""
     fr = os.environ.get("PMD_FAULT_RANK")
     fs = os.environ.get("PMD_FAULT_STEP")
     if fr is not None and fs is not None and int(fr) == rank and int(fs) == step:
         raise RuntimeError(f"injected fault on rank {rank} at step {step}")
+    fd = os.environ.get("PMD_FAULT_DELAY")
+    if fd:
+        r, s, sec = fd.split(":")
+        if int(r) == rank and int(s) == step:
+            import time
+            time.sleep(float(sec))

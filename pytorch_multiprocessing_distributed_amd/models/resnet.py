@@ -220,7 +220,9 @@ class ResNet(nn.Module):
             return None
         ws = self.__dict__.get("_pmd_wset")
         f8 = OF.get_fp8()
-        key = (x.shape[-1], self.conv1.weight.data_ptr(), self.linear.weight.data_ptr(), id(f8))
+        fl = self.__dict__.get("_pmd_flat")
+        key = (x.shape[-1], self.conv1.weight.data_ptr(), self.linear.weight.data_ptr(), id(f8),
+               fl.version if fl is not None else -1)
         if ws is None or self.__dict__.get("_pmd_wset_key") != key:
             entries = [(self.conv1, x.shape[-1], False)]
             for mod in self.modules():

@@ -310,6 +310,15 @@ def _wgrad_flush():
         _join_pending(pend)
 
 
+def flush_pending_wgrads():
+    """Join every side-stream weight gradient still deferred and mark those
+    weights ready.  The data-parallel reducer calls this at the START of its
+    end-of-backward finalize (before it force-launches any bucket), so no
+    bucket is ever all-reduced while its gradients are still being written and
+    every deferred weight is marked inside the iteration it belongs to."""
+    _wgrad_flush()
+
+
 def _bn_acc(bn):
     """(d_beta, d_gamma) arena targets for a BN module, or None."""
     tb, tg = _grad_target(bn.bias), _grad_target(bn.weight)

@@ -62,10 +62,17 @@ class Comm:
         text = f"{self._seq}:{self._ncoll}:{list(extra)}"
         self.check_same(text, "collective sequence")
 
-    def enable_xgmi(self, timeout_s: float = 60.0):
+    def raise_if_failed(self):
+        """Cheap per-step health check (no device sync): xGMI exchange timeouts."""
+        if self.xgmi is not None:
+            self.xgmi.raise_if_failed()
+
+    def enable_xgmi(self, timeout_s: float | None = None):
         """Route small fp32 GPU all-reduces (SyncBN statistics) through the
         one-shot xGMI kernel (parallel/xgmi.py).  Collective: every rank calls it."""
         from .xgmi import XgmiAllReduce
+        if timeout_s is None:
+            timeout_s = float(os.environ.get("PMD_XGMI_TIMEOUT", "60"))
         self.xgmi = XgmiAllReduce(self.group, timeout_s)
         return self.xgmi
 

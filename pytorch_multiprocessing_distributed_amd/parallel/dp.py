@@ -6,26 +6,37 @@ What it does:
     re-homes parameters/grads into flat arenas (:mod:`.flat`), then
     broadcasts the parameter arena and all buffers from rank 0 in one
     collective per dtype (C3) -- replicas start identical (README.md:6);
-  * backward: gradients accumulate straight into the grad arena; a
-    post-accumulate hook counts readiness per bucket and, when a bucket is
-    complete, launches an asynchronous in-place *average* all-reduce on it
-    (RCCL ``ncclAvg`` over xGMI; pre-scale + SUM on gloo), overlapping the
-    rest of backward.  Buckets are contiguous arena slices in reverse
-    registration order with a small first bucket (DDP: 1 MiB first / 25 MiB
-    rest; defaults here are sized for xGMI rings, see ``bucket_mb``);
-  * end of backward (autograd engine callback): waits on every bucket's Work
-    (a stream-side wait, no host block) and checks each bucket fired exactly
-    once (race / double-launch detector, SURVEY §5.2);
+  * backward: gradients accumulate straight into the grad arena; a hook
+    counts readiness per bucket and buckets are launched as asynchronous
+    in-place *average* all-reduces strictly in bucket-index order (a
+    cursor, like DDP's ``next_bucket``: every rank issues the identical
+    collective sequence), overlapping the rest of backward.  Buckets are
+    contiguous arena slices with a small first bucket (DDP: 1 MiB first /
+    25 MiB rest; sized here for xGMI rings, see ``bucket_mb``);
+  * after the first iteration the arena is re-laid out in the OBSERVED
+    gradient-ready order (rank 0's order, broadcast) and the buckets are
+    rebuilt over it -- torch's Reducer does the same
+    (torch:nn/parallel/distributed.py:1551, ``_rebuild_buckets``);
+  * end of backward (autograd engine callback): joins the side-stream weight
+    gradients still pending (``functional.flush_pending_wgrads``, BEFORE any
+    bucket is force-launched), waits on every bucket (stream-side, no host
+    block) and checks each bucket fired exactly once (SURVEY §5.2);
+  * transport: ``"c10d"`` -- the torch process group (RCCL via
+    ProcessGroupNCCL on GPU, gloo on CPU) -- or ``"rccl"`` -- the framework's
+    own RCCL communicator (csrc/runtime/rccl_comm.cpp: uniqueId over the
+    TCPStore, its own HIP stream, hipEvent fences);
   * the bucket bookkeeping + collective launch runs in the native C++
-    ``_C.Reducer`` (csrc/runtime/reducer.cpp) over the c10d process group
-    (RCCL on GPU, gloo on CPU); ``reducer="python"`` keeps an equivalent
-    pure-Python implementation for debugging / cross-checking;
+    ``_C.Reducer`` (csrc/runtime/reducer.cpp); ``reducer="python"`` keeps an
+    equivalent pure-Python implementation for debugging / cross-checking;
   * ``compress="bf16"`` sends gradients over the wire in bf16 (half the xGMI
     bytes, fp32 arena kept);
   * ``no_sync()`` skips communication for gradient accumulation;
   * ``broadcast_buffers=True`` re-broadcasts BN buffers from rank 0 before
     each training forward (reference DDP default, C4); off by default since
-    SyncBN keeps them identical.
+    SyncBN keeps them identical;
+  * ``timeline=True`` (or ``PMD_REDUCER_TIMELINE=1``) records each bucket's
+    launch time and, on the RCCL transport, its device start/end relative to
+    the end of backward (``bucket_timeline()``).
 
 ``state_dict()`` carries the ``module.`` prefix exactly like the reference's
 DDP checkpoint (main.py:77).
@@ -33,6 +44,7 @@ DDP checkpoint (main.py:77).
 from __future__ import annotations
 
 import contextlib
+import os
 
 import torch
 import torch.distributed as dist
@@ -55,62 +67,79 @@ class _Bucket:
         self.fired = 0
 
 
+def _flush_wgrads():
+    from ..ops.functional import flush_pending_wgrads
+    flush_pending_wgrads()
+
+
 class DataParallel(nn.Module):
     def __init__(self, module: nn.Module, comm: Comm | None = None, bucket_mb: float = 25.0,
                  first_bucket_mb: float = 1.0, broadcast_buffers: bool = False,
-                 check_collectives: bool = True, reducer: str = "native", compress: str = "none"):
+                 check_collectives: bool = True, reducer: str = "native", compress: str = "none",
+                 transport: str = "c10d", rebuild_buckets: bool = True, timeline: bool | None = None):
         super().__init__()
         self.module = module
         self.comm = comm
         self.world_size = comm.world_size if comm is not None else 1
         self.broadcast_buffers = broadcast_buffers
         self.check_collectives = check_collectives
+        self.bucket_mb, self.first_bucket_mb = bucket_mb, first_bucket_mb
+        if reducer not in ("native", "python") or compress not in ("none", "bf16") \
+                or transport not in ("c10d", "rccl"):
+            raise ValueError(f"bad reducer/compress/transport: {reducer!r}/{compress!r}/{transport!r}")
         if comm is not None:
             desc = ";".join(f"{n}:{tuple(p.shape)}" for n, p in module.named_parameters())
             comm.check_same(desc, "parameter names/shapes")
         self.flat = flatten_module(module)
-        self._build_buckets(bucket_mb, first_bucket_mb)
+        self._build_buckets()
+        self.rccl = None
+        if comm is not None and transport == "rccl":
+            if reducer != "native" or comm.backend != "nccl":
+                raise ValueError("transport='rccl' needs the native reducer and GPU ranks")
+            from . import rccl
+            self.rccl = rccl.create(comm.group)
         if comm is not None:
             self._sync_module_states()
         self._sync_enabled = True
         self._callback_queued = False
         self._marked = [False] * len(self.flat.params)
+        self._marks, self._last_marks, self._next = [], [], 0   # python reducer state
         self._hooks = []
-        if reducer not in ("native", "python") or compress not in ("none", "bf16"):
-            raise ValueError(f"bad reducer/compress: {reducer!r}/{compress!r}")
         self.reducer_kind = reducer if comm is not None else None
         self.compress = compress
+        self.transport = transport if comm is not None else None
+        self.timeline = (os.environ.get("PMD_REDUCER_TIMELINE", "0") == "1") if timeline is None \
+            else bool(timeline)
         self._native = None
+        self._rebuild_pending = bool(rebuild_buckets) and comm is not None
+        self.rebuilt_order = None
         if comm is not None and reducer == "native":
             from ..ops.native import C
-            bounds = [b.start for b in self.buckets] + [self.flat.numel]
-            pbucket = [self._param_bucket[i].index for i in range(len(self.flat.params))]
-            pg = comm.group if comm.group is not None else dist.group.WORLD
-            self._native = C.Reducer(pg, self.flat.grad_arena, bounds, pbucket,
-                                     comm.supports_avg, compress == "bf16")
+            pg = None
+            if self.rccl is None:
+                pg = comm.group if comm.group is not None else dist.group.WORLD
+            bounds, pbucket = self._bounds()
+            self._native = C.Reducer(pg, self.rccl, self.flat.grad_arena, bounds, pbucket,
+                                     comm.supports_avg, compress == "bf16", _flush_wgrads,
+                                     self.timeline)
         elif comm is not None and compress != "none":
             raise ValueError("compress requires the native reducer")
         if comm is not None:
-            for i, p in enumerate(self.flat.params):
-                h = self._make_native_hook(i) if self._native is not None else self._make_hook(i)
-                # AccumulateGrad path (params whose grad is returned to autograd) ...
-                self._hooks.append(p.register_post_accumulate_grad_hook(h))
-                # ... and the direct path (fused ops that wrote into the arena call this)
-                p._pmd_ready = h
+            self._install_hooks()
         self.iteration = 0
 
     # ------------------------------------------------------------ buckets
-    def _build_buckets(self, bucket_mb, first_mb):
+    def _build_buckets(self):
         fp = self.flat
         groups, cur, nbytes = [], [], 0
-        cap = int(first_mb * 2 ** 20)
+        cap = int(self.first_bucket_mb * 2 ** 20)
         for i, p in enumerate(fp.params):
             cur.append(i)
             nbytes += p.numel() * p.element_size()
             if nbytes >= cap:
                 groups.append(cur)
                 cur, nbytes = [], 0
-                cap = int(bucket_mb * 2 ** 20)
+                cap = int(self.bucket_mb * 2 ** 20)
         if cur:
             groups.append(cur)
         # bucket = contiguous arena slice from its first param to the next bucket's start
@@ -121,13 +150,57 @@ class DataParallel(nn.Module):
             for i in b.params:
                 self._param_bucket[i] = b
 
+    def _bounds(self):
+        bounds = [b.start for b in self.buckets] + [self.flat.numel]
+        pbucket = [self._param_bucket[i].index for i in range(len(self.flat.params))]
+        return bounds, pbucket
+
     def bucket_sizes_mb(self):
         return [(b.end - b.start) * 4 / 2 ** 20 for b in self.buckets]
+
+    def _install_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        for i, p in enumerate(self.flat.params):
+            h = self._make_native_hook(i) if self._native is not None else self._make_hook(i)
+            # AccumulateGrad path (params whose grad is returned to autograd) ...
+            self._hooks.append(p.register_post_accumulate_grad_hook(h))
+            # ... and the direct path (fused ops that wrote into the arena call this)
+            p._pmd_ready = h
+
+    def _maybe_rebuild(self):
+        """Once, before the second iteration: re-lay the arena out in the order
+        gradients became ready in iteration 1 (rank 0's observation, broadcast so
+        every rank builds the identical layout) and rebuild the buckets."""
+        self._rebuild_pending = False
+        if self._native is not None:
+            seen = list(self._native.last_mark_order())
+        else:
+            seen = list(self._last_marks)
+        n = len(self.flat.params)
+        order = seen + [i for i in range(n) if i not in set(seen)]   # unused params last
+        t = torch.tensor(order, dtype=torch.int64,
+                         device=self.flat.device if self.comm.backend == "nccl" else "cpu")
+        self.comm.broadcast_(t, 0)
+        order = [int(v) for v in t.tolist()]
+        self.rebuilt_order = [self.flat.names[i] for i in order]
+        if order == list(range(n)):
+            return
+        self.flat.relayout(order)
+        self._build_buckets()
+        if self._native is not None:
+            self._native.rebuild(*self._bounds())
+        self._marked = [False] * n
+        self._install_hooks()
 
     # --------------------------------------------------------- state sync
     @torch.no_grad()
     def _sync_module_states(self):
-        self.comm.broadcast_(self.flat.param_arena, 0)
+        if self.rccl is not None:
+            self.rccl.broadcast_(self.flat.param_arena, 0)
+        else:
+            self.comm.broadcast_(self.flat.param_arena, 0)
         self._broadcast_buffers()
 
     @torch.no_grad()
@@ -153,13 +226,15 @@ class DataParallel(nn.Module):
             if not self._sync_enabled or self._marked[i]:
                 return
             self._marked[i] = True
+            self._marks.append(i)
             if not self._callback_queued:
                 self._callback_queued = True
                 torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
             b = self._param_bucket[i]
             b.pending -= 1
-            if b.pending == 0:
-                self._launch(b)
+            while self._next < len(self.buckets) and self.buckets[self._next].pending == 0:
+                self._launch(self.buckets[self._next])
+                self._next += 1
         return hook
 
     def _make_native_hook(self, i):
@@ -176,10 +251,11 @@ class DataParallel(nn.Module):
         b.work = self.comm.all_reduce_mean_async(self.flat.grad_arena[b.start: b.end])
 
     def _finalize(self):
+        _flush_wgrads()          # deferred side-stream weight grads are marked first
         # params that received no gradient this iteration (unused): launch their bucket anyway
-        for b in self.buckets:
-            if b.work is None:
-                self._launch(b)
+        while self._next < len(self.buckets):
+            self._launch(self.buckets[self._next])
+            self._next += 1
         for b in self.buckets:
             b.work.wait()
         if self.check_collectives:
@@ -191,6 +267,9 @@ class DataParallel(nn.Module):
             b.fired = 0
             b.pending = len(b.params)
         self._marked = [False] * len(self.flat.params)
+        self._last_marks = self._marks
+        self._marks = []
+        self._next = 0
         self._callback_queued = False
         self.iteration += 1
 
@@ -214,16 +293,31 @@ class DataParallel(nn.Module):
             return self._native.last_launch_order()
         return []
 
+    def bucket_timeline(self):
+        """Last iteration: [(bucket, host launch us after first mark, host finalize us,
+        device start ms, device end ms)], device times relative to the end of the
+        backward's compute work (negative = overlapped), NaN where unavailable."""
+        if self._native is None:
+            return []
+        return [tuple(r) for r in self._native.timeline()]
+
     @property
     def num_iterations(self):
         return self._native.iteration if self._native is not None else self.iteration
 
     # ------------------------------------------------------------- forward
     def forward(self, *args, **kwargs):
-        if self.comm is not None and self.broadcast_buffers and self.module.training \
-                and torch.is_grad_enabled():
-            self._broadcast_buffers()
+        if self.comm is not None and self.module.training and torch.is_grad_enabled():
+            if self._rebuild_pending and self.num_iterations >= 1:
+                self._maybe_rebuild()
+            if self.broadcast_buffers:
+                self._broadcast_buffers()
         return self.module(*args, **kwargs)
 
     def zero_grad(self, set_to_none: bool = False):
         self.flat.zero_grad()
+
+    def shutdown(self):
+        """Abort the native communicator (peers blocked in a collective error out)."""
+        if self.rccl is not None:
+            self.rccl.abort()

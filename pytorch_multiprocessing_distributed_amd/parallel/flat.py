@@ -14,6 +14,12 @@ also the order torch's DDP Reducer builds buckets in
 
 Parameter logical shapes/strides are preserved (conv weights keep their
 channels-last strides), so state_dict keys/shapes are unchanged.
+
+:meth:`FlatParams.relayout` re-orders the arenas in place (same storage) once
+the data-parallel wrapper has OBSERVED the order gradients become ready in
+(torch's Reducer rebuilds its buckets after the first iteration the same way,
+torch:nn/parallel/distributed.py:1551); optimizer state arenas registered as
+``companions`` are permuted with them.
 """
 from __future__ import annotations
 
@@ -51,6 +57,8 @@ class FlatParams:
             off += (p.numel() + _ALIGN - 1) // _ALIGN * _ALIGN
         self.numel = off
         self.device = dev
+        self.version = 0          # bumped by relayout(): parameter storage moved
+        self.companions = []      # same-layout state arenas (optimizer momentum)
         self.param_arena = torch.zeros(off, dtype=dtype, device=dev)
         self.grad_arena = torch.zeros(off, dtype=dtype, device=dev)
         with torch.no_grad():
@@ -71,6 +79,36 @@ class FlatParams:
     def slice_of(self, i):
         o = self.offsets[i]
         return o, o + self.params[i].numel()
+
+    @torch.no_grad()
+    def relayout(self, order):
+        """Re-order the arenas so parameter ``order[k]`` (current index) comes
+        k-th; contents move in place (no reallocation), ``p.data``/``p.grad``
+        are re-pointed.  Returns nothing; ``self.params``/``names``/``offsets``
+        follow the new order and ``version`` increments."""
+        order = [int(i) for i in order]
+        if sorted(order) != list(range(len(self.params))):
+            raise ValueError("relayout: order must be a permutation of the parameter indices")
+        if order == list(range(len(self.params))):
+            return
+        new_params = [self.params[i] for i in order]
+        new_offsets, off = [], 0
+        for p in new_params:
+            new_offsets.append(off)
+            off += (p.numel() + _ALIGN - 1) // _ALIGN * _ALIGN
+        assert off == self.numel
+        for arena in [self.param_arena, self.grad_arena, *self.companions]:
+            tmp = arena.clone()
+            for i, no in zip(order, new_offsets):
+                oo, n = self.offsets[i], self.params[i].numel()
+                arena[no: no + n].copy_(tmp[oo: oo + n])
+        for p, o in zip(new_params, new_offsets):
+            p.data = self._view(self.param_arena, p, o)
+            p.grad = self._view(self.grad_arena, p, o)
+        self.names = [self.names[i] for i in order]
+        self.params = new_params
+        self.offsets = new_offsets
+        self.version += 1
 
     def zero_grad(self):
         self.grad_arena.zero_()

@@ -1,0 +1,49 @@
+"""Native RCCL communicator bootstrap (reference
+main.py:190-193, where ``init_process_group('nccl')`` hides all of this).
+
+``init_process_group`` has already created the c10d TCPStore on
+``MASTER_ADDR:MASTER_PORT``; it is the only piece borrowed from c10d.  Rank 0
+calls ``ncclGetUniqueId`` and publishes the 128-byte id under a fresh store
+key; every rank reads it and calls ``ncclCommInitRank`` on its own HIP device
+(csrc/runtime/rccl_comm.cpp).  The resulting communicator owns one HIP
+stream of the requested priority; the gradient reducer launches its bucket
+all-reduces there, fenced with HIP events (no host blocking).
+"""
+from __future__ import annotations
+
+import itertools
+
+import torch
+import torch.distributed as dist
+
+_SEQ = itertools.count()
+
+
+def _store():
+    from torch.distributed import distributed_c10d as c10d
+    return c10d._get_default_store()
+
+
+def create(group=None, priority: int = 0, store=None):
+    """Collective over ``group`` (every rank calls it).  Returns ``_C.RcclComm``."""
+    from ..ops.native import C
+    if not dist.is_initialized():
+        raise RuntimeError("torch.distributed must be initialised first (it hosts the TCPStore)")
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    store = store if store is not None else _store()
+    key = f"pmd_rccl_uid_{next(_SEQ)}"
+    if rank == 0:
+        store.set(key, C.RcclComm.unique_id())
+    uid = store.get(key)                      # blocks until rank 0 published it
+    dev = torch.cuda.current_device()
+    comm = C.RcclComm(bytes(uid), rank, world, dev, priority)
+    return comm
+
+
+def create_single(device: int | None = None, priority: int = 0):
+    """A one-rank communicator (no process group needed): exercises the real
+    RCCL launch / stream / event path on one GPU (tests, W=1 benches)."""
+    from ..ops.native import C
+    dev = torch.cuda.current_device() if device is None else device
+    return C.RcclComm(bytes(C.RcclComm.unique_id()), 0, 1, dev, priority)

@@ -78,6 +78,18 @@ class XgmiAllReduce:
         if not self._c.check():
             raise RuntimeError(f"xGMI all-reduce timed out waiting for a peer (rank {self.rank})")
 
+    def raise_if_failed(self):
+        """Non-blocking health check (host-mapped error word, no device sync):
+        raises if any exchange that has COMPLETED so far timed out on a peer.
+        The training loop calls it after every step; a timed-out exchange has
+        produced wrong statistics, so training must not continue."""
+        if self._c.failed():
+            raise RuntimeError(f"xGMI SyncBN exchange timed out waiting for a peer (rank {self.rank}, "
+                               f"timeout {self._c.timeout:.3g} s): statistics of that step are invalid")
+
+    def set_timeout(self, seconds: float):
+        self._c.set_timeout(float(seconds))
+
     @property
     def calls(self):
         return self._c.calls

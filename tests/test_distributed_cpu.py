@@ -48,6 +48,11 @@ def _data(seed=3):
     return x, y
 
 
+def _grads(dp):
+    # by name: the data-parallel arena is re-laid out in ready order after iteration 1
+    return {n: p.grad.detach().clone() for n, p in dp.module.named_parameters()}
+
+
 def _worker(rank, world, port, out_path, reducer="native", compress="none"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -73,7 +78,7 @@ def _worker(rank, world, port, out_path, reducer="native", compress="none"):
     comm.all_reduce_(gl[0])
     if rank == 0:
         torch.save({"state": dp.module.state_dict(), "loss": gl[0] / world,
-                    "grad": dp.flat.grad_arena.clone()}, out_path)
+                    "grad": _grads(dp), "order": dp.rebuilt_order}, out_path)
     OF.set_bn_sync(None)
     dist.destroy_process_group()
 
@@ -96,7 +101,12 @@ def test_two_rank_step_equals_single_process(tmp_path, reducer):
         torch.testing.assert_close(got["state"][k], v, rtol=1e-7, atol=1e-9, msg=k)
     # per-rank mean loss averaged over ranks == global-batch loss
     torch.testing.assert_close(got["loss"], torch.stack(losses), rtol=1e-9, atol=1e-9)
-    torch.testing.assert_close(got["grad"], dp.flat.grad_arena, rtol=1e-6, atol=1e-9)
+    for n, g in _grads(dp).items():
+        torch.testing.assert_close(got["grad"][n], g, rtol=1e-6, atol=1e-9, msg=n)
+    # the arena was re-laid out in the observed gradient-ready order: the linear
+    # layer (first node of backward) leads, the stem conv comes last
+    assert got["order"] is not None and got["order"][0].startswith("linear")
+    assert got["order"][-1] in ("conv1.weight", "bn1.weight", "bn1.bias")
 
 
 @pytest.mark.slow
@@ -111,7 +121,8 @@ def test_two_rank_bf16_wire_compression(tmp_path):
     ref_model = build_model("res").double()
     x, y = _data()
     dp, _ = _run_steps(ref_model, x, y, 2, None)
-    g, r = got["grad"], dp.flat.grad_arena
+    g = torch.cat([got["grad"][n].flatten() for n, _ in dp.module.named_parameters()])
+    r = torch.cat([p.grad.flatten() for _, p in dp.module.named_parameters()])
     assert ((g - r).norm() / r.norm()).item() < 5e-2   # 2 steps of bf16-rounded averages
 
 
