@@ -78,24 +78,26 @@ def _defer_worker(rank, world, port, out, defer):
     torch.manual_seed(0)
     model = build_model("resnet50", num_classes=10, stem="imagenet").cuda()
     dp = DataParallel(model, comm, bucket_mb=2.0, first_bucket_mb=0.5)
-    p0 = {n: p.detach().float().clone() for n, p in dp.module.named_parameters()}
-    opt = FusedSGD(dp, lr=0.05, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    # lr=0: the weights stay fixed, so every step's averaged gradients must agree
+    # between the deferred and the per-block join (a race on the last bucket, or
+    # a double all-reduce, shows up in ANY of the three steps)
+    opt = FusedSGD(dp, lr=0.0, momentum=0.9, nesterov=True)
     x, y = _data(8, 64)
     per = x.shape[0] // world
     xs, ys = x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per]
-    launches = []
+    launches, grads = [], []
     for _ in range(3):
         loss = OF.cross_entropy(dp(xs), ys)
         opt.zero_grad()
         loss.backward()
         opt.step()
         launches.append(list(dp.collective_signature()))
+        grads.append({n: p.grad.detach().float().cpu() for n, p in dp.module.named_parameters()})
     torch.cuda.synchronize()
     comm.xgmi.check()
     if rank == 0:
-        upd = {n: (p.detach().float() - p0[n]).cpu() for n, p in dp.module.named_parameters()}
         torch.save({"iters": dp.num_iterations, "nb": len(dp.buckets), "launches": launches,
-                    "params": upd, "loss": float(loss)}, out)
+                    "grads": grads, "loss": float(loss)}, out)
     OF.set_bn_sync(None)
     dist.destroy_process_group()
 
@@ -116,12 +118,13 @@ def test_deferred_wgrad_buckets_fire_once_and_match(tmp_path):
             assert order == list(range(len(order))), (defer, it, order)  # each once, index order
             if it > 0:
                 assert len(order) == r["nb"], (defer, it, order)
-    # same 3-step parameter update with and without the deferred join (up to
-    # run-to-run fp32-atomics ordering noise, amplified by bf16 rounding)
-    a, b = res[1]["params"], res[0]["params"]
-    num = sum(((a[k] - b[k]) ** 2).sum() for k in a)
-    den = sum((b[k] ** 2).sum() for k in b)
-    assert (num / den).sqrt().item() < 5e-2, (num / den).sqrt().item()
+    # same averaged gradients at every step with and without the deferred join,
+    # up to run-to-run fp32-atomic summation order in the split-K weight gradients
+    # (~1e-3 global relative L2; a double all-reduce is a factor 2, a torn bucket O(1))
+    for step, (a, b) in enumerate(zip(res[1]["grads"], res[0]["grads"])):
+        num = sum(((a[k] - b[k]) ** 2).sum() for k in a)
+        den = sum((b[k] ** 2).sum() for k in b)
+        assert (num / den).sqrt().item() < 1e-2, (step, (num / den).sqrt().item())
 
 
 # ------------------------------------------------------------- native RCCL comm
@@ -183,7 +186,9 @@ def test_native_rccl_comm_single_rank_reducer():
 def _straggler_worker(rank, world, port, out):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    os.environ["PMD_FAULT_DELAY"] = "1:1:4"          # rank 1 sleeps 4 s before step 1
+    # rank 1 sleeps 4 s before step 2 (step 1 begins with the host-side broadcast of
+    # the bucket rebuild order, which would re-align the ranks on the host)
+    os.environ["PMD_FAULT_DELAY"] = "1:2:4"
     import datetime
     import torch.distributed as dist
     from pytorch_multiprocessing_distributed_amd import launch
@@ -195,7 +200,7 @@ def _straggler_worker(rank, world, port, out):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
     comm = get_comm()
-    comm.enable_xgmi(timeout_s=20.0)    # step 0 (per-rank kernel autotuning) at a safe timeout
+    comm.enable_xgmi(timeout_s=20.0)    # steps 0-1 (per-rank kernel autotuning) at a safe timeout
     OF.set_bn_sync(comm)
     torch.manual_seed(0)
     dp = DataParallel(build_model("res").cuda(), comm, bucket_mb=1.0)
@@ -213,7 +218,7 @@ def _straggler_worker(rank, world, port, out):
             torch.cuda.synchronize()
             comm.raise_if_failed()
             steps_done += 1
-            if i == 0:
+            if i == 1:
                 comm.barrier()
                 comm.xgmi.set_timeout(0.5)
     except Exception as e:  # noqa: BLE001
@@ -230,7 +235,7 @@ def test_straggler_timeout_raises(tmp_path):
     assert _join_all(ctx, 180)
     r0 = json.load(open(f"{out}.0"))
     assert "timed out" in r0["err"], r0
-    assert r0["steps"] == 1, r0      # step 0 fine, step 1 detected, no step 2
+    assert r0["steps"] == 2, r0      # steps 0-1 fine, step 2 detected, no step 3
 
 
 # ------------------------------------------- spinning kernels on two streams
