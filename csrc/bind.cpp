@@ -53,12 +53,21 @@ float* opt_f32(const c10::optional<Tensor>& t, const char* what) {
   return t->data_ptr<float>();
 }
 
+// BatchNorm statistics shift [C] (nullable)
+float* shift_ptr(const c10::optional<Tensor>& t, int64_t C) {
+  float* p = opt_f32(t, "BN statistics shift");
+  if (p) TORCH_CHECK(t->numel() == C, "BN statistics shift must have one value per channel");
+  return p;
+}
+
 // stats_buf: optional pre-zeroed [S,2,K] slot buffer (pool); allocated zeroed otherwise
 // out_h/out_w < 0: the usual (H + 2 pad - R) / stride + 1; otherwise an explicit
 // (cropped) output extent -- the space-to-depth stem's 4x4 conv pads 2 rows on
 // the top but only 1 at the bottom, i.e. the last full-pad output row is dropped
+// shift: optional fp32 [K] BatchNorm statistics shift (the stats are taken about it, bn_moments)
 static std::vector<Tensor> conv_fwd_impl(Tensor x, Tensor wk, int64_t stride, int64_t pad, bool want_stats,
-                                         c10::optional<Tensor> stats_buf, int64_t out_h, int64_t out_w) {
+                                         c10::optional<Tensor> stats_buf, int64_t out_h, int64_t out_w,
+                                         const c10::optional<Tensor>& shift) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_CONT(x);
   CHECK_DEV(wk); CHECK_BF16(wk); CHECK_CONT(wk);
   TORCH_CHECK(x.dim() == 4 && wk.dim() == 4, "x [N,H,W,C], wk [K,R,S,C]");
@@ -80,23 +89,25 @@ static std::vector<Tensor> conv_fwd_impl(Tensor x, Tensor wk, int64_t stride, in
       stats = torch::zeros({pmd_slots(), 2, K}, x.options().dtype(torch::kFloat32));
     }
   }
+  const float* shp = shift_ptr(shift, K);
   const int rc = pmd::conv_igemm_launch(bfp(x), bfp(wk), bfp_mut(y),
                                         want_stats ? stats.data_ptr<float>() : nullptr, N, H, W, C, P,
                                         Q, K, R, S, (int)stride, (int)pad, false, nullptr, nullptr, nullptr,
-                                        cur_stream());
+                                        cur_stream(), shp);
   CHECK_RC(rc, "conv_fwd");
   if (want_stats) return {y, stats};
   return {y};
 }
 
 std::vector<Tensor> conv_fwd(Tensor x, Tensor wk, int64_t stride, int64_t pad, bool want_stats,
-                             c10::optional<Tensor> stats_buf) {
-  return conv_fwd_impl(x, wk, stride, pad, want_stats, stats_buf, -1, -1);
+                             c10::optional<Tensor> stats_buf, c10::optional<Tensor> shift) {
+  return conv_fwd_impl(x, wk, stride, pad, want_stats, stats_buf, -1, -1, shift);
 }
 
 std::vector<Tensor> conv_fwd_hw(Tensor x, Tensor wk, int64_t stride, int64_t pad, int64_t out_h,
-                                int64_t out_w, bool want_stats, c10::optional<Tensor> stats_buf) {
-  return conv_fwd_impl(x, wk, stride, pad, want_stats, stats_buf, out_h, out_w);
+                                int64_t out_w, bool want_stats, c10::optional<Tensor> stats_buf,
+                                c10::optional<Tensor> shift) {
+  return conv_fwd_impl(x, wk, stride, pad, want_stats, stats_buf, out_h, out_w, shift);
 }
 
 // ----------------------------------------------------------- s2d stem
@@ -172,7 +183,7 @@ Tensor winograd_input(Tensor x) {
 }
 
 std::vector<Tensor> winograd_output(Tensor M, int64_t N, int64_t H, int64_t W, bool want_stats,
-                                    c10::optional<Tensor> stats_buf) {
+                                    c10::optional<Tensor> stats_buf, c10::optional<Tensor> shift) {
   CHECK_DEV(M); CHECK_BF16(M); CHECK_CONT(M);
   const int64_t T = N * ((H + 1) / 2) * ((W + 1) / 2);
   TORCH_CHECK(M.dim() == 3 && M.size(0) == 16 && M.size(1) == T, "M must be [16, tiles, K]");
@@ -190,7 +201,7 @@ std::vector<Tensor> winograd_output(Tensor M, int64_t N, int64_t H, int64_t W, b
     }
   }
   CHECK_RC(pmd::winograd_output_launch(bfp(M), bfp_mut(y), want_stats ? stats.data_ptr<float>() : nullptr,
-                                       (int)N, (int)H, (int)W, K, cur_stream()),
+                                       (int)N, (int)H, (int)W, K, cur_stream(), shift_ptr(shift, K)),
            "winograd_output");
   if (want_stats) return {y, stats};
   return {y};
@@ -292,7 +303,7 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int64_t R, int64_t S, int64_t stride, int
 // -------------------------------------------------------------------- BN
 Tensor bn_finalize(c10::optional<Tensor> sums, c10::optional<Tensor> count, Tensor gamma, Tensor beta, double eps,
                    c10::optional<Tensor> rm, c10::optional<Tensor> rv, double momentum,
-                   c10::optional<Tensor> nbt, bool eval_mode) {
+                   c10::optional<Tensor> nbt, bool eval_mode, c10::optional<Tensor> shift) {
   CHECK_DEV(gamma); CHECK_F32(gamma);
   const int C = gamma.numel();
   c10::DeviceGuard g(gamma.device());
@@ -313,8 +324,9 @@ Tensor bn_finalize(c10::optional<Tensor> sums, c10::optional<Tensor> count, Tens
   Tensor gm = gamma.contiguous(), bt = beta.contiguous();
   pmd::bn_finalize_launch(eval_mode ? nullptr : s.data_ptr<float>(),
                           eval_mode ? nullptr : cnt.data_ptr<float>(), gm.data_ptr<float>(),
-                          bt.data_ptr<float>(), params.data_ptr<float>(), rmp, rvp, nb, C, (float)eps,
-                          (float)momentum, eval_mode, cur_stream());
+                          bt.data_ptr<float>(), params.data_ptr<float>(), rmp, rvp, nb,
+                          eval_mode ? nullptr : shift_ptr(shift, C), C, (float)eps, (float)momentum,
+                          eval_mode, cur_stream());
   return params;
 }
 
@@ -351,7 +363,7 @@ Tensor stats_collapse(Tensor a, c10::optional<Tensor> b, c10::optional<double> c
 // collapse(+clear) slot stats and finalize BN params in one launch (no all-reduce case)
 Tensor stats_finalize_local(Tensor slots, double count, Tensor gamma, Tensor beta, double eps,
                             c10::optional<Tensor> rm, c10::optional<Tensor> rv, double momentum,
-                            c10::optional<Tensor> nbt) {
+                            c10::optional<Tensor> nbt, c10::optional<Tensor> shift) {
   CHECK_DEV(slots); CHECK_F32(slots); CHECK_CONT(slots);
   const int C = gamma.numel();
   TORCH_CHECK(slots.numel() == pmd_slots() * 2 * C, "slot stats [S,2,C]");
@@ -362,8 +374,8 @@ Tensor stats_finalize_local(Tensor slots, double count, Tensor gamma, Tensor bet
   Tensor gm = gamma.contiguous(), bt = beta.contiguous();
   pmd::stats_finalize_local_launch(slots.data_ptr<float>(), (float)count, gm.data_ptr<float>(),
                                    bt.data_ptr<float>(), params.data_ptr<float>(), opt_f32(rm, "rm"),
-                                   opt_f32(rv, "rv"), nb, C, (float)eps, (float)momentum,
-                                   cur_stream());
+                                   opt_f32(rv, "rv"), nb, shift_ptr(shift, C), C, (float)eps,
+                                   (float)momentum, cur_stream());
   return params;
 }
 
@@ -696,7 +708,8 @@ Tensor fp8_mfma_probe(Tensor A, Tensor Bt) {
 
 // sx, sw: device scalars the operands were quantised with (y = conv(xq, wq) / (sx * sw))
 std::vector<Tensor> conv_fp8_fwd(Tensor xq, Tensor wq, Tensor sx, Tensor sw, int64_t stride, int64_t pad,
-                                 bool want_stats, c10::optional<Tensor> stats_buf) {
+                                 bool want_stats, c10::optional<Tensor> stats_buf,
+                                 c10::optional<Tensor> shift) {
   CHECK_DEV(xq); CHECK_U8(xq); CHECK_CONT(xq); CHECK_U8(wq); CHECK_CONT(wq); CHECK_F32(sx); CHECK_F32(sw);
   TORCH_CHECK(xq.dim() == 4 && wq.dim() == 4, "fp8 conv: NHWC input and KRSC weight");
   const int N = xq.size(0), H = xq.size(1), W = xq.size(2), C = xq.size(3);
@@ -717,8 +730,8 @@ std::vector<Tensor> conv_fp8_fwd(Tensor xq, Tensor wq, Tensor sx, Tensor sw, int
   CHECK_RC(pmd::conv_fp8_fwd_launch(xq.data_ptr<uint8_t>(), wq.data_ptr<uint8_t>(), bfp_mut(y),
                                     want_stats ? stats.data_ptr<float>() : nullptr,
                                     sx.data_ptr<float>(), sw.data_ptr<float>(), N, H, W, C, P, Q, K, R, S,
-                                    (int)stride,
-                                    (int)pad, cur_stream()), "conv_fp8_fwd");
+                                    (int)stride, (int)pad, cur_stream(), shift_ptr(shift, K)),
+           "conv_fp8_fwd");
   if (want_stats) return {y, stats};
   return {y};
 }
@@ -741,20 +754,29 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_autotune_clear", &pmd::conv_autotune_clear);
   m.def("conv_wgrad_set_impl", &pmd::conv_wgrad_set_impl,
         "wgrad staging variant: 0 registers, 1 LDS-DMA 64x2 (default), 2 LDS-DMA 32x4, 3 LDS-DMA 64x3");
-  m.def("conv_fwd", &conv_fwd);
-  m.def("conv_fwd_hw", &conv_fwd_hw);
+  namespace py = pybind11;
+  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("wk"), py::arg("stride"), py::arg("pad"),
+        py::arg("want_stats"), py::arg("stats_buf"), py::arg("shift") = py::none());
+  m.def("conv_fwd_hw", &conv_fwd_hw, py::arg("x"), py::arg("wk"), py::arg("stride"), py::arg("pad"),
+        py::arg("out_h"), py::arg("out_w"), py::arg("want_stats"), py::arg("stats_buf"),
+        py::arg("shift") = py::none());
   m.def("stem_s2d_input", &stem_s2d_input);
   m.def("stem_s2d_weight", &stem_s2d_weight);
   m.def("stem_s2d_wgrad_fold", &stem_s2d_wgrad_fold);
   m.def("winograd_filter", &winograd_filter);
   m.def("winograd_input", &winograd_input);
-  m.def("winograd_output", &winograd_output);
+  m.def("winograd_output", &winograd_output, py::arg("M"), py::arg("N"), py::arg("H"), py::arg("W"),
+        py::arg("want_stats"), py::arg("stats_buf"), py::arg("shift") = py::none());
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);
-  m.def("bn_finalize", &bn_finalize);
+  m.def("bn_finalize", &bn_finalize, py::arg("sums"), py::arg("count"), py::arg("gamma"), py::arg("beta"),
+        py::arg("eps"), py::arg("rm"), py::arg("rv"), py::arg("momentum"), py::arg("nbt"),
+        py::arg("eval_mode"), py::arg("shift") = py::none());
   m.def("bn_apply", &bn_apply);
   m.def("stats_collapse", &stats_collapse);
-  m.def("stats_finalize_local", &stats_finalize_local);
+  m.def("stats_finalize_local", &stats_finalize_local, py::arg("slots"), py::arg("count"), py::arg("gamma"),
+        py::arg("beta"), py::arg("eps"), py::arg("rm"), py::arg("rv"), py::arg("momentum"), py::arg("nbt"),
+        py::arg("shift") = py::none());
   m.def("bn_bwd_reduce", &bn_bwd_reduce);
   m.def("bn_bwd_elemt", &bn_bwd_elemt);
   m.def("maxpool_fwd", &maxpool_fwd);
@@ -773,5 +795,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("quant_weight_fp8", &quant_weight_fp8);
   m.def("dequant_fp8", &dequant_fp8);
   m.def("fp8_mfma_probe", &fp8_mfma_probe);
-  m.def("conv_fp8_fwd", &conv_fp8_fwd);
+  m.def("conv_fp8_fwd", &conv_fp8_fwd, py::arg("xq"), py::arg("wq"), py::arg("sx"), py::arg("sw"),
+        py::arg("stride"), py::arg("pad"), py::arg("want_stats"), py::arg("stats_buf"),
+        py::arg("shift") = py::none());
 }

@@ -35,17 +35,16 @@ __device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
 __global__ void bn_finalize_kernel(const float* __restrict__ sums, const float* __restrict__ count,
                                    const float* __restrict__ gamma, const float* __restrict__ beta,
                                    float* __restrict__ params, float* running_mean,
-                                   float* running_var, long long* nbt, int C, float eps,
-                                   float momentum, int eval_mode) {
+                                   float* running_var, long long* nbt, float* shift, int C,
+                                   float eps, float momentum, int eval_mode) {
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
     float mean, var;
     if (eval_mode) {
       mean = running_mean[c];
       var = running_var[c];
     } else {
-      const float cnt = count[0];
-      mean = sums[c] / cnt;
-      var = fmaxf(sums[C + c] / cnt - mean * mean, 0.f);
+      bn_moments(sums[c], sums[C + c], count[0], shift ? shift[c] : 0.f, mean, var);
+      if (shift) shift[c] = mean;  // the next step's statistics shift
     }
     const float invstd = rsqrtf(var + eps);
     const float sc = gamma[c] * invstd;
@@ -365,7 +364,7 @@ int stats_collapse_launch(float* a, int Ca, float* b, int Cb, float count, float
 __global__ __launch_bounds__(256) void stats_finalize_local_kernel(
     float* __restrict__ slots, float count, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ params, float* running_mean,
-    float* running_var, long long* nbt, int C, float eps, float momentum) {
+    float* running_var, long long* nbt, float* shift, int C, float eps, float momentum) {
   __shared__ float part[2][kSlotGroups][64];
   const int li = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + li;
@@ -393,8 +392,9 @@ __global__ __launch_bounds__(256) void stats_finalize_local_kernel(
   if (g == 0 && c < C) {
     s1 = ((part[0][0][li] + part[0][1][li]) + part[0][2][li]) + part[0][3][li];
     s2 = ((part[1][0][li] + part[1][1][li]) + part[1][2][li]) + part[1][3][li];
-    const float mean = s1 / count;
-    const float var = fmaxf(s2 / count - mean * mean, 0.f);
+    float mean, var;
+    bn_moments(s1, s2, count, shift ? shift[c] : 0.f, mean, var);
+    if (shift) shift[c] = mean;
     const float invstd = rsqrtf(var + eps);
     const float sc = gamma[c] * invstd;
     params[c] = mean;
@@ -411,10 +411,10 @@ __global__ __launch_bounds__(256) void stats_finalize_local_kernel(
 }
 
 int stats_finalize_local_launch(float* slots, float count, const float* gamma, const float* beta,
-                                float* params, float* rm, float* rv, long long* nbt, int C, float eps,
-                                float momentum, hipStream_t st) {
+                                float* params, float* rm, float* rv, long long* nbt, float* shift, int C,
+                                float eps, float momentum, hipStream_t st) {
   hipLaunchKernelGGL(stats_finalize_local_kernel, dim3((C + 63) / 64), dim3(256), 0, st, slots, count,
-                     gamma, beta, params, rm, rv, nbt, C, eps, momentum);
+                     gamma, beta, params, rm, rv, nbt, shift, C, eps, momentum);
   return 0;
 }
 
@@ -430,11 +430,11 @@ static int ew_grid(long long nchunk, int C8) {
 }
 
 int bn_finalize_launch(const float* sums, const float* count, const float* gamma, const float* beta,
-                       float* params, float* rm, float* rv, long long* nbt, int C, float eps,
-                       float momentum, bool eval_mode, hipStream_t st) {
+                       float* params, float* rm, float* rv, long long* nbt, float* shift, int C,
+                       float eps, float momentum, bool eval_mode, hipStream_t st) {
   const int blocks = (C + 255) / 256;
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(blocks), dim3(256), 0, st, sums, count, gamma, beta,
-                     params, rm, rv, nbt, C, eps, momentum, eval_mode ? 1 : 0);
+                     params, rm, rv, nbt, shift, C, eps, momentum, eval_mode ? 1 : 0);
   return 0;
 }
 

@@ -80,6 +80,19 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return base + j;
 }
 
+// BatchNorm statistics are accumulated about a per-channel SHIFT K -- the
+// previous training step's batch mean of the same BN site (0 before the first):
+//   s1 = sum (v - K),  s2 = sum (v - K)^2,   mean = K + s1/n,  var = s2/n - (s1/n)^2
+// Plain (sum v, sum v^2) cancels catastrophically once |mean| >> std (the fp32
+// sum of squares loses (mean/std)^2 of its relative precision); with K within a
+// few std of the mean the subtraction is benign ("shifted data" algorithm).
+__device__ __forceinline__ void bn_moments(float s1, float s2, float n, float K, float& mean,
+                                           float& var) {
+  const float d = s1 / n;
+  mean = K + d;
+  var = fmaxf(s2 / n - d * d, 0.f);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -35,7 +35,8 @@ struct ConvArgs {
   const bf16_t* src;  // gathered operand, NHWC [N, H, W, Cs]
   const bf16_t* wt;   // B^T image [Nout][Kg]
   bf16_t* out;        // [M][Nout]
-  float* stats;       // [kStatSlots][2][Nout] or nullptr
+  float* stats;       // [kStatSlots][2][Nout] or nullptr: (sum (y-K), sum (y-K)^2) per channel
+  const float* shift;  // K = the BN statistics shift [Nout] (nullable: 0), see bn_moments
   const bf16_t* addend;  // optional [M][Nout] tensor added to the output (grad accumulation)
   const uint8_t* addend_mask;  // optional ReLU bitmask gating the addend (identity-path dz = dout*mask)
   // optional fused BatchNorm-backward reduce over the (final, bf16) output tile
@@ -459,11 +460,16 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
   bf16_t* Cs = lds;
   const int crow0 = wm * (BM / WM) + (lane >> 4) * 4;
   const int ccol0 = wn * (BN / WN) + (lane & 15);
-  float csum[NI], csq[NI];
+  float csum[NI], csq[NI], cshift[NI];
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     csum[j] = 0.f;
     csq[j] = 0.f;
+    cshift[j] = 0.f;
+    if (STATS && a.shift) {
+      const int col = n0 + (MF32 ? wn * (BN / WN) + j * 32 + (lane & 31) : ccol0 + j * 16);
+      if ((!MF32 || j < NI2) && col < a.Nout) cshift[j] = a.shift[col];
+    }
   }
   if constexpr (MF32) {
     // 32x32 C layout: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
@@ -477,7 +483,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
           const int row = wm * (BM / WM) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
           Cs[row * LDC + wn * (BN / WN) + j * 32 + (lane & 31)] = h;
           if (STATS) {
-            const float v = bf2f(h);
+            // rows past M (zero accumulators) must not contribute (0 - K) to the shifted sums
+            const float v = m0 + row < Mp ? bf2f(h) - cshift[j] : 0.f;
             csum[j] += v;
             csq[j] += v * v;
           }
@@ -492,7 +499,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
           const bf16_t h = f2bf(acc[i][j][e]);
           Cs[(crow0 + i * 16 + e) * LDC + ccol0 + j * 16] = h;
           if (STATS) {
-            const float v = bf2f(h);
+            const float v = m0 + crow0 + i * 16 + e < Mp ? bf2f(h) - cshift[j] : 0.f;
             csum[j] += v;
             csq[j] += v * v;
           }
@@ -1013,7 +1020,7 @@ static void launch_sel(const ConvArgs& a, hipStream_t st) {
 int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* stats, int N, int H,
                       int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
                       bool dgrad, const bf16_t* addend, const uint8_t* addend_mask,
-                      const BnReduceArgs* bnr, hipStream_t st) {
+                      const BnReduceArgs* bnr, hipStream_t st, const float* shift) {
   if (Cs % 8 != 0 || (Cs & (Cs - 1)) != 0) return 1;  // power-of-two channels (>= 8)
   if (Nout % 8 != 0) return 2;
   if (stride != 1 && stride != 2) return 3;
@@ -1022,6 +1029,7 @@ int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* s
   a.wt = wt;
   a.out = out;
   a.stats = stats;
+  a.shift = stats ? shift : nullptr;
   a.addend = addend;
   a.addend_mask = addend ? addend_mask : nullptr;
   a.bn_mask = nullptr;

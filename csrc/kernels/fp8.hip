@@ -185,7 +185,8 @@ struct Fp8ConvArgs {
   const uint8_t* src;  // NHWC e4m3 [N,H,W,C]
   const uint8_t* wt;   // e4m3 [K][R][S][C]
   bf16_t* out;         // [M][K]
-  float* stats;
+  float* stats;        // BN statistic slots about the shift K (see bn_moments)
+  const float* shift;  // K [Nout] (nullable: 0)
   const float* sx;     // device scalars: the per-tensor scales the operands were quantised with
   const float* sw;
   int N, H, W, Cs, log2Cs, OH, OW, Nout, R, S, stride, pad, M, Kg;
@@ -305,9 +306,12 @@ __global__ __launch_bounds__(256, 2) void conv_fp8_fwd_kernel(Fp8ConvArgs a) {
   bf16_t* Cs = reinterpret_cast<bf16_t*>(smem);
   const int crow0 = wm * (BM / 2) + (lane >> 4) * 4;
   const int ccol0 = wn * (BN / 2) + (lane & 15);
-  float csum[NI], csq[NI];
+  float csum[NI], csq[NI], cshift[NI];
 #pragma unroll
-  for (int j = 0; j < NI; ++j) csum[j] = csq[j] = 0.f;
+  for (int j = 0; j < NI; ++j) {
+    csum[j] = csq[j] = cshift[j] = 0.f;
+    if (STATS && a.shift && n0 + ccol0 + j * 16 < a.Nout) cshift[j] = a.shift[n0 + ccol0 + j * 16];
+  }
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -317,7 +321,7 @@ __global__ __launch_bounds__(256, 2) void conv_fp8_fwd_kernel(Fp8ConvArgs a) {
         const bf16_t h = f2bf(acc[i][j][e] * ds);
         Cs[(crow0 + i * 16 + e) * LDC + ccol0 + j * 16] = h;
         if (STATS) {
-          const float v = bf2f(h);
+          const float v = m0 + crow0 + i * 16 + e < a.M ? bf2f(h) - cshift[j] : 0.f;
           csum[j] += v;
           csq[j] += v * v;
         }
@@ -360,7 +364,7 @@ __global__ __launch_bounds__(256, 2) void conv_fp8_fwd_kernel(Fp8ConvArgs a) {
 
 int conv_fp8_fwd_launch(const uint8_t* x, const uint8_t* w, bf16_t* out, float* stats, const float* sx,
                         const float* sw, int N, int H, int W, int C, int OH, int OW, int K, int R,
-                        int S, int stride, int pad, hipStream_t st) {
+                        int S, int stride, int pad, hipStream_t st, const float* shift) {
   if (C % 16 != 0 || (C & (C - 1)) != 0) return 1;  // a 16-B chunk = 16 channels of one tap
   if (K % 8 != 0) return 2;
   Fp8ConvArgs a;
@@ -368,6 +372,7 @@ int conv_fp8_fwd_launch(const uint8_t* x, const uint8_t* w, bf16_t* out, float* 
   a.wt = w;
   a.out = out;
   a.stats = stats;
+  a.shift = stats ? shift : nullptr;
   a.sx = sx;
   a.sw = sw;
   a.N = N; a.H = H; a.W = W; a.Cs = C;

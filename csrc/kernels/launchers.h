@@ -14,15 +14,17 @@ struct BnReduceArgs {
   const float* p[2];
   float* red[2];
 };
+// stats (optional): BN statistic slots [kStatSlots][2][Nout] of (sum (y-K), sum (y-K)^2) with
+// K = shift[n] (nullable: 0) -- see bn_moments in common.h
 int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* stats, int N, int H,
                       int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
                       bool dgrad, const bf16_t* addend, const uint8_t* addend_mask,
-                      const BnReduceArgs* bnr, hipStream_t st);
+                      const BnReduceArgs* bnr, hipStream_t st, const float* shift = nullptr);
 // Winograd F(2x2,3x3) transforms (stride-1 pad-1 3x3; the 16 GEMMs run on hipBLASLt)
 int winograd_filter_launch(const bf16_t* wk, bf16_t* U, int K, int Cp, bool flip, hipStream_t st);
 int winograd_input_launch(const bf16_t* x, bf16_t* V, int N, int H, int W, int C, hipStream_t st);
 int winograd_output_launch(const bf16_t* M, bf16_t* y, float* stats, int N, int H, int W, int K,
-                           hipStream_t st);
+                           hipStream_t st, const float* shift = nullptr);
 void conv_set_impl(int impl);
 void conv_wgrad_set_impl(int impl);
 void conv_set_tile(int t);
@@ -48,15 +50,17 @@ int conv_wgrad_splits(int N, int H, int W, int C, int P, int Q, int K, int R, in
 int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, float* ws, int N, int H, int W,
                       int C, int P, int Q, int K, int R, int S, int stride, int pad, hipStream_t st);
 
+// shift (nullable): the statistics shift K the sums were taken about; overwritten with
+// the batch mean (the next step's shift)
 int bn_finalize_launch(const float* sums, const float* count, const float* gamma, const float* beta,
-                       float* params, float* rm, float* rv, long long* nbt, int C, float eps,
-                       float momentum, bool eval_mode, hipStream_t st);
+                       float* params, float* rm, float* rv, long long* nbt, float* shift, int C,
+                       float eps, float momentum, bool eval_mode, hipStream_t st);
 int stats_collapse_launch(float* a, int Ca, float* b, int Cb, float count, float* out,
                           bool with_count, bool clear, float* acc_a0, float* acc_a1, float* acc_b0,
                           float* acc_b1, hipStream_t st);
 int stats_finalize_local_launch(float* slots, float count, const float* gamma, const float* beta,
-                                float* params, float* rm, float* rv, long long* nbt, int C, float eps,
-                                float momentum, hipStream_t st);
+                                float* params, float* rm, float* rv, long long* nbt, float* shift, int C,
+                                float eps, float momentum, hipStream_t st);
 // mask: ReLU bitmask, one byte per 8-channel chunk (bit k = element k of the chunk > 0)
 // q8 (optional): e4m3 copy of the output scaled by *qscale, amax(|out|) -> *qamax
 int bn_apply_launch(const bf16_t* y1, const float* p1, const bf16_t* r, const float* p2, bf16_t* out,
@@ -122,7 +126,7 @@ int fp8_mfma_probe_launch(const uint8_t* A, const uint8_t* Bt, float* C, hipStre
 // y(bf16) = conv(xq, wq) / (sx * sw) with e4m3 NHWC input / KRSC weight; optional BN stats slots
 int conv_fp8_fwd_launch(const uint8_t* x, const uint8_t* w, bf16_t* out, float* stats, const float* sx,
                         const float* sw, int N, int H, int W, int C, int OH, int OW, int K, int R,
-                        int S, int stride, int pad, hipStream_t st);
+                        int S, int stride, int pad, hipStream_t st, const float* shift = nullptr);
 
 // One-shot xGMI all-reduce (kernels/xgmi.hip).  Receive-buffer layout per rank:
 // flags [kXgmiMaxRanks][kXgmiMaxBlocks] uint32 (kXgmiFlagBytes), then data
@@ -145,6 +149,7 @@ struct BnFinalizeOut {
   float* rm;      // running stats (nullable)
   float* rv;
   long long* nbt;
+  float* shift;   // statistics shift K (nullable), overwritten with the batch mean
   float eps, momentum;
 };
 struct XgmiBnArgs {

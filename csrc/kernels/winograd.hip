@@ -120,11 +120,13 @@ __global__ __launch_bounds__(256) void winograd_input_kernel(const bf16_t* __res
 }
 
 // y[n, 2th+i, 2tw+j, k] = (A^T M A)[i][j] from M[xi][t][K]; optional BN statistics
-// (sum, sum^2 of the bf16-rounded outputs) into stats[slot][2][K], slot = block % 64.
+// (sum (v-K), sum (v-K)^2 of the bf16-rounded outputs v about the shift K, bn_moments)
+// into stats[slot][2][K], slot = block % 64.
 // Grid stride is a multiple of K/8, so each thread keeps ONE 8-channel chunk.
 __global__ __launch_bounds__(256) void winograd_output_kernel(const bf16_t* __restrict__ M,
                                                               bf16_t* __restrict__ y,
-                                                              float* __restrict__ stats, int N,
+                                                              float* __restrict__ stats,
+                                                              const float* __restrict__ shift, int N,
                                                               int H, int W, int K, int TH, int TW) {
   const int K8 = K >> 3;
   const long long T = (long long)N * TH * TW;
@@ -134,6 +136,9 @@ __global__ __launch_bounds__(256) void winograd_output_kernel(const bf16_t* __re
   for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
   const long long start = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int k8 = (int)(start % K8);
+  float sh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sh[e] = (stats && shift) ? shift[k8 * 8 + e] : 0.f;
   for (long long i = start; i < total; i += (long long)gridDim.x * blockDim.x) {
     const long long t = i / K8;
     const int tw = (int)(t % TW), th = (int)((t / TW) % TH), n = (int)(t / ((long long)TW * TH));
@@ -175,8 +180,9 @@ __global__ __launch_bounds__(256) void winograd_output_kernel(const bf16_t* __re
             unpack8(pk, r);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-              s1[e] += r[e];
-              s2[e] += r[e] * r[e];
+              const float d = r[e] - sh[e];
+              s1[e] += d;
+              s2[e] += d * d;
             }
           }
         }
@@ -224,12 +230,12 @@ int winograd_input_launch(const bf16_t* x, bf16_t* V, int N, int H, int W, int C
 }
 
 int winograd_output_launch(const bf16_t* M, bf16_t* y, float* stats, int N, int H, int W, int K,
-                           hipStream_t st) {
+                           hipStream_t st, const float* shift) {
   const int K8 = K >> 3;
   if (K % 8 || K8 > 256 || (K8 & (K8 - 1))) return 1;  // 256-thread blocks: stride % K8 == 0
   const int TH = (H + 1) / 2, TW = (W + 1) / 2;
   hipLaunchKernelGGL(winograd_output_kernel, dim3(ew_blocks((long long)N * TH * TW * K8)), dim3(256), 0,
-                     st, M, y, stats, N, H, W, K, TH, TW);
+                     st, M, y, stats, shift, N, H, W, K, TH, TW);
   return 0;
 }
 

@@ -221,8 +221,10 @@ __global__ __launch_bounds__(256) void xgmi_bn_kernel(XgmiPeers peers, XgmiBnArg
     const int c = isA ? pi : pi - a.CA;
     if (a.mode == 0) {
       const BnFinalizeOut& o = isA ? a.fA : a.fB;
-      const float mean = g0 / cnt;
-      const float var = fmaxf(g1 / cnt - mean * mean, 0.f);
+      // every rank shifted its sums by the same K (the previous step's global mean)
+      float mean, var;
+      bn_moments(g0, g1, cnt, o.shift ? o.shift[c] : 0.f, mean, var);
+      if (o.shift) o.shift[c] = mean;
       const float inv = rsqrtf(var + o.eps);
       const float sc = o.gamma[c] * inv;
       o.params[c] = mean;

@@ -130,7 +130,8 @@ class XgmiComm {
            c10::optional<at::Tensor> count_out, c10::optional<at::Tensor> acc_a0,
            c10::optional<at::Tensor> acc_a1, c10::optional<at::Tensor> acc_b0,
            c10::optional<at::Tensor> acc_b1, c10::optional<at::Tensor> out_a,
-           c10::optional<at::Tensor> out_b) {
+           c10::optional<at::Tensor> out_b, c10::optional<at::Tensor> shift_a,
+           c10::optional<at::Tensor> shift_b) {
     TORCH_CHECK(opened_ || world_ == 1, "xgmi: open() the peer handles first");
     auto fptr = [](const c10::optional<at::Tensor>& t) -> float* {
       if (!t || !t->defined()) return nullptr;
@@ -155,7 +156,7 @@ class XgmiComm {
     auto fin = [&](pmd::BnFinalizeOut& o, const c10::optional<at::Tensor>& g, const c10::optional<at::Tensor>& bt,
                    const c10::optional<at::Tensor>& pr, const c10::optional<at::Tensor>& rm,
                    const c10::optional<at::Tensor>& rv, const c10::optional<at::Tensor>& nbt, double eps,
-                   double mom, int C) {
+                   double mom, int C, const c10::optional<at::Tensor>& shift) {
       o.gamma = fptr(g);
       o.beta = fptr(bt);
       o.params = fptr(pr);
@@ -165,10 +166,12 @@ class XgmiComm {
       o.nbt = (nbt && nbt->defined()) ? reinterpret_cast<long long*>(nbt->data_ptr<int64_t>()) : nullptr;
       o.eps = (float)eps;
       o.momentum = (float)mom;
+      o.shift = fptr(shift);  // statistics shift K [C]: every rank must pass the same values
+      TORCH_CHECK(!o.shift || shift->numel() == C, "xgmi bn fwd: shift must be [C]");
     };
     if (mode == 0) {
-      fin(a.fA, gamma_a, beta_a, params_a, rm_a, rv_a, nbt_a, eps_a, mom_a, a.CA);
-      if (hasB) fin(a.fB, gamma_b, beta_b, params_b, rm_b, rv_b, nbt_b, eps_b, mom_b, a.CB);
+      fin(a.fA, gamma_a, beta_a, params_a, rm_a, rv_a, nbt_a, eps_a, mom_a, a.CA, shift_a);
+      if (hasB) fin(a.fB, gamma_b, beta_b, params_b, rm_b, rv_b, nbt_b, eps_b, mom_b, a.CB, shift_b);
       a.count_out = fptr(count_out);
     } else {
       a.accA0 = fptr(acc_a0);

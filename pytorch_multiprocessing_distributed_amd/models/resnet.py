@@ -203,7 +203,7 @@ class ResNet(nn.Module):
         with OF.weight_images(self._weight_set(x)):
             if self.stem == "imagenet" and OF.fused_stem_enabled():
                 # conv1 -> BN -> ReLU -> 3x3/s2 max-pool; the activation is never stored
-                y, s = OF.conv(x, self.conv1, want_stats=self.bn1.training)
+                y, s = OF.conv(x, self.conv1, want_stats=self.bn1.training, bn=self.bn1)
                 out = OF.bn_relu_maxpool(y, s, self.bn1)
             else:
                 out = OF.conv_bn_act(x, self.conv1, self.bn1, relu=True)

@@ -203,10 +203,24 @@ def _grad_target(p):
 
 
 def _ready(*ps):
+    """Tell the gradient reducer these parameters' arena gradients are final
+    (on the current stream).  Clears a pending-writer claim (:func:`_claim`)."""
     for p in ps:
+        if getattr(p, "_pmd_claim", False):
+            p._pmd_claim = False
         h = getattr(p, "_pmd_ready", None)
         if h is not None:
             h(p)
+
+
+def _claim(p):
+    """A writer on ANOTHER stream owns ``p``'s arena gradient until it calls
+    :func:`_ready`.  autograd runs a parameter's post-accumulate-grad hook even
+    when the node returned None for it (no gradient to accumulate), i.e. right
+    when the block backward returns -- before a deferred side-stream wgrad has
+    been joined.  The reducer's post-hook skips claimed parameters, so a bucket
+    can never be all-reduced while a side-stream kernel still writes into it."""
+    p._pmd_claim = True
 
 
 def _wgrad(P, dy, x, wpack, stride, pad, w):
@@ -261,6 +275,7 @@ class _WgradSide:
     def wgrad(self, P, dy, x, wpack, stride, pad, w):
         if not self.on or _grad_target(w) is None:
             return _wgrad(P, dy, x, wpack, stride, pad, w)
+        _claim(w)
         self.side.wait_stream(self.main)
         with torch.cuda.stream(self.side):
             tgt = _grad_target(w)
@@ -327,6 +342,39 @@ def _bn_acc(bn):
     return (tb, tg)
 
 
+def bn_stat_shift(bn):
+    """Per-BN-site statistics shift K (fp32 [C], on the BN's device): the conv
+    epilogue accumulates (sum (y-K), sum (y-K)^2) and every finalize overwrites K
+    with the batch mean, so the next step's sums are taken about (nearly) the
+    mean and E[y^2] - E[y]^2 cannot cancel catastrophically (common.h
+    bn_moments).  Starts at the running mean (0 for a fresh model).  A plain
+    attribute -- not a buffer: not in state_dict, not broadcast; under SyncBN it
+    stays identical on every rank because it is set from the global mean."""
+    ref = bn.running_mean if bn.running_mean is not None else bn.weight
+    k = getattr(bn, "_pmd_shift", None)
+    if k is None or k.device != ref.device or k.numel() != ref.numel():
+        k = (bn.running_mean.detach().float().clone() if bn.running_mean is not None
+             else torch.zeros(ref.numel(), dtype=torch.float32, device=ref.device))
+        bn._pmd_shift = k
+    return k
+
+
+_BN_SHIFT = os.environ.get("PMD_BN_SHIFT", "1") != "0"
+
+
+def _shift_of(bn):
+    return bn_stat_shift(bn) if (_BN_SHIFT and bn is not None) else None
+
+
+def _stats_req(bn, training):
+    """``want_stats`` for the conv feeding ``bn``: its statistics shift (True when
+    shifting is off, PMD_BN_SHIFT=0), or False."""
+    if not training:
+        return False
+    k = _shift_of(bn)
+    return True if k is None else k
+
+
 class _Pre(list):
     """BN-backward reduce slot buffers produced by a fused dgrad epilogue, plus
     the HIP event recorded right after that dgrad (None on CPU)."""
@@ -357,15 +405,17 @@ def _bn_forward_params(P, y, st, bn, training, sync, y2=None, st2=None, bn2=None
         return p1, p2, None
     c1 = y.shape[-1]
     m_local = y.numel() // c1
+    k1 = _shift_of(bn)
+    k2 = _shift_of(bn2)
     if sync is None:
         p1 = P.stats_finalize_local(st, float(m_local), bn.weight, bn.bias, bn.eps,
                                     bn.running_mean, bn.running_var, bn.momentum,
-                                    bn.num_batches_tracked)
+                                    bn.num_batches_tracked, k1)
         p2 = None
         if bn2 is not None:
             p2 = P.stats_finalize_local(st2, float(m_local), bn2.weight, bn2.bias, bn2.eps,
                                         bn2.running_mean, bn2.running_var, bn2.momentum,
-                                        bn2.num_batches_tracked)
+                                        bn2.num_batches_tracked, k2)
         return p1, p2, float(m_local)
     fused = getattr(sync, "fused_bn_ok", None)
     if fused is not None and fused(st) and hasattr(P, "_release"):
@@ -374,20 +424,20 @@ def _bn_forward_params(P, y, st, bn, training, sync, y2=None, st2=None, bn2=None
         p1 = torch.empty(4, c1, dtype=torch.float32, device=dev)
         p2 = torch.empty(4, y2.shape[-1], dtype=torch.float32, device=dev) if bn2 is not None else None
         count = torch.empty(1, dtype=torch.float32, device=dev)
-        sync.bn_stats_fwd(st, st2, float(m_local), bn, bn2, p1, p2, count)
+        sync.bn_stats_fwd(st, st2, float(m_local), bn, bn2, p1, p2, count, k1, k2)
         P._release(st, st2)
         return p1, p2, count
     buf = P.stats_collapse(st, st2, float(m_local))
     sync.all_reduce_stats_(buf)
     count = buf[-1:]
     p1 = P.bn_finalize(buf[: 2 * c1].view(2, c1), count, bn.weight, bn.bias, bn.eps,
-                       bn.running_mean, bn.running_var, bn.momentum, bn.num_batches_tracked)
+                       bn.running_mean, bn.running_var, bn.momentum, bn.num_batches_tracked, k1)
     p2 = None
     if bn2 is not None:
         c2 = y2.shape[-1]
         p2 = P.bn_finalize(buf[2 * c1: 2 * c1 + 2 * c2].view(2, c2), count, bn2.weight, bn2.bias,
                            bn2.eps, bn2.running_mean, bn2.running_var, bn2.momentum,
-                           bn2.num_batches_tracked)
+                           bn2.num_batches_tracked, k2)
     return p1, p2, count
 
 
@@ -480,6 +530,7 @@ def _bn_backward(P, dout, mask, relu, training, sync, count, y1, p1, bn1, y2=Non
 class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, stride, pad, want_stats):
+        # want_stats: False / True / the BN statistics shift tensor (bn_stat_shift)
         P = prims_for(x)
         wpack = _weight_images(P, w, x.dtype, x.shape[-1], x.requires_grad)
         y, stats = P.conv_fwd(x, wpack, stride, pad, want_stats)
@@ -517,10 +568,11 @@ class _StemS2DConvFn(torch.autograd.Function):
         xs = C.stem_s2d_input(x)                       # [N, H/2, W/2, 16]
         ws = C.stem_s2d_weight(w.detach())             # [K, 4, 4, 16] bf16
         oh, ow = x.shape[1] // 2, x.shape[2] // 2
-        buf = HP._acquire(w.shape[0], x.device) if want_stats else None
-        out = C.conv_fwd_hw(xs, ws, 1, 2, oh, ow, bool(want_stats), buf)
+        want, shift = HP._TP.stats_request(want_stats)
+        buf = HP._acquire(w.shape[0], x.device) if want else None
+        out = C.conv_fwd_hw(xs, ws, 1, 2, oh, ow, want, buf, shift)
         y = out[0]
-        stats = out[1] if want_stats else _empty(x.device)
+        stats = out[1] if want else _empty(x.device)
         ctx.save_for_backward(xs)
         ctx.w = w
         ctx.mark_non_differentiable(stats)
@@ -563,14 +615,16 @@ def _s2d_stem_ok(x, conv_mod):
             and not x.requires_grad)
 
 
-def conv(x, conv_mod, want_stats=None):
+def conv(x, conv_mod, want_stats=None, bn=None):
     """Returns ``(y, stats)``; ``stats`` = per-channel (sum, sum^2) of y in the
-    backend's layout (consumed by :func:`bn_add_act`)."""
+    backend's layout (consumed by :func:`bn_add_act`), taken about ``bn``'s
+    statistics shift when the consuming BN module is given."""
     if want_stats is None:
         want_stats = conv_mod.training
+    req = _stats_req(bn, True) if (bn is not None and want_stats) else bool(want_stats)
     if _s2d_stem_ok(x, conv_mod):
-        return _StemS2DConvFn.apply(x, conv_mod.weight, bool(want_stats))
-    return _ConvFn.apply(x, conv_mod.weight, conv_mod.stride, conv_mod.padding, bool(want_stats))
+        return _StemS2DConvFn.apply(x, conv_mod.weight, req)
+    return _ConvFn.apply(x, conv_mod.weight, conv_mod.stride, conv_mod.padding, req)
 
 
 # ------------------------------------------------------------------------ BN
@@ -612,7 +666,7 @@ def bn_add_act(y, stats, bn, residual=None, res_y=None, res_stats=None, res_bn=N
 
 
 def conv_bn_act(x, conv_mod, bn, relu=True):
-    y, s = conv(x, conv_mod, want_stats=bn.training)
+    y, s = conv(x, conv_mod, want_stats=bn.training, bn=bn)
     return bn_add_act(y, s, bn, relu=relu)
 
 
@@ -735,7 +789,7 @@ class _ResidualBlockFn(torch.autograd.Function):
         recs = []
         for conv_m, bn in stages:
             wp = _conv_weight(P, conv_m, x.dtype, h.shape[-1], True)
-            y, st = _conv_fwd_any(P, f8, h, hq, wp, conv_m, training)
+            y, st = _conv_fwd_any(P, f8, h, hq, wp, conv_m, _stats_req(bn, training))
             p, _, count = _bn_forward_params(P, y, st, bn, training, sync)
             if f8 is not None:
                 site = f8.site(("a", id(bn)))
@@ -747,12 +801,12 @@ class _ResidualBlockFn(torch.autograd.Function):
             h = z
         fconv, fbn = final
         wpf = _conv_weight(P, fconv, x.dtype, h.shape[-1], True)
-        yf, stf = _conv_fwd_any(P, f8, h, hq, wpf, fconv, training)
+        yf, stf = _conv_fwd_any(P, f8, h, hq, wpf, fconv, _stats_req(fbn, training))
         osite = f8.site(("a", id(fbn))) if f8 is not None else None
         if shortcut is not None:
             sconv, sbn = shortcut
             wps = _conv_weight(P, sconv, x.dtype, x.shape[-1], x.requires_grad)
-            ys, sts = _conv_fwd_any(P, f8, x, xq, wps, sconv, training)
+            ys, sts = _conv_fwd_any(P, f8, x, xq, wps, sconv, _stats_req(sbn, training))
             pf, ps, countf = _bn_forward_params(P, yf, stf, fbn, training, sync, ys, sts, sbn)
             r = P.bn_apply(yf, pf, None, ys, ps, relu=True, **({"fp8": osite} if osite else {}))
         else:

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import torch
 
+from . import torch_prims as _TP
 from . import winograd as _WG
 from .native import C as _C
 
@@ -48,9 +49,10 @@ def quant_weight_fp8(w, cin, scale, amax):
 
 
 def conv_fp8_fwd(xq, wq, sx, sw, stride, pad, want_stats):
-    if want_stats:
+    want, shift = _TP.stats_request(want_stats)
+    if want:
         buf = _acquire(wq.shape[0], xq.device)
-        y, st = _C.conv_fp8_fwd(xq, wq, sx, sw, int(stride), int(pad), True, buf)
+        y, st = _C.conv_fp8_fwd(xq, wq, sx, sw, int(stride), int(pad), True, buf, shift)
         return y, st
     return _C.conv_fp8_fwd(xq, wq, sx, sw, int(stride), int(pad), False, None)[0], None
 
@@ -63,12 +65,15 @@ def conv_weight(w, dtype, cin, want_t=True):
 
 
 def conv_fwd(x, wpack, stride, pad, want_stats):
+    """``want_stats``: False, True, or the BN statistics shift (fp32 [K], see
+    torch_prims.conv_fwd): the slots then hold sums about that shift."""
+    want, shift = _TP.stats_request(want_stats)
     if _WG.get_algo() == "winograd" and _WG.eligible(tuple(wpack[0].shape), stride, pad, x.shape[-1]):
-        return _WG.conv_fwd(x, wpack[0], want_stats,
-                            _acquire(wpack[0].shape[0], x.device) if want_stats else None)
-    if want_stats:
+        return _WG.conv_fwd(x, wpack[0], want,
+                            _acquire(wpack[0].shape[0], x.device) if want else None, shift)
+    if want:
         buf = _acquire(wpack[0].shape[0], x.device)
-        y, st = _C.conv_fwd(x, wpack[0], int(stride), int(pad), True, buf)
+        y, st = _C.conv_fwd(x, wpack[0], int(stride), int(pad), True, buf, shift)
         return y, st
     return _C.conv_fwd(x, wpack[0], int(stride), int(pad), False, None)[0], None
 
@@ -101,15 +106,15 @@ def conv_wgrad(dy, x, wk_shape, stride, pad, out=None):
 
 # ----------------------------------------------------------------------- BN
 def bn_finalize(sums, count, gamma, beta, eps, running_mean=None, running_var=None,
-                momentum=0.1, num_batches_tracked=None):
+                momentum=0.1, num_batches_tracked=None, shift=None):
     return _C.bn_finalize(sums, count, gamma.detach(), beta.detach(), float(eps), running_mean,
-                          running_var, float(momentum), num_batches_tracked, False)
+                          running_var, float(momentum), num_batches_tracked, False, shift)
 
 
 def stats_finalize_local(slots, count, gamma, beta, eps, running_mean=None, running_var=None,
-                         momentum=0.1, num_batches_tracked=None):
+                         momentum=0.1, num_batches_tracked=None, shift=None):
     p = _C.stats_finalize_local(slots, float(count), gamma.detach(), beta.detach(), float(eps),
-                                running_mean, running_var, float(momentum), num_batches_tracked)
+                                running_mean, running_var, float(momentum), num_batches_tracked, shift)
     _release(slots)
     return p
 

@@ -35,13 +35,26 @@ def conv_weight(w, dtype, cin, want_t=True):
     return (wk.contiguous(),)
 
 
+def stats_request(want_stats):
+    """``want_stats``: False/True, or the BN statistics shift K (a [C] tensor; True = K 0).
+    -> (want, shift or None)."""
+    if torch.is_tensor(want_stats):
+        return True, want_stats
+    return bool(want_stats), None
+
+
 def conv_fwd(x, wpack, stride, pad, want_stats):
+    """y and, when requested, the BN statistics of the (rounded) output about the
+    shift K: [sum (y-K), sum (y-K)^2] (csrc/kernels/common.h bn_moments)."""
+    want, shift = stats_request(want_stats)
     wk = wpack[0]
     y = F.conv2d(_f(_nchw(x)), _f(wk.permute(0, 3, 1, 2)), stride=stride, padding=pad)
     y = _nhwc(y).to(x.dtype)
     stats = None
-    if want_stats:
+    if want:
         yf = _f(y).reshape(-1, y.shape[-1])
+        if shift is not None:
+            yf = yf - _f(shift)
         stats = torch.stack([yf.sum(0), (yf * yf).sum(0)])
     return y, stats
 
@@ -80,13 +93,17 @@ def conv_wgrad(dy, x, wk_shape, stride, pad, out=None):
 # BN "params" are one fp32 [4, C] tensor: rows mean, invstd, scale=gamma*invstd,
 # shift=beta-mean*scale (the same packing the HIP kernels use).
 def bn_finalize(sums, count, gamma, beta, eps, running_mean=None, running_var=None,
-                momentum=0.1, num_batches_tracked=None):
-    """Global (sum, sum^2, count) -> params; updates running stats with the
-    unbiased variance (torch batch_norm_gather_stats_with_counts semantics).
-    ``count`` is a 1-element fp32 tensor so no host sync is needed."""
+                momentum=0.1, num_batches_tracked=None, shift=None):
+    """Global (sum (y-K), sum (y-K)^2, count) -> params; updates running stats with
+    the unbiased variance (torch batch_norm_gather_stats_with_counts semantics).
+    ``count`` is a 1-element fp32 tensor so no host sync is needed.  ``shift`` = K
+    (None: 0) is overwritten with the batch mean, the next step's shift."""
     cnt = _f(count)
-    mean = sums[0] / cnt
-    var = (sums[1] / cnt - mean * mean).clamp_min(0.0)
+    d = sums[0] / cnt
+    mean = d if shift is None else _f(shift) + d
+    var = (sums[1] / cnt - d * d).clamp_min(0.0)
+    if shift is not None:
+        shift.copy_(mean.to(shift.dtype))
     invstd = torch.rsqrt(var + eps)
     scale = _f(gamma.detach()) * invstd
     shift = _f(beta.detach()) - mean * scale
@@ -100,10 +117,10 @@ def bn_finalize(sums, count, gamma, beta, eps, running_mean=None, running_var=No
 
 
 def stats_finalize_local(stats, count, gamma, beta, eps, running_mean=None, running_var=None,
-                         momentum=0.1, num_batches_tracked=None):
+                         momentum=0.1, num_batches_tracked=None, shift=None):
     cnt = torch.full((1,), float(count), dtype=stats.dtype, device=stats.device)
     return bn_finalize(stats, cnt, gamma, beta, eps, running_mean, running_var, momentum,
-                       num_batches_tracked)
+                       num_batches_tracked, shift)
 
 
 def bn_eval_params(running_mean, running_var, gamma, beta, eps):

@@ -85,14 +85,15 @@ def _c():
     return C
 
 
-def conv_fwd(x, wk, want_stats, stats_buf=None):
-    """Forward (+ conv_fwd-compatible [slots,2,K] statistics) on the gfx950 transforms."""
+def conv_fwd(x, wk, want_stats, stats_buf=None, shift=None):
+    """Forward (+ conv_fwd-compatible [slots,2,K] statistics about ``shift``) on the
+    gfx950 transforms."""
     C = _c()
     U = C.winograd_filter(wk, False)                 # [16, K, C]
     V = C.winograd_input(x)                          # [16, T, C]
     M = torch.bmm(V, U.transpose(1, 2))              # [16, T, K]  hipBLASLt
     N, H, W, _ = x.shape
-    out = C.winograd_output(M.contiguous(), N, H, W, bool(want_stats), stats_buf)
+    out = C.winograd_output(M.contiguous(), N, H, W, bool(want_stats), stats_buf, shift)
     return (out[0], out[1]) if want_stats else (out[0], None)
 
 

@@ -95,9 +95,11 @@ class Comm:
         """Can the fused SyncBN statistics kernel handle these slot buffers?"""
         return self.xgmi is not None and t.is_cuda and t.dim() == 3 and t.shape[0] == 64
 
-    def bn_stats_fwd(self, slots_a, slots_b, count, bn_a, bn_b, params_a, params_b, count_out):
+    def bn_stats_fwd(self, slots_a, slots_b, count, bn_a, bn_b, params_a, params_b, count_out,
+                     shift_a=None, shift_b=None):
         self._record("xgmi_bn_fwd", slots_a)
-        self.xgmi.bn_fwd(slots_a, slots_b, count, bn_a, bn_b, params_a, params_b, count_out)
+        self.xgmi.bn_fwd(slots_a, slots_b, count, bn_a, bn_b, params_a, params_b, count_out,
+                         shift_a, shift_b)
 
     def bn_stats_bwd(self, slots_a, slots_b, acc_a, acc_b, out_a, out_b):
         self._record("xgmi_bn_bwd", slots_a)

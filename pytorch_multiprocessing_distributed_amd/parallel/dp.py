@@ -165,9 +165,19 @@ class DataParallel(nn.Module):
         for i, p in enumerate(self.flat.params):
             h = self._make_native_hook(i) if self._native is not None else self._make_hook(i)
             # AccumulateGrad path (params whose grad is returned to autograd) ...
-            self._hooks.append(p.register_post_accumulate_grad_hook(h))
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._post_hook(h)))
             # ... and the direct path (fused ops that wrote into the arena call this)
             p._pmd_ready = h
+
+    @staticmethod
+    def _post_hook(h):
+        # autograd fires post-accumulate hooks even for a None gradient; a param
+        # whose arena gradient is still being written on a side stream is
+        # claimed (ops.functional._claim) and is marked by its writer's _ready
+        def post(p):
+            if not getattr(p, "_pmd_claim", False):
+                h(p)
+        return post
 
     def _maybe_rebuild(self):
         """Once, before the second iteration: re-lay the arena out in the order
@@ -307,10 +317,12 @@ class DataParallel(nn.Module):
 
     # ------------------------------------------------------------- forward
     def forward(self, *args, **kwargs):
-        if self.comm is not None and self.module.training and torch.is_grad_enabled():
+        if self.comm is not None and torch.is_grad_enabled():
+            # like DDP: buckets are rebuilt after the first iteration that produced
+            # gradients, whatever the BN mode of the module
             if self._rebuild_pending and self.num_iterations >= 1:
                 self._maybe_rebuild()
-            if self.broadcast_buffers:
+            if self.broadcast_buffers and self.module.training:
                 self._broadcast_buffers()
         return self.module(*args, **kwargs)
 

@@ -214,3 +214,41 @@ def test_roctx_region_noop_without_env():
     from pytorch_multiprocessing_distributed_amd.utils.trace import region
     with region("x"):
         pass
+
+
+def test_post_accumulate_hook_skips_claimed_params():
+    """autograd runs a parameter's post-accumulate-grad hook even when the node
+    returned None for it; a parameter whose arena gradient a side-stream wgrad
+    is still writing is claimed and must be marked ready only by its writer
+    (the torn-bucket race found by bench/race_probe.py)."""
+    import torch.nn as nn
+    from pytorch_multiprocessing_distributed_amd.ops import functional as OF
+    from pytorch_multiprocessing_distributed_amd.parallel.dp import DataParallel
+
+    class _NoGrad(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, w):
+            return x * 2
+
+        @staticmethod
+        def backward(ctx, g):
+            return g * 2, None
+
+    w = nn.Parameter(torch.ones(3))
+    fired = []
+    w.register_post_accumulate_grad_hook(lambda p: fired.append(p.grad))
+    x = torch.ones(3, requires_grad=True)
+    _NoGrad.apply(x, w).sum().backward()
+    assert fired == [None]          # the premise: the hook fires for a None gradient
+
+    marks = []
+    post = DataParallel._post_hook(marks.append)
+    p = nn.Parameter(torch.ones(2))
+    p._pmd_ready = marks.append
+    OF._claim(p)
+    post(p)
+    assert marks == []              # claimed: autograd's hook does not mark it
+    OF._ready(p)
+    assert marks == [p] and not p._pmd_claim
+    post(p)
+    assert len(marks) == 2          # unclaimed again (the reducer's mark is idempotent)

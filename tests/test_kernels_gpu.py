@@ -518,3 +518,55 @@ def _dgrad_fused_bn_reduce(shape, two):
         got = HP.stats_collapse(r).view(2, C)
         want = HP.stats_collapse(HP.bn_bwd_reduce(dx, mask, yb, p, True)).view(2, C)  # unfused
         _close(got, want, 1e-3)
+
+
+def test_bn_stats_large_mean_shift():
+    """|mean|/std = 100: the conv-epilogue statistics are
+    taken about the BN's shift (previous batch mean, common.h bn_moments), so
+    from step 2 on the variance matches an fp64 reference on the SAME bf16
+    outputs; the unshifted first step shows the cancellation it avoids.  Then
+    the fused conv->BN->ReLU path on the HIP kernels against torch.nn.BatchNorm2d
+    in fp64 over three training steps (outputs and running statistics)."""
+    import torch.nn as nn
+    from pytorch_multiprocessing_distributed_amd.ops import functional as OF
+    HP = _hp()
+    torch.manual_seed(5)
+    N, H, C, K = 16, 15, 64, 64     # M = 3600: the last 128-row tile is partial
+
+    def inp(seed):
+        g = torch.Generator(device=DEV).manual_seed(seed)
+        x = torch.randn(N, H, H, C, device=DEV, generator=g)
+        x[..., 0] = 1.0
+        return x.to(torch.bfloat16)
+    from pytorch_multiprocessing_distributed_amd.models.resnet import Conv2d
+    conv = Conv2d(C, K, 1, stride=1, padding=0).to(DEV)
+    with torch.no_grad():
+        conv.weight.normal_(0, (1.0 / (C - 1)) ** 0.5)
+        conv.weight[:, 0] = 100.0
+    x = inp(0)
+    wp = HP.conv_weight(conv.weight, torch.bfloat16, C, False)
+    y, _ = HP.conv_fwd(x, wp, 1, 0, False)
+    t = y.double().reshape(-1, K)
+    tvar = t.var(0, unbiased=False)
+    shift = torch.zeros(K, device=DEV)
+    errs = []
+    for _ in range(2):
+        _, st = HP.conv_fwd(x, wp, 1, 0, shift)
+        p = HP.stats_finalize_local(st, t.shape[0], torch.ones(K, device=DEV), torch.zeros(K, device=DEV),
+                                    0.0, shift=shift)
+        errs.append(((1.0 / p[1].double() ** 2 - tvar).abs() / tvar).max().item())
+    assert errs[1] < 1e-4 and errs[1] < errs[0] / 10, errs
+    # the module path (fused BN finalize on the HIP kernels) vs nn.BatchNorm2d
+    bn = nn.BatchNorm2d(K).to(DEV)
+    ref_bn = nn.BatchNorm2d(K).to(DEV).double()
+    for step in range(3):
+        xs = inp(step + 1)
+        out = OF.conv_bn_act(xs, conv, bn, relu=True)
+        with torch.no_grad():
+            yy, _ = HP.conv_fwd(xs, wp, 1, 0, False)       # the same bf16 conv output
+            ref = torch.relu(ref_bn(yy.double().permute(0, 3, 1, 2))).permute(0, 2, 3, 1)
+        if step >= 1:
+            # bf16 output rounding only: relative L2 ~ 2^-9
+            _close_norm(out.double(), ref, 5e-3)
+    torch.testing.assert_close(bn.running_mean.double(), ref_bn.running_mean, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(bn.running_var.double(), ref_bn.running_var, rtol=5e-3, atol=1e-4)

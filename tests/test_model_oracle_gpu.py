@@ -1,0 +1,107 @@
+"""Whole-model numerics at a realistic size: ONE training
+step of ResNet-50 (224x224, batch 32) on the gfx950 kernels (bf16 activations,
+fp32 accumulation) against the SAME model (same weights, same input) on the
+PyTorch reference primitives in fp32 ON THE GPU (ops/torch_prims.py via
+force_torch_prims), and -- as the yardstick for what bf16 activations cost --
+the reference primitives run on bf16 activations.
+
+What is and is not well defined (measured on MI355X, bench/oracle_probe.py):
+  * BN in eval mode (running statistics: the net is a fixed piecewise-linear
+    map), the gradient is well conditioned: perturbing the input by 2^-9
+    (one bf16 rounding) moves the fp32 gradients by ~1e-2 relative L2 per
+    tensor, and bf16 activations cost ~2e-2 median / ~0.12 worst tensor.
+  * BN in TRAINING mode at random init, the gradient is chaotic (the
+    batch-statistics coupling of 53 BN layers explodes gradients at
+    initialisation): the same 2^-9 input perturbation moves the fp32
+    gradients by ~100%, so NO bf16 implementation -- torch's included --
+    can agree with the fp32 gradients tensor by tensor.  Forward quantities
+    (loss, BN running statistics) stay well defined.
+
+Assertions: eval mode -- every tensor within 1.5x (+5e-3) of the error of the
+reference primitives on bf16 activations, median < 5e-2; training mode --
+loss within 1e-2, running var within 1e-2 relative L2 per tensor, running
+mean within 1e-2 of 0.1 x the batch std (its one-step scale), and
+the gradient error distribution no worse than the bf16 reference's (median
+and 90th percentile within 1.2x).  A real bug (wrong tap, statistic,
+dropped residual gradient, stale bucket) breaks the eval-mode bounds by an
+order of magnitude on the affected tensors.
+"""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _step(m, x, y, torch_prims):
+    from pytorch_multiprocessing_distributed_amd.ops import functional as OF
+    OF.force_torch_prims(torch_prims)
+    try:
+        loss = OF.cross_entropy(m(x), y)
+        loss.backward()
+    finally:
+        OF.force_torch_prims(False)
+    return float(loss.detach())
+
+
+def _runs(train):
+    from pytorch_multiprocessing_distributed_amd.models import ResNet50
+    from pytorch_multiprocessing_distributed_amd.ops.native import C
+    torch.manual_seed(0)
+    m0 = ResNet50(num_classes=1000, stem="imagenet").to(DEV)
+    m0.train(train)
+    x, y = C.synth_images(32, 224, 224, 8, 3, 1000, 7, 0)
+    ms = {k: copy.deepcopy(m0) for k in ("hip", "f32", "bf16ref")}
+    loss = {"hip": _step(ms["hip"], x, y, False),
+            "f32": _step(ms["f32"], x.float(), y, True),
+            "bf16ref": _step(ms["bf16ref"], x, y, True)}
+    torch.cuda.synchronize()
+    grads = {k: dict((n, p.grad) for n, p in m.named_parameters()) for k, m in ms.items()}
+    return ms, loss, grads
+
+
+def _err(grads, which):
+    return {n: _rel(g, grads["f32"][n]) for n, g in grads[which].items()}
+
+
+def _q(v, q):
+    v = sorted(v)
+    return v[min(int(len(v) * q), len(v) - 1)]
+
+
+def test_resnet50_eval_bn_step_vs_fp32_oracle():
+    _, loss, grads = _runs(train=False)
+    assert abs(loss["hip"] - loss["f32"]) / loss["f32"] < 1e-3, loss
+    eh, eb = _err(grads, "hip"), _err(grads, "bf16ref")
+    bad = [(n, eh[n], eb[n]) for n in eh if eh[n] > 1.5 * eb[n] + 5e-3]
+    assert not bad, bad[:8]
+    assert _q(eh.values(), 0.5) < 5e-2, _q(eh.values(), 0.5)
+
+
+def test_resnet50_train_bn_step_vs_fp32_oracle():
+    ms, loss, grads = _runs(train=True)
+    assert abs(loss["hip"] - loss["f32"]) / loss["f32"] < 1e-2, loss
+    bufs = {k: dict(m.named_buffers()) for k, m in ms.items()}
+    for n, br in bufs["f32"].items():
+        bh = bufs["hip"][n]
+        if not bh.dtype.is_floating_point:
+            assert torch.equal(bh, br), n
+        elif n.endswith("running_var"):
+            assert _rel(bh, br) < 1e-2, (n, _rel(bh, br))
+        elif n.endswith("running_mean"):
+            # one momentum-0.1 step from 0: the batch mean of a conv output is
+            # small next to its std, so measure the error in units of 0.1 * std
+            std = ((bufs["f32"][n[:-4] + "var"].double() - 0.9) / 0.1).clamp_min(0).sqrt()
+            err = ((bh - br).double().norm() / (0.1 * std).norm()).item()
+            assert err < 1e-2, (n, err)
+    eh, eb = _err(grads, "hip"), _err(grads, "bf16ref")
+    for q in (0.5, 0.9):
+        assert _q(eh.values(), q) < 1.2 * _q(eb.values(), q), (q, _q(eh.values(), q), _q(eb.values(), q))

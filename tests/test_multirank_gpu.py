@@ -78,6 +78,11 @@ def _defer_worker(rank, world, port, out, defer):
     torch.manual_seed(0)
     model = build_model("resnet50", num_classes=10, stem="imagenet").cuda()
     dp = DataParallel(model, comm, bucket_mb=2.0, first_bucket_mb=0.5)
+    # BN in eval mode: training-mode BN at random init makes the gradient chaotic
+    # (tests/test_model_oracle_gpu.py: a 2^-9 input perturbation moves it ~100%),
+    # which would drown a schedule bug in fp32-atomic ordering noise.  The
+    # reducer, the bucket rebuild and the deferred side-stream wgrads run the same.
+    dp.module.eval()
     # lr=0: the weights stay fixed, so every step's averaged gradients must agree
     # between the deferred and the per-block join (a race on the last bucket, or
     # a double all-reduce, shows up in ANY of the three steps)
@@ -107,24 +112,31 @@ def test_deferred_wgrad_buckets_fire_once_and_match(tmp_path):
     reducer's final step -- else every step all-reduces twice and the last
     bucket races the wgrads still writing it."""
     res = {}
-    for defer in (1, 0):
-        out = str(tmp_path / f"d{defer}.pt")
+    for tag, defer in (("d1", 1), ("d1b", 1), ("d0", 0)):
+        out = str(tmp_path / f"{tag}.pt")
         mp.spawn(_defer_worker, args=(2, _free_port(), out, defer), nprocs=2, join=True)
-        res[defer] = torch.load(out, weights_only=True)
-    for defer, r in res.items():
-        assert r["iters"] == 3, (defer, r["iters"])
+        res[tag] = torch.load(out, weights_only=True)
+    for tag, r in res.items():
+        assert r["iters"] == 3, (tag, r["iters"])
         # iteration 1 runs on the construction-time buckets, 2-3 on the ready-order rebuild
         for it, order in enumerate(r["launches"]):
-            assert order == list(range(len(order))), (defer, it, order)  # each once, index order
+            assert order == list(range(len(order))), (tag, it, order)  # each once, index order
             if it > 0:
-                assert len(order) == r["nb"], (defer, it, order)
-    # same averaged gradients at every step with and without the deferred join,
-    # up to run-to-run fp32-atomic summation order in the split-K weight gradients
-    # (~1e-3 global relative L2; a double all-reduce is a factor 2, a torn bucket O(1))
-    for step, (a, b) in enumerate(zip(res[1]["grads"], res[0]["grads"])):
-        num = sum(((a[k] - b[k]) ** 2).sum() for k in a)
-        den = sum((b[k] ** 2).sum() for k in b)
-        assert (num / den).sqrt().item() < 1e-2, (step, (num / den).sqrt().item())
+                assert len(order) == r["nb"], (tag, it, order)
+
+    def rel(x, y):
+        num = sum(((x[k] - y[k]) ** 2).sum() for k in x)
+        den = sum((y[k] ** 2).sum() for k in y)
+        return (num / den).sqrt().item()
+    # Same averaged gradients at every step with and without the deferred join.
+    # Two runs of the SAME schedule differ only by fp32-atomic summation order
+    # (split-K weight gradients): that run-to-run spread is the noise floor.  A
+    # double all-reduce (factor 2) or a torn bucket (O(1)) is far above it.
+    for step in range(3):
+        floor = rel(res["d1b"]["grads"][step], res["d1"]["grads"][step])
+        diff = rel(res["d0"]["grads"][step], res["d1"]["grads"][step])
+        assert diff < 4 * floor + 5e-3, (step, diff, floor)
+        assert diff < 2e-2, (step, diff, floor)
 
 
 # ------------------------------------------------------------- native RCCL comm
