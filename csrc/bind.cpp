@@ -46,6 +46,23 @@ std::vector<Tensor> conv_weight_prep(Tensor w, int64_t cp, bool want_t) {
   return {wk};
 }
 
+// zero-filled tensor on the current stream through the framework's own fill kernel
+// (keeps ATen's FillFunctor off the training step)
+Tensor pmd_zeros(at::IntArrayRef sizes, const at::TensorOptions& opt) {
+  Tensor t = torch::empty(sizes, opt);
+  pmd::zero_launch(t.data_ptr(), (long long)t.numel() * t.element_size(), cur_stream());
+  return t;
+}
+
+// in-place zero of a contiguous GPU tensor (the gradient arena's zero_grad)
+Tensor zero_(Tensor t) {
+  CHECK_DEV(t);
+  CHECK_CONT(t);
+  c10::DeviceGuard g(t.device());
+  pmd::zero_launch(t.data_ptr(), (long long)t.numel() * t.element_size(), cur_stream());
+  return t;
+}
+
 float* opt_f32(const c10::optional<Tensor>& t, const char* what) {
   if (!t || !t->defined()) return nullptr;
   TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kFloat32 && t->is_contiguous(), what,
@@ -86,7 +103,7 @@ static std::vector<Tensor> conv_fwd_impl(Tensor x, Tensor wk, int64_t stride, in
       opt_f32(stats_buf, "stats_buf");
       stats = *stats_buf;
     } else {
-      stats = torch::zeros({pmd_slots(), 2, K}, x.options().dtype(torch::kFloat32));
+      stats = pmd_zeros({pmd_slots(), 2, K}, x.options().dtype(torch::kFloat32));
     }
   }
   const float* shp = shift_ptr(shift, K);
@@ -197,7 +214,7 @@ std::vector<Tensor> winograd_output(Tensor M, int64_t N, int64_t H, int64_t W, b
       opt_f32(stats_buf, "stats_buf");
       stats = *stats_buf;
     } else {
-      stats = torch::zeros({pmd_slots(), 2, K}, M.options().dtype(torch::kFloat32));
+      stats = pmd_zeros({pmd_slots(), 2, K}, M.options().dtype(torch::kFloat32));
     }
   }
   CHECK_RC(pmd::winograd_output_launch(bfp(M), bfp_mut(y), want_stats ? stats.data_ptr<float>() : nullptr,
@@ -287,7 +304,7 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int64_t R, int64_t S, int64_t stride, int
     opt_f32(out, "wgrad out");
     dw = *out;
   } else {
-    dw = torch::zeros({K, R, S, C}, x.options().dtype(torch::kFloat32));
+    dw = pmd_zeros({K, R, S, C}, x.options().dtype(torch::kFloat32));
   }
   const int splits = pmd::conv_wgrad_splits(N, H, W, C, P, Q, K, (int)R, (int)S, (int)stride,
                                             (int)pad);
@@ -450,7 +467,7 @@ Tensor bn_bwd_reduce(Tensor dout, c10::optional<Tensor> mask, Tensor y, Tensor p
     opt_f32(red_buf, "red_buf");
     red = *red_buf;
   } else {
-    red = torch::zeros({pmd_slots(), 2, C}, y.options().dtype(torch::kFloat32));
+    red = pmd_zeros({pmd_slots(), 2, C}, y.options().dtype(torch::kFloat32));
   }
   const int rc = pmd::bn_bwd_reduce_launch(bfp(dout), mask_ptr(mask, M * (C / 8), relu), bfp(y),
                                            params.data_ptr<float>(), red.data_ptr<float>(), (int)M, C,
@@ -589,9 +606,9 @@ std::vector<Tensor> xent_fwd(Tensor logits, Tensor target) {
   TORCH_CHECK(target.scalar_type() == torch::kInt64 && target.is_cuda(), "target int64 GPU");
   const int N = logits.size(0), V = logits.size(1);
   c10::DeviceGuard g(logits.device());
-  Tensor loss = torch::zeros({1}, logits.options());
+  Tensor loss = pmd_zeros({1}, logits.options());
   Tensor lse = torch::empty({N}, logits.options());
-  Tensor correct = torch::zeros({1}, logits.options().dtype(torch::kInt64));
+  Tensor correct = pmd_zeros({1}, logits.options().dtype(torch::kInt64));
   Tensor tg = target.contiguous();
   pmd::xent_fwd_launch(logits.data_ptr<float>(), reinterpret_cast<const long long*>(tg.data_ptr<int64_t>()),
                        loss.data_ptr<float>(), lse.data_ptr<float>(),
@@ -724,7 +741,7 @@ std::vector<Tensor> conv_fp8_fwd(Tensor xq, Tensor wq, Tensor sx, Tensor sw, int
       stats = *stats_buf;
       TORCH_CHECK(stats.numel() == pmd_slots() * 2 * K, "stats buffer must be [slots, 2, K]");
     } else {
-      stats = torch::zeros({pmd_slots(), 2, K}, xq.options().dtype(torch::kFloat32));
+      stats = pmd_zeros({pmd_slots(), 2, K}, xq.options().dtype(torch::kFloat32));
     }
   }
   CHECK_RC(pmd::conv_fp8_fwd_launch(xq.data_ptr<uint8_t>(), wq.data_ptr<uint8_t>(), bfp_mut(y),
@@ -734,6 +751,59 @@ std::vector<Tensor> conv_fp8_fwd(Tensor xq, Tensor wq, Tensor sx, Tensor sw, int
            "conv_fp8_fwd");
   if (want_stats) return {y, stats};
   return {y};
+}
+
+// ------------------------------------------------------------- classifier
+static void chk_lin(const Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kFloat32 && t.is_contiguous() && t.dim() == 2, what,
+              " must be a contiguous 2-D fp32 GPU tensor");
+}
+
+// out[N][V] = x[N][K] . w[V][K]^T (+ b)
+Tensor linear_fwd(Tensor x, Tensor w, c10::optional<Tensor> b) {
+  chk_lin(x, "x");
+  chk_lin(w, "w");
+  TORCH_CHECK(x.size(1) == w.size(1), "linear: feature mismatch");
+  const int N = x.size(0), K = x.size(1), V = w.size(0);
+  const float* bp = opt_f32(b, "bias");
+  if (bp) TORCH_CHECK(b->numel() == V, "linear: bias size");
+  c10::DeviceGuard g(x.device());
+  Tensor out = torch::empty({N, V}, x.options());
+  CHECK_RC(pmd::linear_mfma_launch(x.data_ptr<float>(), w.data_ptr<float>(), out.data_ptr<float>(), bp,
+                                   K, 1, 1, K, N, V, K, false, cur_stream()), "linear_fwd");
+  return out;
+}
+
+// dx[N][K] = dout[N][V] . w[V][K]
+Tensor linear_dgrad(Tensor dout, Tensor w) {
+  chk_lin(dout, "dout");
+  chk_lin(w, "w");
+  TORCH_CHECK(dout.size(1) == w.size(0), "linear dgrad: class mismatch");
+  const int N = dout.size(0), V = w.size(0), K = w.size(1);
+  c10::DeviceGuard g(dout.device());
+  Tensor dx = torch::empty({N, K}, dout.options());
+  CHECK_RC(pmd::linear_mfma_launch(dout.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(), nullptr,
+                                   V, 1, K, 1, N, K, V, false, cur_stream()), "linear_dgrad");
+  return dx;
+}
+
+// dw[V][K] (+)= dout^T . x ; db[V] (+)= column sums of dout (both optional targets,
+// e.g. grad-arena views; accumulate=false overwrites)
+void linear_wgrad(Tensor dout, Tensor x, Tensor dw, c10::optional<Tensor> db, bool accumulate) {
+  chk_lin(dout, "dout");
+  chk_lin(x, "x");
+  chk_lin(dw, "dw");
+  const int N = dout.size(0), V = dout.size(1), K = x.size(1);
+  TORCH_CHECK(x.size(0) == N && dw.size(0) == V && dw.size(1) == K, "linear wgrad: shapes");
+  c10::DeviceGuard g(dout.device());
+  CHECK_RC(pmd::linear_mfma_launch(dout.data_ptr<float>(), x.data_ptr<float>(), dw.data_ptr<float>(), nullptr,
+                                   1, V, K, 1, V, K, N, accumulate, cur_stream()), "linear_wgrad");
+  float* dbp = opt_f32(db, "db");
+  if (dbp) {
+    TORCH_CHECK(db->numel() == V, "linear wgrad: bias grad size");
+    CHECK_RC(pmd::linear_colsum_launch(dout.data_ptr<float>(), dbp, N, V, accumulate, cur_stream()),
+             "linear_colsum");
+  }
 }
 
 }  // namespace
@@ -788,6 +858,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
+  m.def("linear_fwd", &linear_fwd);
+  m.def("linear_dgrad", &linear_dgrad);
+  m.def("linear_wgrad", &linear_wgrad);
+  m.def("zero_", &zero_, "in-place zero of a contiguous GPU tensor (framework fill kernel)");
   m.def("sgd_", &sgd_);
   m.def("synth_images", &synth_images);
   m.def("cifar_augment", &cifar_augment);

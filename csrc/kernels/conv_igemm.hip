@@ -113,8 +113,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
   constexpr int LDC = BN + 8;
   constexpr int SMEM_MAIN = NST * STAGE * 2;
   constexpr int SMEM_EPI = BM * LDC * 2;
-  constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
-  static_assert(SMEM >= NT * 33 * 4, "LDS too small for the fused BN-reduce partials");
+  constexpr int SMEM_PART = DGRAD ? NT * 33 * 4 : 0;  // fused BN-reduce partials [NT][33]
+  constexpr int SMEM0 = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
+  constexpr int SMEM = SMEM0 > SMEM_PART ? SMEM0 : SMEM_PART;
   static_assert(SMEM + (STATS ? WM * 2 * BN * 4 : 0) <= 160 * 1024, "exceeds the 160 KiB LDS of a CU");
   __shared__ __attribute__((aligned(16))) char smem[SMEM + (STATS ? WM * 2 * BN * 4 : 0)];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
@@ -838,15 +839,24 @@ static void launch_big(const ConvArgs& a, hipStream_t st) {
 
 // Tile policy (conv_set_tile or PMD_CONV_TILE): 0 auto (autotuned per shape, else
 // 128-row tiles), 1 128-row tiles only, 2 256x128 wherever legal, 3 256x256
-// wherever legal (Nout >= 256).
+// wherever legal (Nout >= 256), 4/5 8-wave 128-row tiles (see launch_w8).
 static int g_conv_tile = -1;
 void conv_set_tile(int t) { g_conv_tile = t; }
 static int conv_tile() {
   if (g_conv_tile < 0) {
     const char* e = getenv("PMD_CONV_TILE");
-    g_conv_tile = (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 0;
+    g_conv_tile = (e && e[0] >= '0' && e[0] <= '5') ? e[0] - '0' : 0;
   }
   return g_conv_tile;
+}
+
+// 8-wave 128-row tiles (4 waves per SIMD at 2 blocks/CU, half the MFMA work per
+// wave): 128x128 as 2x4 (policy 4) or 4x2 (policy 5) waves, 128x64 as 4x2
+template <bool DGRAD, bool STATS>
+static void launch_w8(const ConvArgs& a, hipStream_t st, int shape) {
+  if (a.Nout <= 64) launch_k<128, 64, 64, 2, DGRAD, STATS, true, false, 4, 2>(a, st);
+  else if (shape == 0) launch_k<128, 128, 64, 2, DGRAD, STATS, true, false, 2, 4>(a, st);
+  else launch_k<128, 128, 64, 2, DGRAD, STATS, true, false, 4, 2>(a, st);
 }
 
 static bool big_ok(const ConvArgs& a) {
@@ -861,9 +871,13 @@ static bool big_ok(const ConvArgs& a) {
 //      CU, for the short-reduction dgrads whose fused epilogue (addend, BN-backward
 //      reduce over 1-2 BN inputs) streams 3-4 activation tensors and needs the
 //      extra waves to hide HBM latency
+//   5  8-wave 128-row tile (launch_w8): 4 waves per SIMD at the LDS of a 4-wave
+//      block (measured +3..7% on several forward 3x3 / 1x1 layers, slower dgrads)
 template <bool DGRAD, bool STATS>
 static void launch_choice(int c, const ConvArgs& a, hipStream_t st) {
-  if (c == 4 && a.Nout > 64) {
+  if (c == 5 && a.Cs >= 64) {
+    launch_w8<DGRAD, STATS>(a, st, 0);
+  } else if (c == 4 && a.Nout > 64) {
     launch_k<128, 128, 32, 2, DGRAD, STATS, true>(a, st);
   } else if (c == 2 && big_ok(a) && a.Nout >= 256) {
     launch_k<256, 256, 64, 2, DGRAD, STATS, true, false, 2, 4>(a, st);
@@ -949,9 +963,10 @@ static int tune(const ConvArgs& a0, hipStream_t st) {
   }
   int best = -1;
   float best_ms = 1e30f;
-  const int ncand = 5;
+  const int ncand = 6;
   for (int c = 0; c < ncand; ++c) {
-    if ((c == 2 && !(big_ok(a) && a.Nout >= 256)) || (c == 3 && !big_ok(a)) || (c == 4 && a.Nout <= 64))
+    if ((c == 2 && !(big_ok(a) && a.Nout >= 256)) || (c == 3 && !big_ok(a)) || (c == 4 && a.Nout <= 64) ||
+        (c == 5 && (DGRAD || a.Cs < 64)))
       continue;
     launch_choice<DGRAD, STATS>(c, a, st);  // warm (code object load, caches)
     float t = 1e30f;
@@ -1005,7 +1020,9 @@ static void launch_sel(const ConvArgs& a, hipStream_t st) {
     }
   }
   const int t = conv_tile();
-  if (big_ok(a) && t == 3 && a.Nout >= 256) {
+  if ((t == 4 || t == 5) && a.Cs >= 64) {
+    launch_w8<DGRAD, STATS>(a, st, t - 4);
+  } else if (big_ok(a) && t == 3 && a.Nout >= 256) {
     launch_big<256, 256, 2, 4, DGRAD, STATS>(a, st);
   } else if (big_ok(a) && t == 2) {
     launch_big<256, 128, 4, 2, DGRAD, STATS>(a, st);

@@ -97,8 +97,15 @@ int xent_fwd_launch(const float* logits, const long long* target, float* loss, f
                     long long* correct, int N, int V, hipStream_t st);
 int xent_bwd_launch(const float* logits, const long long* target, const float* lse, const float* gloss,
                     float* grad, int N, int V, hipStream_t st);
+int zero_launch(void* ptr, long long nbytes, hipStream_t st);  // memset 0 (framework kernel)
 int sgd_launch(float* p, const float* g, float* buf, long long n, float lr, const float* lr_dev,
                float momentum, float wd, float damp, bool nesterov, bool first, hipStream_t st);
+
+// classifier GEMMs (kernels/linear.hip): C[i][j] (+)= sum_r A(i,r) B(r,j) on bf16 MFMA, fp32 I/O
+int linear_mfma_launch(const float* A, const float* B, float* C, const float* bias, long long sai,
+                       long long sar, long long sbr, long long sbj, int M, int Nc, int R, bool accumulate,
+                       hipStream_t st);
+int linear_colsum_launch(const float* g, float* db, int rows, int cols, bool accumulate, hipStream_t st);
 
 int synth_images_launch(bf16_t* x, long long* labels, int N, int H, int W, int Cp, int Creal,
                         int classes, unsigned long long seed, hipStream_t st);

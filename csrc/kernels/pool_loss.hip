@@ -301,6 +301,31 @@ int xent_bwd_launch(const float* logits, const long long* target, const float* l
                      target, lse, gloss, grad, N, V);
   return 0;
 }
+// memset(0) as a framework kernel (gradient-arena zeroing, fresh accumulators): 16-B
+// stores for the aligned bulk, bytes for the head/tail
+__global__ __launch_bounds__(256) void zero_kernel(unsigned char* __restrict__ p, long long head,
+                                                   long long n16, long long tail_off, long long tail) {
+  const long long t0 = blockIdx.x * 256ll + threadIdx.x, stride = (long long)gridDim.x * 256;
+  uint4* q = reinterpret_cast<uint4*>(p + head);
+  for (long long i = t0; i < n16; i += stride) q[i] = make_uint4(0, 0, 0, 0);
+  if (t0 < head) p[t0] = 0;
+  if (t0 < tail) p[tail_off + t0] = 0;
+}
+
+int zero_launch(void* ptr, long long nbytes, hipStream_t st) {
+  if (nbytes <= 0) return 0;
+  unsigned char* p = static_cast<unsigned char*>(ptr);
+  long long head = (16 - (reinterpret_cast<uintptr_t>(p) & 15)) & 15;
+  if (head > nbytes) head = nbytes;
+  const long long n16 = (nbytes - head) / 16;
+  const long long tail_off = head + n16 * 16, tail = nbytes - tail_off;
+  long long b = (n16 + 255) / 256;
+  if (b < 1) b = 1;
+  if (b > 4096) b = 4096;
+  hipLaunchKernelGGL(zero_kernel, dim3((int)b), dim3(256), 0, st, p, head, n16, tail_off, tail);
+  return 0;
+}
+
 int sgd_launch(float* p, const float* g, float* buf, long long n, float lr, const float* lr_dev,
                float momentum, float wd, float damp, bool nesterov, bool first, hipStream_t st) {
   hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n / 4 + 4, 8192)), dim3(256), 0, st, p, g, buf, n, lr,

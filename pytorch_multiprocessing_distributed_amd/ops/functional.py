@@ -990,8 +990,45 @@ def global_avg_pool(x):
     return _AvgPoolFn.apply(x)
 
 
+class _LinearFn(torch.autograd.Function):
+    """Classifier head (reference model/resnet.py:86,104) on the gfx950 MFMA GEMMs
+    (kernels/linear.hip): forward with the bias fused, dgrad, and the weight /
+    bias gradients written straight into the gradient arena (no AccumulateGrad
+    pass, no library GEMM or reduction kernels on the step)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        P = prims_for(x)
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        ctx.b = b
+        return P.linear_fwd(x, w, b)
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, w = ctx.saved_tensors
+        b = ctx.b
+        P = prims_for(dout)
+        dout = dout.contiguous()
+        dx = P.linear_dgrad(dout, w).to(x.dtype) if ctx.needs_input_grad[0] else None
+        tw = _grad_target(w)
+        tb = _grad_target(b) if b is not None else None
+        dw = db = None
+        if tw is not None and (b is None or tb is not None):
+            P.linear_wgrad(dout, x, tw, tb, True)
+            _ready(w, *([b] if b is not None else []))
+        else:
+            if ctx.needs_input_grad[1]:
+                dw = torch.empty_like(w, dtype=torch.float32)
+                db = torch.empty_like(b, dtype=torch.float32) if (b is not None and ctx.needs_input_grad[2]) else None
+                P.linear_wgrad(dout, x, dw, db, False)
+            elif b is not None and ctx.needs_input_grad[2]:
+                db = dout.float().sum(0)
+        return dx, dw, db
+
+
 def linear(x, lin):
-    return torch.nn.functional.linear(x, lin.weight, lin.bias)
+    return _LinearFn.apply(x, lin.weight, lin.bias)
 
 
 # ---------------------------------------------------------------------- loss

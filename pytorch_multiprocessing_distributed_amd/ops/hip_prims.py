@@ -203,6 +203,20 @@ def avgpool_bwd(dout, x_shape, dtype):
     return _C.avgpool_bwd(dout.float().contiguous(), int(x_shape[1]), int(x_shape[2]))
 
 
+# ------------------------------------------------------------- classifier
+def linear_fwd(x, w, b):
+    return _C.linear_fwd(x.float().contiguous(), w.detach(), None if b is None else b.detach())
+
+
+def linear_dgrad(dout, w):
+    return _C.linear_dgrad(dout.contiguous(), w.detach())
+
+
+def linear_wgrad(dout, x, dw, db, accumulate):
+    """dw (+)= dout^T x, db (+)= column sums of dout, into the given fp32 targets."""
+    _C.linear_wgrad(dout.contiguous(), x.contiguous(), dw, db, bool(accumulate))
+
+
 # --------------------------------------------------------------- loss/acc
 def xent_fwd(logits, target):
     loss, lse, _ = _C.xent_fwd(logits.float().contiguous(), target)

@@ -240,6 +240,29 @@ def avgpool_bwd(dout, x_shape, dtype):
     return (_f(dout) / (h * w)).reshape(n, 1, 1, c).expand(n, h, w, c).to(dtype).contiguous()
 
 
+# ------------------------------------------------------------- classifier
+def linear_fwd(x, w, b):
+    return F.linear(_f(x), _f(w.detach()), None if b is None else _f(b.detach()))
+
+
+def linear_dgrad(dout, w):
+    return _f(dout) @ _f(w.detach())
+
+
+def linear_wgrad(dout, x, dw, db, accumulate):
+    g = _f(dout).t() @ _f(x)
+    if accumulate:
+        dw.add_(g.to(dw.dtype))
+    else:
+        dw.copy_(g)
+    if db is not None:
+        s = _f(dout).sum(0)
+        if accumulate:
+            db.add_(s.to(db.dtype))
+        else:
+            db.copy_(s)
+
+
 # --------------------------------------------------------------- loss/acc
 def xent_fwd(logits, target):
     """Mean softmax cross-entropy; returns (loss[1] fp32, lse[N] fp32)."""

@@ -111,7 +111,11 @@ class FlatParams:
         self.version += 1
 
     def zero_grad(self):
-        self.grad_arena.zero_()
+        if self.grad_arena.is_cuda:
+            from ..ops.native import C
+            C.zero_(self.grad_arena)       # the framework's fill kernel, not ATen's
+        else:
+            self.grad_arena.zero_()
 
     def rebind_grads(self):
         """Re-attach .grad views (e.g. after someone set them to None)."""

@@ -137,11 +137,12 @@ def test_conv_pipeline_variants(shape, impl):
     _close(dx, dxr, 2e-2)
 
 
-@pytest.mark.parametrize("tile,pipe", [(2, 0), (2, 1), (2, 2), (3, 0), (3, 2)])
+@pytest.mark.parametrize("tile,pipe", [(2, 0), (2, 1), (2, 2), (3, 0), (3, 2), (4, 0), (5, 0)])
 @pytest.mark.parametrize("shape", R50_SHAPES + CIFAR_SHAPES, ids=lambda s: "C%d_H%d_K%d_R%d_s%d" % s)
 def test_conv_big_tiles(shape, tile, pipe):
     """8-wave 256x128 / 256x256 tiles (forced wherever legal: Cs >= 64, Nout >= 128)
-    with each LDS-DMA pipeline, fwd (+BN stats epilogue) and dgrad."""
+    with each LDS-DMA pipeline, and the 8-wave 128-row tiles (policies 4/5, Cs >= 64),
+    fwd (+BN stats epilogue) and dgrad."""
     from pytorch_multiprocessing_distributed_amd.ops.native import C as _C
     HP = _hp()
     torch.manual_seed(4)
@@ -570,3 +571,36 @@ def test_bn_stats_large_mean_shift():
             _close_norm(out.double(), ref, 5e-3)
     torch.testing.assert_close(bn.running_mean.double(), ref_bn.running_mean, rtol=1e-5, atol=1e-4)
     torch.testing.assert_close(bn.running_var.double(), ref_bn.running_var, rtol=5e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("N,K,V", [(256, 2048, 1000), (32, 512, 10), (7, 64, 33)])
+def test_linear_mfma(N, K, V):
+    """Classifier GEMMs (kernels/linear.hip, bf16 MFMA with fp32 accumulation)
+    against fp32 torch: forward (+bias), dgrad, and dW/db accumulated into
+    existing targets (the grad-arena contract)."""
+    HP = _hp()
+    torch.manual_seed(3)
+    x = torch.randn(N, K, device=DEV)
+    w = torch.randn(V, K, device=DEV) / K ** 0.5
+    b = torch.randn(V, device=DEV)
+    dout = torch.randn(N, V, device=DEV)
+    _close_norm(HP.linear_fwd(x, w, b), TP.linear_fwd(x, w, b), 1e-2)
+    _close_norm(HP.linear_dgrad(dout, w), TP.linear_dgrad(dout, w), 1e-2)
+    dw0, db0 = torch.randn(V, K, device=DEV), torch.randn(V, device=DEV)
+    dw1, db1 = dw0.clone(), db0.clone()
+    HP.linear_wgrad(dout, x, dw0, db0, True)
+    TP.linear_wgrad(dout, x, dw1, db1, True)
+    _close_norm(dw0, dw1, 1e-2)
+    _close(db0, db1, 1e-5)
+
+
+@pytest.mark.parametrize("n,off", [(1, 0), (15, 3), (4096, 0), (1000003, 5)])
+def test_zero_kernel(n, off):
+    """The framework's fill kernel (gradient-arena zero_grad, fresh accumulators):
+    unaligned head, 16-B bulk and byte tail; bytes outside the view untouched."""
+    from pytorch_multiprocessing_distributed_amd.ops.native import C
+    buf = torch.full((n + off + 7,), 7, dtype=torch.uint8, device=DEV)
+    C.zero_(buf[off:off + n])
+    torch.cuda.synchronize()
+    assert int(buf[off:off + n].sum()) == 0
+    assert bool((buf[:off] == 7).all()) and bool((buf[off + n:] == 7).all())
