@@ -59,7 +59,9 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="")
+    ap.add_argument("--tile", type=int, default=0, help="conv_set_tile policy (0 = autotuned)")
     a = ap.parse_args()
+    _C.conv_set_tile(a.tile)
     dev = "cuda"
     N = a.batch
     tot_us = tot_ideal = 0.0

@@ -604,3 +604,4 @@ def test_zero_kernel(n, off):
     torch.cuda.synchronize()
     assert int(buf[off:off + n].sum()) == 0
     assert bool((buf[:off] == 7).all()) and bool((buf[off + n:] == 7).all())
+
