@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--comm", default="c10d", choices=["c10d", "rccl"],
                     help="gradient-bucket transport: torch ProcessGroupNCCL or the native "
                          "RCCL communicator (csrc/runtime/rccl_comm.cpp)")
+    ap.add_argument("--tune_table", default="",
+                    help="load a per-shape kernel tuning table (JSON, ops/tuning.py) before warmup")
+    ap.add_argument("--save_tune_table", default="", help="rank 0 writes the tuning table after warmup")
     ap.add_argument("--with_stock", action="store_true",
                     help="also measure the stock PyTorch-ROCm comparator in this run (W=1)")
     ap.add_argument("--timeline", action="store_true",
@@ -146,8 +149,15 @@ def bench_rank(rank, world, a):
             sy.copy_(y)
             graph.replay()
             return static_loss
+    from pytorch_multiprocessing_distributed_amd.ops import tuning
+    if a.tune_table:
+        tuning.load(a.tune_table)
     for i in range(a.warmup):
         step(i)
+        if i == 0 and comm is not None:
+            tuning.sync(comm.group)         # every rank runs rank 0's kernel choices
+    if a.save_tune_table and rank == 0:
+        tuning.save(a.save_tune_table)
     torch.cuda.synchronize()
     if comm is not None:
         comm.barrier()

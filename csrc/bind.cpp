@@ -4,6 +4,7 @@
 // kernels do not support (no silent fallback), allocates its outputs through
 // the PyTorch-ROCm caching allocator and launches on the current HIP stream.
 #include <torch/extension.h>
+#include <pybind11/stl.h>
 #include <c10/hip/HIPStream.h>
 #include <c10/core/DeviceGuard.h>
 #include <hip/hip_runtime.h>
@@ -822,6 +823,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_set_autotune", &pmd::conv_set_autotune, "per-shape conv kernel autotuning on/off");
   m.def("conv_autotune_entries", &pmd::conv_autotune_entries);
   m.def("conv_autotune_clear", &pmd::conv_autotune_clear);
+  m.def("conv_autotune_export", &pmd::conv_autotune_export);
+  m.def("conv_autotune_import", &pmd::conv_autotune_import);
+  m.def("wgrad_autotune_export", &pmd::wgrad_autotune_export);
+  m.def("wgrad_autotune_import", &pmd::wgrad_autotune_import);
+  m.def("wgrad_autotune_clear", &pmd::wgrad_autotune_clear);
   m.def("conv_wgrad_set_impl", &pmd::conv_wgrad_set_impl,
         "wgrad staging variant: 0 registers, 1 LDS-DMA 64x2 (default), 2 LDS-DMA 32x4, 3 LDS-DMA 64x3");
   namespace py = pybind11;

@@ -52,30 +52,52 @@ def _run(cmd):
     return r
 
 
-def build(force=False, jobs=None, debug=False, verbose=True):
+ASAN_DIR = os.path.join(ROOT, "build", "asan")
+ASAN_FLAGS = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer"]
+
+
+def asan_runtime():
+    """Path of the clang ASan runtime to LD_PRELOAD into Python (host code only)."""
+    r = subprocess.run([HIPCC, "-print-file-name=libclang_rt.asan-x86_64.so"], capture_output=True, text=True)
+    p = r.stdout.strip()
+    return p if r.returncode == 0 and os.path.isabs(p) and os.path.exists(p) else None
+
+
+def build(force=False, jobs=None, debug=False, verbose=True, asan=False):
+    """asan=True: the host C++ (binding layer + native runtime: reducer, RCCL/xGMI
+    communicators, weight-image sets) instrumented with AddressSanitizer
+    (-Xarch_host only: GPU code is never sanitised), device kernels reused, the
+    library written to build/asan/ -- load it with PMD_EXT_DIR=build/asan and
+    the ASan runtime preloaded (tests/test_asan_cpu.py)."""
     os.makedirs(BUILD, exist_ok=True)
     inc, lib, abi = _torch_paths()
     headers = glob.glob(os.path.join(CSRC, "kernels", "*.h"))
-    opt = ["-O1", "-g"] if debug else ["-O3"]
+    opt = ["-O1", "-g"] if (debug or asan) else ["-O3"]
     common = [HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", *opt,
               "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
               *os.environ.get("PMD_EXTRA_CFLAGS", "").split()]  # A/B variant macros
     jobs_ = []
     objs = []
+    kcommon = [HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-O3",
+               "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+               *os.environ.get("PMD_EXTRA_CFLAGS", "").split()]
     for src in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))):
-        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        obj = os.path.join(BUILD, os.path.basename(src) + ".o")   # shared by the ASan build
         objs.append(obj)
         if force or _newer([src, *headers], obj):
-            jobs_.append(common + ["-c", src, "-o", obj, f"-I{os.path.join(CSRC, 'kernels')}"])
+            jobs_.append((kcommon if asan else common) + ["-c", src, "-o", obj,
+                                                          f"-I{os.path.join(CSRC, 'kernels')}"])
+    hbuild = os.path.join(ROOT, "build", "csrc_asan") if asan else BUILD
+    os.makedirs(hbuild, exist_ok=True)
     # host TUs that include torch headers: the binding layer + native runtime
     # (reducer, comm bootstrap); they are host-only C++ compiled by hipcc
     torch_tus = [os.path.join(CSRC, "bind.cpp")] + sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
     rt_headers = glob.glob(os.path.join(CSRC, "runtime", "*.h"))
     for src in torch_tus:
-        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        obj = os.path.join(hbuild, os.path.basename(src) + ".o")
         objs.append(obj)
         if force or _newer([src, *headers, *rt_headers], obj):
-            jobs_.append(common + [
+            jobs_.append(common + (ASAN_FLAGS if asan else []) + [
                 "-x", "hip", "-c", src, "-o", obj, f"-I{CSRC}",
                 *[f"-I{p}" for p in inc], f"-I{sysconfig.get_paths()['include']}",
                 "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
@@ -88,8 +110,12 @@ def build(force=False, jobs=None, debug=False, verbose=True):
             for f in [ex.submit(_run, j) for j in jobs_]:
                 f.result()
     out = target_path()
+    if asan:
+        os.makedirs(ASAN_DIR, exist_ok=True)
+        out = os.path.join(ASAN_DIR, os.path.basename(out))
     if force or jobs_ or _newer(objs, out):
         link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs,
+                *(["-Xarch_host", "-fsanitize=address", "-shared-libsan"] if asan else []),
                 f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
                 "-ltorch_python", "-l:librccl.so", f"-Wl,-rpath,{lib}",
                 "-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"]
@@ -104,8 +130,9 @@ def main():
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=None)
     ap.add_argument("--debug", action="store_true")
+    ap.add_argument("--asan", action="store_true", help="host-side AddressSanitizer build -> build/asan/")
     a = ap.parse_args()
-    build(force=a.force, jobs=a.jobs, debug=a.debug)
+    build(force=a.force, jobs=a.jobs, debug=a.debug, asan=a.asan)
 
 
 if __name__ == "__main__":

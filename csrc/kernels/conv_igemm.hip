@@ -27,6 +27,7 @@
 #include <stdlib.h>
 
 #include <map>
+#include <vector>
 #include <mutex>
 
 namespace pmd {
@@ -926,6 +927,27 @@ int conv_autotune_entries() {
 void conv_autotune_clear() {
   std::lock_guard<std::mutex> lk(g_tune_mu);
   g_tune.clear();
+}
+// flat table export/import (persisted tuning table, rank-0 broadcast): each entry
+// is the 13 key fields followed by the chosen candidate
+std::vector<int> conv_autotune_export() {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  std::vector<int> out;
+  for (const auto& kv : g_tune) {
+    out.insert(out.end(), kv.first.v, kv.first.v + 13);
+    out.push_back(kv.second);
+  }
+  return out;
+}
+int conv_autotune_import(const std::vector<int>& flat) {
+  if (flat.size() % 14) return -1;
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  for (size_t i = 0; i < flat.size(); i += 14) {
+    TuneKey k;
+    for (int j = 0; j < 13; ++j) k.v[j] = flat[i + j];
+    g_tune[k] = flat[i + 13];
+  }
+  return (int)(flat.size() / 14);
 }
 
 template <bool DGRAD, bool STATS>

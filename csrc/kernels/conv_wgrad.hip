@@ -25,6 +25,7 @@
 #include <stdlib.h>
 
 #include <map>
+#include <vector>
 #include <mutex>
 
 namespace pmd {
@@ -494,6 +495,31 @@ struct WgradKey {
 };
 static std::map<WgradKey, int> g_wtune;
 static std::mutex g_wtune_mu;
+
+// flat table export/import: 11 key fields + the chosen variant per entry
+std::vector<int> wgrad_autotune_export() {
+  std::lock_guard<std::mutex> lk(g_wtune_mu);
+  std::vector<int> out;
+  for (const auto& kv : g_wtune) {
+    out.insert(out.end(), kv.first.v, kv.first.v + 11);
+    out.push_back(kv.second);
+  }
+  return out;
+}
+int wgrad_autotune_import(const std::vector<int>& flat) {
+  if (flat.size() % 12) return -1;
+  std::lock_guard<std::mutex> lk(g_wtune_mu);
+  for (size_t i = 0; i < flat.size(); i += 12) {
+    WgradKey k;
+    for (int j = 0; j < 11; ++j) k.v[j] = flat[i + j];
+    g_wtune[k] = flat[i + 11];
+  }
+  return (int)(flat.size() / 12);
+}
+void wgrad_autotune_clear() {
+  std::lock_guard<std::mutex> lk(g_wtune_mu);
+  g_wtune.clear();
+}
 static bool wgrad_autotune_on() {
   static int on = -1;
   if (on < 0) {

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace pmd {
 typedef unsigned short bf16_t;
 
@@ -32,6 +34,12 @@ void conv_set_big_pipe(int p);
 void conv_set_autotune(int on);
 int conv_autotune_entries();
 void conv_autotune_clear();
+// per-shape tuning tables (conv fwd/dgrad: 13 key ints + choice; wgrad: 11 + variant)
+std::vector<int> conv_autotune_export();
+int conv_autotune_import(const std::vector<int>& flat);
+std::vector<int> wgrad_autotune_export();
+int wgrad_autotune_import(const std::vector<int>& flat);
+void wgrad_autotune_clear();
 // grouped weight-image prep (one launch for every conv of a model)
 struct WeightPrepDesc {
   const float* w;  // fp32 [K][R][S][C] (channels_last parameter storage)

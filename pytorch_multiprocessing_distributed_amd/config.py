@@ -62,6 +62,10 @@ def build_parser():
     p.add_argument("--syncbn_comm", default="auto", choices=["auto", "xgmi", "rccl"],
                    help="SyncBN statistics transport: one-shot xGMI IPC kernel or the process "
                         "group (auto: xgmi on multi-GPU runs)")
+    p.add_argument("--tune_table", default="", type=str,
+                   help="load a per-shape kernel tuning table (JSON, ops/tuning.py) before training")
+    p.add_argument("--save_tune_table", default="", type=str,
+                   help="rank 0 writes the tuning table after the first training step")
     p.add_argument("--reducer", default="native", choices=["native", "python"],
                    help="gradient bucket reducer implementation")
     p.add_argument("--grad_compress", default="none", choices=["none", "bf16"],

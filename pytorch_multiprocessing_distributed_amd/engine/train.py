@@ -55,6 +55,18 @@ def build_loaders(args, rank, world, dev, dtype, cpad):
     return tr, te
 
 
+def _first_step_tuning(args, rank, comm):
+    """After the first step every conv shape has been met (and tuned): adopt rank
+    0's kernel choices on every rank (cudnn.benchmark state made rank-consistent),
+    and optionally persist them (ops/tuning.py)."""
+    from ..ops import tuning
+    if comm is not None:
+        tuning.sync(comm.group)
+    path = getattr(args, "save_tune_table", "")
+    if path and rank == 0:
+        tuning.save(path)
+
+
 def train_epoch(loader, model, optimizer, epoch, logger, args, rank, dev, comm=None,
                 step_offset=0):
     batch_time = DeviceMeter()
@@ -79,6 +91,8 @@ def train_epoch(loader, model, optimizer, epoch, logger, args, rank, dev, comm=N
             optimizer.step()
         if comm is not None:
             comm.raise_if_failed()      # xGMI SyncBN timeout of a finished step (no device sync)
+        if step_offset + i == 0 and dev.type == "cuda":
+            _first_step_tuning(args, rank, comm)
         if comm is not None and comm.order_check_every and (step_offset + i) % comm.order_check_every == 0:
             comm.verify_order(model.collective_signature())
         bsz = inp.size(0)
@@ -203,6 +217,9 @@ def _run(rank, world_size, args, dev):
     train_loader, test_loader = build_loaders(args, rank, world_size, dev, dtype, cpad)
     if args.seed is not None:
         torch.manual_seed(args.seed)
+    if on_gpu and getattr(args, "tune_table", ""):
+        from ..ops import tuning
+        tuning.load(args.tune_table)
     model = build_model(args.model, num_classes=args.num_classes, stem=args.stem).to(dev)
     comm = get_comm()
     setup_syncbn(comm, args.sync_bn, getattr(args, "syncbn_comm", "auto"), on_gpu)

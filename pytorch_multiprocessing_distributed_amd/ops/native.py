@@ -28,6 +28,18 @@ def _ensure_built():
 
 def _load():
     import torch  # noqa: F401  (libtorch must be loaded first)
+    ext_dir = os.environ.get("PMD_EXT_DIR")
+    if ext_dir:   # an alternative build of _C (e.g. the host-ASan one, csrc/build.py --asan)
+        import importlib.util as _ilu
+        import sysconfig
+        path = os.path.join(ext_dir, "_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+        spec = _ilu.spec_from_file_location("pytorch_multiprocessing_distributed_amd._C", path)
+        if spec is None or not os.path.exists(path):
+            raise ImportError(f"PMD_EXT_DIR={ext_dir}: no extension at {path}")
+        mod = _ilu.module_from_spec(spec)
+        sys.modules[spec.name] = mod
+        spec.loader.exec_module(mod)
+        return mod
     try:
         return importlib.import_module("pytorch_multiprocessing_distributed_amd._C")
     except ImportError:

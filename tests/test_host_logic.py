@@ -252,3 +252,10 @@ def test_post_accumulate_hook_skips_claimed_params():
     assert marks == [p] and not p._pmd_claim
     post(p)
     assert len(marks) == 2          # unclaimed again (the reducer's mark is idempotent)
+
+
+def test_native_extension_imports():
+    """The in-tree extension loads through ops/native.py (the path every GPU op
+    takes); it is built by csrc/build.py for gfx950 but imports on any host."""
+    from pytorch_multiprocessing_distributed_amd.ops.native import C
+    assert C.__file__.endswith(".so") and hasattr(C, "conv_fwd")

@@ -605,3 +605,32 @@ def test_zero_kernel(n, off):
     assert int(buf[off:off + n].sum()) == 0
     assert bool((buf[:off] == 7).all()) and bool((buf[off + n:] == 7).all())
 
+
+
+def test_tuning_table_roundtrip(tmp_path):
+    """Per-shape tuning tables (ops/tuning.py): the tuned choices of a conv
+    fwd/dgrad/wgrad export, survive clear + load from JSON, and an imported
+    table is used as-is (no re-tuning: the entry count does not grow)."""
+    from pytorch_multiprocessing_distributed_amd.ops import tuning
+    from pytorch_multiprocessing_distributed_amd.ops.native import C as _C
+    HP = _hp()
+    _C.conv_autotune_clear()
+    _C.wgrad_autotune_clear()
+    x = torch.randn(4, 14, 14, 64, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(128, 64, 3, 3, device=DEV) / 24).contiguous(memory_format=torch.channels_last)
+    wp = HP.conv_weight(w, torch.bfloat16, 64, True)
+    y, _ = HP.conv_fwd(x, wp, 1, 1, False)
+    HP.conv_dgrad(torch.randn_like(y), wp, tuple(x.shape), 1, 1)
+    HP.conv_wgrad(torch.randn_like(y), x, (128, 3, 3, 64), 1, 1)
+    torch.cuda.synchronize()
+    tab = tuning.export_table()
+    assert len(tab["conv"]) == 2 and len(tab["wgrad"]) == 1, tab
+    path = str(tmp_path / "t.json")
+    tuning.save(path)
+    _C.conv_autotune_clear()
+    _C.wgrad_autotune_clear()
+    assert tuning.load(path) == 3
+    assert tuning.export_table()["conv"] == tab["conv"]
+    y2, _ = HP.conv_fwd(x, wp, 1, 1, False)
+    torch.cuda.synchronize()
+    assert _C.conv_autotune_entries() == 2 and torch.equal(y, y2)

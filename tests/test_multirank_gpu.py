@@ -172,7 +172,10 @@ def test_native_rccl_comm_single_rank_reducer():
             m = build_model("res").cuda()
             dp = DataParallel(m, comm if transport else None, bucket_mb=0.5, first_bucket_mb=0.1,
                               transport=transport or "c10d", timeline=True)
-            opt = FusedSGD(dp, lr=0.05)
+            # eval-mode BN and lr 0: the gradient is a deterministic function of the
+            # weights (tests/test_model_oracle_gpu.py: training-mode BN at init is chaotic)
+            dp.module.eval()
+            opt = FusedSGD(dp, lr=0.0)
             for _ in range(2):
                 loss = OF.cross_entropy(dp(x), y)
                 opt.zero_grad()
@@ -186,10 +189,11 @@ def test_native_rccl_comm_single_rank_reducer():
                 tl = dp.bucket_timeline()
                 assert len(tl) == len(dp.buckets) and all(r[4] == r[4] for r in tl)   # device times set
                 dp.shutdown()
-        # same model, same kernels; only fp32-atomic summation order differs between runs
+        # same model, same kernels, deterministic split-K reduction: the single-rank
+        # averaging all-reduce over the native communicator must not change a bit
         for n, g in grads[None].items():
             rel = ((grads["rccl"][n] - g).float().norm() / g.float().norm().clamp_min(1e-12)).item()
-            assert rel < 2e-2, (n, rel)
+            assert rel < 1e-6, (n, rel)
     finally:
         dist.destroy_process_group()
 
