@@ -815,13 +815,14 @@ static void launch_t(const ConvArgs& a, hipStream_t st, int impl) {
 }
 
 // 8-wave 256-row tiles (LDS-DMA only; one block per CU).  Pipeline by
-// PMD_CONV_BIGPIPE: 0 (default) BK=64 x2 stages, 1 BK=64 x3, 2 BK=32 x4.
+// PMD_CONV_BIGPIPE: 0 (default) BK=64 x2 stages, 1 BK=64 x3, 2 BK=32 x4, 3 BK=64 x2 on
+// the 32x32x16 MFMA.
 static int g_big_pipe = -1;
 void conv_set_big_pipe(int p) { g_big_pipe = p; }
 static int big_pipe() {
   if (g_big_pipe < 0) {
     const char* e = getenv("PMD_CONV_BIGPIPE");
-    g_big_pipe = (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 0;
+    g_big_pipe = (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 0;
   }
   return g_big_pipe;
 }
@@ -834,6 +835,10 @@ static void launch_big(const ConvArgs& a, hipStream_t st) {
       else launch_k<BM, BN, 64, 2, DGRAD, STATS, true, false, WM, WN>(a, st);
       break;
     case 2: launch_k<BM, BN, 32, 4, DGRAD, STATS, true, false, WM, WN>(a, st); break;
+    case 3:  // 32x32x16 MFMA (half the MFMA instructions per FLOP); needs the uniform-tap loader
+      if (a.Cs % 64 == 0) launch_k<BM, BN, 64, 2, DGRAD, STATS, true, true, WM, WN>(a, st);
+      else launch_k<BM, BN, 64, 2, DGRAD, STATS, true, false, WM, WN>(a, st);
+      break;
     default: launch_k<BM, BN, 64, 2, DGRAD, STATS, true, false, WM, WN>(a, st); break;
   }
 }

@@ -137,7 +137,7 @@ def test_conv_pipeline_variants(shape, impl):
     _close(dx, dxr, 2e-2)
 
 
-@pytest.mark.parametrize("tile,pipe", [(2, 0), (2, 1), (2, 2), (3, 0), (3, 2), (4, 0), (5, 0)])
+@pytest.mark.parametrize("tile,pipe", [(2, 0), (2, 1), (2, 2), (2, 3), (3, 0), (3, 2), (3, 3), (4, 0), (5, 0)])
 @pytest.mark.parametrize("shape", R50_SHAPES + CIFAR_SHAPES, ids=lambda s: "C%d_H%d_K%d_R%d_s%d" % s)
 def test_conv_big_tiles(shape, tile, pipe):
     """8-wave 256x128 / 256x256 tiles (forced wherever legal: Cs >= 64, Nout >= 128)
