@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--impl", type=int, default=5)
     ap.add_argument("--pass", dest="which", default="fwd")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--nostats", action="store_true", help="forward without BN statistics")
     a = ap.parse_args()
     _C.conv_set_autotune(0)
     _C.conv_set_tile(a.tile)
@@ -35,14 +36,23 @@ def main():
     wp = HP.conv_weight(w, torch.bfloat16, a.C, True)
     y, s = HP.conv_fwd(x, wp, a.stride, pad, True)
     dy = torch.randn_like(y)
+    ts = []
     for _ in range(a.iters):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
         if a.which == "fwd":
-            y, s = HP.conv_fwd(x, wp, a.stride, pad, True)
-            HP._release(s)
+            y, s = HP.conv_fwd(x, wp, a.stride, pad, not a.nostats)
+            if s is not None:
+                HP._release(s)
         else:
             HP.conv_dgrad(dy, wp, tuple(x.shape), a.stride, pad)
+        e1.record()
+        ts.append((e0, e1))
     torch.cuda.synchronize()
-    print("done")
+    us = sorted(e0.elapsed_time(e1) * 1e3 for e0, e1 in ts[2:])
+    print(f"done {a.which} C{a.C} H{a.H} K{a.K} R{a.R} s{a.stride} tile {a.tile} impl {a.impl} "
+          f"stats {not a.nostats}: {us[len(us) // 2]:.1f} us")
 
 
 if __name__ == "__main__":

@@ -92,12 +92,21 @@ __device__ __forceinline__ int swz(int row) {
 // 4x2 / 2x4 = 256-row tiles at one 8-wave block per CU, i.e. half the operand
 // bytes per MFMA FLOP from L2 (128x128: 64 FLOP/B -> 256x128: 85, 256x256: 128),
 // for the layers whose grid still fills the chip with the bigger tile.
+//
+// P8: register-resident fragment pipeline (LDS-DMA, BK=64, 2 LDS buffers, uniform-tap
+// loader): a whole K-tile's A/B fragments live in VGPRs, so the LDS buffer they came
+// from is re-filled (tile kt+2) right after ONE barrier while the tile's MFMAs run from
+// registers; the DMA queue never drains to zero inside the loop (counted vmcnt leaves
+// the next tile's loads in flight across both barriers of a K-tile), and the next
+// tile's fragments are read into each register set as soon as its MFMAs retire
+// (cdna_hip_programming.md §5 "Pipelining across barriers", T3/T4, T5).
 template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA, bool MF32 = false,
-          int WM = 2, int WN = 2>
+          int WM = 2, int WN = 2, bool P8 = false>
 __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   static_assert(DMA || (BK == 64 && NST == 2 && NW == 4), "register staging: BK=64, 2 stages, 4 waves");
   static_assert(!MF32 || (DMA && BK == 64), "32x32 MFMA path: LDS-DMA, BK=64");
+  static_assert(!P8 || (DMA && BK == 64 && NST == 2 && !MF32), "P8: LDS-DMA, BK=64, 2 buffers, 16x16 MFMA");
   constexpr int CH = BK / 8;                      // 16-B chunks per LDS row
   constexpr int RPI = DMA ? 64 / CH : 32;         // rows per load instruction (wave / block)
   constexpr int PA = DMA ? BM / (NW * RPI) : BM / 32;  // A load instructions per thread per tile
@@ -440,8 +449,77 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
       compute(kt % NST);
     }
     };
-    if (uni) pipeline(load_tile_uni);
-    else pipeline(load_tile);
+    if constexpr (P8) {
+      if (uni) {
+        static_assert(MI % 2 == 0, "P8 splits the wave's row tiles in two halves");
+        bf16x8 fa[MI][2], fb[NI][2];
+        auto rd_a = [&](int buf, int i) {
+          const bf16_t* As = lds + buf * STAGE;
+#pragma unroll
+          for (int kh = 0; kh < 2; ++kh) fa[i][kh] = frag(As, wm * (BM / WM) + i * 16 + frow, kh * 4 + (lane >> 4));
+        };
+        auto rd_b = [&](int buf) {
+          const bf16_t* Bs = lds + buf * STAGE + A_ELEMS;
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+#pragma unroll
+            for (int kh = 0; kh < 2; ++kh)
+              fb[j][kh] = frag(Bs, wn * (BN / WN) + j * 16 + frow, kh * 4 + (lane >> 4));
+        };
+        auto mma = [&](int i) {
+#pragma unroll
+          for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int j = 0; j < NI; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kh], fb[j][kh], acc[i][j], 0, 0, 0);
+        };
+        // prologue: tiles 0 and 1 in flight, tile 0's fragments in registers
+        load_tile_uni(0, 0);
+        if (nk > 1) {
+          load_tile_uni(1, 1);
+          wait_vmcnt<LPT>();
+        } else {
+          wait_vmcnt<0>();
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < MI; ++i) rd_a(0, i);
+        rd_b(0);
+        for (int kt = 0; kt < nk; ++kt) {
+          const int cur = kt & 1;
+          // every wave's fragment reads of buffer `cur` have retired: re-fill it
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          if (kt + 2 < nk) load_tile_uni(kt + 2, cur);
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int i = 0; i < MI / 2; ++i) mma(i);
+          __builtin_amdgcn_s_setprio(0);
+          const bool more = kt + 1 < nk;
+          if (more) {
+            // tile kt+1 landed (only tile kt+2's loads may still fly) and is visible
+            if (kt + 2 < nk) wait_vmcnt<LPT>();
+            else wait_vmcnt<0>();
+            asm volatile("s_barrier" ::: "memory");
+#pragma unroll
+            for (int i = 0; i < MI / 2; ++i) rd_a(cur ^ 1, i);
+          }
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int i = MI / 2; i < MI; ++i) mma(i);
+          __builtin_amdgcn_s_setprio(0);
+          if (more) {
+#pragma unroll
+            for (int i = MI / 2; i < MI; ++i) rd_a(cur ^ 1, i);
+            rd_b(cur ^ 1);
+          }
+        }
+      } else {
+        pipeline(load_tile);
+      }
+    } else {
+      if (uni) pipeline(load_tile_uni);
+      else pipeline(load_tile);
+    }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   } else {
     if (nk > 0) {
@@ -784,14 +862,26 @@ static int conv_impl() {
 }
 
 template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA, bool MF32 = false,
-          int WM = 2, int WN = 2>
+          int WM = 2, int WN = 2, bool P8 = false>
 static void launch_k(const ConvArgs& a, hipStream_t st) {
   const bool ph2 = DGRAD && a.stride == 2;
   const int Mgrid = ph2 ? a.N * ((a.OH + 1) >> 1) * ((a.OW + 1) >> 1) : a.M;
   const int tiles = ((Mgrid + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
   const int phases = ph2 ? 4 : 1;
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, NST, DGRAD, STATS, DMA, MF32, WM, WN>),
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, NST, DGRAD, STATS, DMA, MF32, WM, WN, P8>),
                      dim3(tiles, phases), dim3(64 * WM * WN), 0, st, a);
+}
+
+// P8 register-resident fragment pipeline (see the kernel): 0 = 256x256 (8 waves 2x4),
+// 1 = 256x128 (8 waves 4x2), 2 = 128x128 (4 waves 2x2), 3 = 128x128 (8 waves 4x2)
+template <bool DGRAD, bool STATS>
+static void launch_p8(const ConvArgs& a, hipStream_t st, int shape) {
+  switch (shape) {
+    case 0: launch_k<256, 256, 64, 2, DGRAD, STATS, true, false, 2, 4, true>(a, st); break;
+    case 1: launch_k<256, 128, 64, 2, DGRAD, STATS, true, false, 4, 2, true>(a, st); break;
+    case 3: launch_k<128, 128, 64, 2, DGRAD, STATS, true, false, 4, 2, true>(a, st); break;
+    default: launch_k<128, 128, 64, 2, DGRAD, STATS, true, false, 2, 2, true>(a, st); break;
+  }
 }
 
 template <int BM, int BN, bool DGRAD, bool STATS>
@@ -845,13 +935,14 @@ static void launch_big(const ConvArgs& a, hipStream_t st) {
 
 // Tile policy (conv_set_tile or PMD_CONV_TILE): 0 auto (autotuned per shape, else
 // 128-row tiles), 1 128-row tiles only, 2 256x128 wherever legal, 3 256x256
-// wherever legal (Nout >= 256), 4/5 8-wave 128-row tiles (see launch_w8).
+// wherever legal (Nout >= 256), 4/5 8-wave 128-row tiles (see launch_w8),
+// 6..9 the P8 pipeline shapes 0..3 (see launch_p8) wherever legal.
 static int g_conv_tile = -1;
 void conv_set_tile(int t) { g_conv_tile = t; }
 static int conv_tile() {
   if (g_conv_tile < 0) {
     const char* e = getenv("PMD_CONV_TILE");
-    g_conv_tile = (e && e[0] >= '0' && e[0] <= '5') ? e[0] - '0' : 0;
+    g_conv_tile = (e && e[0] >= '0' && e[0] <= '9') ? e[0] - '0' : 0;
   }
   return g_conv_tile;
 }
@@ -879,9 +970,19 @@ static bool big_ok(const ConvArgs& a) {
 //      extra waves to hide HBM latency
 //   5  8-wave 128-row tile (launch_w8): 4 waves per SIMD at the LDS of a 4-wave
 //      block (measured +3..7% on several forward 3x3 / 1x1 layers, slower dgrads)
+//   6..9 P8 pipeline shapes 0..3 (launch_p8): needs the uniform-tap loader (Cs % 64 == 0);
+//      256-row shapes need >= 128 output channels (256x256: >= 256)
+static bool p8_ok(int shape, const ConvArgs& a) {
+  if (a.Cs % 64 != 0) return false;
+  if (shape == 0) return a.Nout >= 256;
+  if (shape == 1) return a.Nout >= 128;
+  return a.Nout > 64;
+}
 template <bool DGRAD, bool STATS>
 static void launch_choice(int c, const ConvArgs& a, hipStream_t st) {
-  if (c == 5 && a.Cs >= 64) {
+  if (c >= 6 && c <= 9 && p8_ok(c - 6, a)) {
+    launch_p8<DGRAD, STATS>(a, st, c - 6);
+  } else if (c == 5 && a.Cs >= 64) {
     launch_w8<DGRAD, STATS>(a, st, 0);
   } else if (c == 4 && a.Nout > 64) {
     launch_k<128, 128, 32, 2, DGRAD, STATS, true>(a, st);
@@ -990,10 +1091,12 @@ static int tune(const ConvArgs& a0, hipStream_t st) {
   }
   int best = -1;
   float best_ms = 1e30f;
+  // the P8 shapes (6..9) measured equal or slower than 0..5 on every R50 layer
+  // (profiles/conv_p8_r02.txt): forced-policy only, not timed by the tuner
   const int ncand = 6;
   for (int c = 0; c < ncand; ++c) {
     if ((c == 2 && !(big_ok(a) && a.Nout >= 256)) || (c == 3 && !big_ok(a)) || (c == 4 && a.Nout <= 64) ||
-        (c == 5 && (DGRAD || a.Cs < 64)))
+        (c == 5 && (DGRAD || a.Cs < 64)) || (c >= 6 && !p8_ok(c - 6, a)))
       continue;
     launch_choice<DGRAD, STATS>(c, a, st);  // warm (code object load, caches)
     float t = 1e30f;
@@ -1047,7 +1150,9 @@ static void launch_sel(const ConvArgs& a, hipStream_t st) {
     }
   }
   const int t = conv_tile();
-  if ((t == 4 || t == 5) && a.Cs >= 64) {
+  if (t >= 6 && p8_ok(t - 6, a)) {
+    launch_p8<DGRAD, STATS>(a, st, t - 6);
+  } else if ((t == 4 || t == 5) && a.Cs >= 64) {
     launch_w8<DGRAD, STATS>(a, st, t - 4);
   } else if (big_ok(a) && t == 3 && a.Nout >= 256) {
     launch_big<256, 256, 2, 4, DGRAD, STATS>(a, st);
