@@ -21,8 +21,21 @@
 #ifndef PMD_EW_U
 #define PMD_EW_U 1
 #endif
+#ifndef PMD_EW_NT
+#define PMD_EW_NT 0  // 1: non-temporal output stores in the elementwise passes (A/B knob)
+#endif
 
 namespace pmd {
+
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st16(void* p, const uint4& v) {
+  if constexpr (PMD_EW_NT) {
+    const u32x4_t w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(p));
+  } else {
+    *reinterpret_cast<uint4*>(p) = v;
+  }
+}
 
 __device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
   const float4 a = *reinterpret_cast<const float4*>(p);
@@ -124,7 +137,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
         v[k] = o;
       }
       const uint4 pk = pack8(v);
-      reinterpret_cast<uint4*>(out)[i] = pk;
+      st16(reinterpret_cast<uint4*>(out) + i, pk);
       if (RELU && mask_out) mask_out[i] = (uint8_t)bits;
       if (Q8) {
         float o[8];
@@ -292,8 +305,8 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(
         d[k] = dz;
         o[k] = EVAL ? ca[k] * dz : ca[k] * dz + cb[k] * v[k] + cc[k];
       }
-      reinterpret_cast<uint4*>(dy)[i] = pack8(o);
-      if (DZM) reinterpret_cast<uint4*>(dzm_out)[i] = pack8(d);
+      st16(reinterpret_cast<uint4*>(dy) + i, pack8(o));
+      if (DZM) st16(reinterpret_cast<uint4*>(dzm_out) + i, pack8(d));
     }
   }
 }

@@ -77,10 +77,24 @@ __device__ __forceinline__ void wait_vmcnt() {
 //            ONE barrier per K-tile (it both publishes tile kt and retires the
 //            reads of the buffer the next DMA overwrites).
 // DMA=false: register staging into 144-B padded rows, 2 stages (BK=64 only).
+// PMD_CONV_SWZ=1: swizzles that make the 16 rows of one ds_read_b128 lane group
+// hit 16 distinct 16-B bank slots (64 banks x 4 B): 128-B rows (BK=64) pair up
+// rows by bit 0 (the two halves of the bank row), so the chunk XOR uses row
+// bits 1..3; 64-B rows (BK=32) put 4 rows in one bank row, so it uses bits 2..3.
+// Both are periodic in 16 rows, so a DMA instruction's rows (a multiple-of-16
+// slab base + RPI i + lane / CH) get their chunk from the in-slab row alone.
+#ifndef PMD_CONV_SWZ
+#define PMD_CONV_SWZ 0
+#endif
 template <int BK>
 __device__ __forceinline__ int swz(int row) {
-  if constexpr (BK == 64) return row & 7;
-  else return (row >> 2) & 2;
+  if constexpr (PMD_CONV_SWZ) {
+    if constexpr (BK == 64) return (row >> 1) & 7;
+    else return (row >> 2) & 3;
+  } else {
+    if constexpr (BK == 64) return row & 7;
+    else return (row >> 2) & 2;
+  }
 }
 
 // MF32: v_mfma_f32_32x32x16_bf16 instead of 16x16x32 (same FLOPs in half the
@@ -166,7 +180,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
   // register staging: thread -> (row rsub + 32 i, chunk tid & 7)
   // DMA: wave w, instruction i, lane l -> row w*(BM/4) + RPI i + l/CH, LDS chunk l%CH
   //      holding logical chunk (l%CH) ^ swz(row)
-  const int chunk = DMA ? ((lane % CH) ^ swz<BK>(lane / CH)) : (tid & 7);
+  // DMA: LDS chunk lane % CH of A (B) instruction i's tile row holds logical chunk
+  // achunk(i) (bchunk(i)); the swizzle is taken of the absolute tile row
+  auto achunk = [&](int i) { return DMA ? ((lane % CH) ^ swz<BK>(wid * (BM / NW) + RPI * i + lane / CH)) : (tid & 7); };
+  auto bchunk = [&](int i) { return DMA ? ((lane % CH) ^ swz<BK>(wid * (BN / NW) + RPI * i + lane / CH)) : (tid & 7); };
+  const int chunk = tid & 7;  // register staging
   const int rsub = tid >> 3;  // 0..31
   auto a_row_of = [&](int i) { return DMA ? wid * (BM / NW) + RPI * i + lane / CH : rsub + 32 * i; };
   auto b_row_of = [&](int i) { return DMA ? wid * (BN / NW) + RPI * i + lane / CH : rsub + 32 * i; };
@@ -218,7 +236,6 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
     u_w[i] = ww;
     u_p[i] = a_base[i] + hh * a.W + ww;
   }
-  const int lane_c = (lane % CH ^ swz<BK>(lane / CH)) * 8;  // == chunk * 8 on the DMA path
   // MF32 swizzle depends on row bits 1..3: instruction i covers rows base + 8i + l/8 with
   // base % 32 == 0 (BM/4, BN/4 multiples of 16 -> (base >> 1) % 8 == 0)
   const int lane_c32[2] = {((lane & 7) ^ (((lane >> 3) >> 1) & 7)) * 8,
@@ -236,10 +253,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
   // per-row source pointers at tap (0,0) channel 0 (+ this lane's chunk); a tile
   // then only adds the wave-uniform offset (dr*W + ds)*Cs + cb
   const bf16_t* a_ptr[PA];
-  const int lane_ci = (lane % CH ^ swz<BK>(lane / CH)) * 8;
 #pragma unroll
   for (int i = 0; i < PA; ++i) {
-    const int ci = MF32 ? lane_c32[i & 1] : lane_ci;
+    const int ci = MF32 ? lane_c32[i & 1] : achunk(i) * 8;
     // signed: u_p is -1.. at padded borders (never dereferenced there: `ok` masks it)
     a_ptr[i] = a.src + ((long long)u_p[i] << a.log2Cs) + ci;
   }
@@ -271,7 +287,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
     }
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
-      const int boff = tapo + (MF32 ? lane_c32[i & 1] : lane_ci);
+      const int boff = tapo + (MF32 ? lane_c32[i & 1] : bchunk(i) * 8);
       const void* src = (b_ok[i] && kok) ? (const void*)(b_row[i] + boff) : (const void*)g_zero16;
       bf16_t* dst = lds + dbuf * STAGE + A_ELEMS + (wid_s * (BN / NW) + RPI * i) * LDR;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
@@ -290,16 +306,15 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
   };
 
   auto load_tile = [&](int kt, int dbuf) {
-    const int k0 = kt * BK + chunk * 8;
-    const bool kok = k0 < Kgp;
-    const int tap = k0 >> a.log2Cs;
-    const int c = k0 & (a.Cs - 1);
-    const int tr = tap / ns;
-    const int r = r0 + rstep * tr;
-    const int s = s0 + rstep * (tap - tr * ns);
-    const int boff = ((r * a.S + s) << a.log2Cs) + c;
 #pragma unroll
     for (int i = 0; i < PA; ++i) {
+      const int k0 = kt * BK + achunk(i) * 8;
+      const bool kok = k0 < Kgp;
+      const int tap = k0 >> a.log2Cs;
+      const int c = k0 & (a.Cs - 1);
+      const int tr = tap / ns;
+      const int r = r0 + rstep * tr;
+      const int s = s0 + rstep * (tap - tr * ns);
       int ih, iw;
       bool ok = a_ok[i] && kok;
       if (DGRAD) {
@@ -329,6 +344,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
     }
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
+      const int k0 = kt * BK + bchunk(i) * 8;
+      const bool kok = k0 < Kgp;
+      const int tap = k0 >> a.log2Cs;
+      const int tr = tap / ns;
+      const int r = r0 + rstep * tr;
+      const int s = s0 + rstep * (tap - tr * ns);
+      const int boff = ((r * a.S + s) << a.log2Cs) + (k0 & (a.Cs - 1));
       if constexpr (DMA) {
         const void* src = (b_ok[i] && kok) ? (const void*)(b_row[i] + boff) : (const void*)g_zero16;
         bf16_t* dst = lds + dbuf * STAGE + A_ELEMS + (wid * (BN / NW) + RPI * i) * LDR;

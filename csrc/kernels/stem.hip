@@ -77,57 +77,78 @@ __global__ __launch_bounds__(256) void stem_pool_fwd_kernel(const bf16_t* __rest
   reinterpret_cast<uint2*>(arg)[o] = packed;
 }
 
-// dz of one 8-channel input chunk (n, h, w, cc): the bf16-rounded sum of the
-// dout of the (<= 4) windows whose argmax is this pixel, gated by the ReLU.
-__device__ __forceinline__ void stem_dz(const bf16_t* __restrict__ dout, const uint8_t* __restrict__ arg,
-                                        int n, int h, int w, int cc, int C8, int P, int Q,
-                                        const float (&v)[8], const float (&sc)[8], const float (&sh)[8],
-                                        float (&dz)[8]) {
-  float acc[8];
+// Backward of the fused stem tail.  Block = (image n, pooled row p): it owns
+// input rows 2p and 2p+1 -- exactly the rows whose windows lie in pooled rows p
+// and p+1 -- and stages those two pooled rows of dout and argmax taps in LDS
+// once, so every input pixel reads its (1, 2 or 4) candidate windows from LDS
+// instead of gathering 4 clamped windows from L2 (8 global loads per 16-B
+// output chunk before; profiles/pool_bench).  Candidates are visited in
+// ascending (p, q) order, the order of the composite maxpool_bwd sum.
+struct StemBwdTile {
+  const bf16_t* dl;   // LDS [2][Q][C] pooled gradient of rows p, p+1
+  const uint8_t* al;  // LDS [2][Q][C] argmax taps
+  int p, P, Q, C8;
+  // dz of the 8-channel chunk (h, w, cc): bf16-rounded sum of the dout of the
+  // windows whose argmax is this pixel, gated by the ReLU of BN(y)
+  __device__ __forceinline__ void dz(int h, int w, int cc, const float (&v)[8], const float (&sc)[8],
+                                     const float (&sh)[8], float (&out)[8]) const {
+    float acc[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-  // windows p with 2p-1 <= h <= 2p+1: p in {h>>1, (h+1)>>1} (one or two of them);
-  // always visit the 2x2 candidates with clamped indices and mask the invalid
-  // ones, so the (up to) 4 gathers are independent loads
-  const int pa = h >> 1, qa = w >> 1;
-  uint2 av[4];
-  uint4 gv[4];
-  int tp[4];
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    const int odd_h = h & 1, odd_w = w & 1;
+    const int q0 = w >> 1;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int p = pa + (u >> 1), q = qa + (u & 1);
-    const int dh = h - (p * 2 - 1), dw = w - (q * 2 - 1);
-    const bool ok = p < P && q < Q && dh >= 0 && dh <= 2 && dw >= 0 && dw <= 2;
-    tp[u] = ok ? dh * 3 + dw : -1;
-    const size_t o = (((size_t)n * P + min(p, P - 1)) * Q + min(q, Q - 1)) * C8 + cc;
-    av[u] = reinterpret_cast<const uint2*>(arg)[o];
-    gv[u] = reinterpret_cast<const uint4*>(dout)[o];
+    for (int a = 0; a < 2; ++a) {      // pooled row p + a
+      if (a == 1 && (!odd_h || p + 1 >= P)) break;
+      const int dh = odd_h ? (a == 0 ? 2 : 0) : 1;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {    // pooled col q0 + b
+        if (b == 1 && (!odd_w || q0 + 1 >= Q)) break;
+        const int dw = odd_w ? (b == 0 ? 2 : 0) : 1;
+        const int tp = dh * 3 + dw;
+        const int o = (a * Q + q0 + b) * C8 + cc;
+        const uint4 gv = reinterpret_cast<const uint4*>(dl)[o];
+        const uint2 av = reinterpret_cast<const uint2*>(al)[o];
+        float g[8];
+        unpack8(gv, g);
+        const uint32_t aw[2] = {av.x, av.y};
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if ((int)((aw[k >> 2] >> ((k & 3) * 8)) & 0xff) == tp) acc[k] += g[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) out[k] = (v[k] * sc[k] + sh[k] > 0.f) ? round_bf(acc[k]) : 0.f;
   }
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    float g[8];
-    unpack8(gv[u], g);
-    const uint32_t aw[2] = {av[u].x, av[u].y};
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if ((int)((aw[k >> 2] >> ((k & 3) * 8)) & 0xff) == tp[u]) acc[k] += g[k];
+};
+
+// stage pooled rows p, p+1 (the second only if it exists) of image n into LDS
+__device__ __forceinline__ void stem_stage_pooled(const bf16_t* __restrict__ dout, const uint8_t* __restrict__ arg,
+                                                  bf16_t* dl, uint8_t* al, int n, int p, int P, int Q, int C8) {
+  const int per_row = Q * C8;
+  const int rows = p + 1 < P ? 2 : 1;
+  const size_t base = ((size_t)n * P + p) * per_row;
+  for (int i = threadIdx.x; i < rows * per_row; i += blockDim.x) {
+    reinterpret_cast<uint4*>(dl)[i] = reinterpret_cast<const uint4*>(dout)[base + i];
+    reinterpret_cast<uint2*>(al)[i] = reinterpret_cast<const uint2*>(arg)[base + i];
   }
-#pragma unroll
-  for (int k = 0; k < 8; ++k) dz[k] = (v[k] * sc[k] + sh[k] > 0.f) ? round_bf(acc[k]) : 0.f;
 }
 
 // Pass 1: per-channel sum(dz), sum(dz * xhat) into kStatSlots slot copies.
-// Block = a run of input rows (n, h); thread tid keeps channel chunk tid % C8
-// for the whole block (256 % C8 == 0), partials combined in LDS, one atomic
-// per channel per block.
+// Dynamic LDS: 2*Q*C*2 B pooled gradient + 2*Q*C B taps; the 256x17 partials
+// reuse the same bytes after the compute loop.
 __global__ __launch_bounds__(256) void stem_pool_bwd_reduce_kernel(
     const bf16_t* __restrict__ dout, const uint8_t* __restrict__ arg, const bf16_t* __restrict__ y,
     const float* __restrict__ params, float* __restrict__ red, int N, int H, int W, int C, int P, int Q,
-    int rows_per_block, int log2C8) {
-  __shared__ float part[256 * 17];
+    int log2C8) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char stem_lds[];
   const int C8 = C >> 3;
   const int tid = threadIdx.x;
-  const int cc = tid % C8;
+  const int cc = tid & (C8 - 1);
+  const int n = blockIdx.x / P, p = blockIdx.x - n * P;
+  bf16_t* dl = reinterpret_cast<bf16_t*>(stem_lds);
+  uint8_t* al = stem_lds + (size_t)2 * Q * C * 2;
+  stem_stage_pooled(dout, arg, dl, al, n, p, P, Q, C8);
   float mean[8], inv[8], sc[8], sh[8];
   ld8(params + cc * 8, mean);
   ld8(params + C + cc * 8, inv);
@@ -136,22 +157,25 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_reduce_kernel(
   float s1[8], s2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
-  const int r0 = blockIdx.x * rows_per_block;
-  const int r1 = min(r0 + rows_per_block, N * H);
-  for (int row = r0; row < r1; ++row) {
-    const int n = row / H, h = row - (row / H) * H;
-    for (int j = tid; j < W * C8; j += 256) {
-      const int w = j >> log2C8;
-      float v[8], dz[8];
-      unpack8(reinterpret_cast<const uint4*>(y)[(size_t)row * W * C8 + j], v);
-      stem_dz(dout, arg, n, h, w, cc, C8, P, Q, v, sc, sh, dz);
+  __syncthreads();
+  const StemBwdTile t{dl, al, p, P, Q, C8};
+  const int per_row = W * C8;
+  const int h0 = 2 * p, nrow = min(2, H - h0);
+  for (int j = tid; j < nrow * per_row; j += 256) {
+    const int r = j >= per_row ? 1 : 0;
+    const int jj = j - r * per_row;
+    const int h = h0 + r, w = jj >> log2C8;
+    float v[8], d[8];
+    unpack8(reinterpret_cast<const uint4*>(y)[((size_t)n * H + h) * per_row + jj], v);
+    t.dz(h, w, cc, v, sc, sh, d);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        s1[k] += dz[k];
-        s2[k] += dz[k] * (v[k] - mean[k]);  // * invstd once, below
-      }
+    for (int k = 0; k < 8; ++k) {
+      s1[k] += d[k];
+      s2[k] += d[k] * (v[k] - mean[k]);  // * invstd once, below
     }
   }
+  __syncthreads();  // the staged pooled rows are dead: the partials reuse the LDS
+  float* part = reinterpret_cast<float*>(stem_lds);
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     part[tid * 17 + k] = s1[k];
@@ -174,13 +198,16 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_elemt_kernel(
     const bf16_t* __restrict__ dout, const uint8_t* __restrict__ arg, const bf16_t* __restrict__ y,
     const float* __restrict__ params, const float* __restrict__ gamma, const float* __restrict__ red,
     const float* __restrict__ count, float count_h, bf16_t* __restrict__ dy, int N, int H, int W, int C,
-    int P, int Q, int rows_per_block, int log2C8) {
-  // same traversal as the reduce: a run of input rows per block, channel chunk
-  // tid % C8 fixed per thread, so the per-channel coefficients are computed once
+    int P, int Q, int log2C8) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char stem_lds[];
   const int C8 = C >> 3;
   const int tid = threadIdx.x;
   const int cc = tid & (C8 - 1);
   const int c0 = cc * 8;
+  const int n = blockIdx.x / P, p = blockIdx.x - n * P;
+  bf16_t* dl = reinterpret_cast<bf16_t*>(stem_lds);
+  uint8_t* al = stem_lds + (size_t)2 * Q * C * 2;
+  stem_stage_pooled(dout, arg, dl, al, n, p, P, Q, C8);
   float sc[8], sh[8], ca[8], cb[8], ccf[8];
   ld8(params + 2 * C + c0, sc);
   ld8(params + 3 * C + c0, sh);
@@ -207,20 +234,21 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_elemt_kernel(
       ccf[k] = a * (mean[k] * inv[k] * mdyx - mdy);
     }
   }
-  const int r0 = blockIdx.x * rows_per_block;
-  const int r1 = min(r0 + rows_per_block, N * H);
-  for (int row = r0; row < r1; ++row) {
-    const int n = row / H, h = row - (row / H) * H;
-    for (int j = tid; j < W * C8; j += 256) {
-      const int w = j >> log2C8;
-      const size_t i = (size_t)row * W * C8 + j;
-      float v[8], dz[8], o[8];
-      unpack8(reinterpret_cast<const uint4*>(y)[i], v);
-      stem_dz(dout, arg, n, h, w, cc, C8, P, Q, v, sc, sh, dz);
+  __syncthreads();
+  const StemBwdTile t{dl, al, p, P, Q, C8};
+  const int per_row = W * C8;
+  const int h0 = 2 * p, nrow = min(2, H - h0);
+  for (int j = tid; j < nrow * per_row; j += 256) {
+    const int r = j >= per_row ? 1 : 0;
+    const int jj = j - r * per_row;
+    const int h = h0 + r, w = jj >> log2C8;
+    const size_t i = ((size_t)n * H + h) * per_row + jj;
+    float v[8], d[8], o[8];
+    unpack8(reinterpret_cast<const uint4*>(y)[i], v);
+    t.dz(h, w, cc, v, sc, sh, d);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] = EVAL ? ca[k] * dz[k] : ca[k] * dz[k] + cb[k] * v[k] + ccf[k];
-      reinterpret_cast<uint4*>(dy)[i] = pack8(o);
-    }
+    for (int k = 0; k < 8; ++k) o[k] = EVAL ? ca[k] * d[k] : ca[k] * d[k] + cb[k] * v[k] + ccf[k];
+    reinterpret_cast<uint4*>(dy)[i] = pack8(o);
   }
 }
 
@@ -239,20 +267,23 @@ int stem_pool_fwd_launch(const bf16_t* y, const float* params, bf16_t* out, uint
   return 0;
 }
 
+// dynamic LDS of the backward kernels: two staged pooled rows (gradient + taps),
+// reused for the 256x17 fp32 partials of the reduce
+static size_t stem_bwd_lds(int Q, int C) {
+  const size_t staged = (size_t)2 * Q * C * 3;
+  const size_t part = (size_t)256 * 17 * 4;
+  return staged > part ? staged : part;
+}
+
 int stem_pool_bwd_reduce_launch(const bf16_t* dout, const uint8_t* arg, const bf16_t* y,
                                 const float* params, float* red, int N, int H, int W, int C, int P, int Q,
                                 hipStream_t st) {
   const int l = l2e(C / 8);
-  if (C % 8 || l < 0 || (C / 8) > 256) return 1;
-  // ~4 input rows per block: thousands of blocks keep many rows' gathers in
-  // flight (the per-block atomics stay far below the streaming cost)
-#ifndef PMD_STEM_RPB
-#define PMD_STEM_RPB 4
-#endif
-  const int rpb = PMD_STEM_RPB;
-  const int blocks = (N * H + rpb - 1) / rpb;
-  hipLaunchKernelGGL(stem_pool_bwd_reduce_kernel, dim3(blocks), dim3(256), 0, st, dout, arg, y, params, red,
-                     N, H, W, C, P, Q, rpb, l);
+  if (C % 8 || l < 0 || (C / 8) > 256 || 2 * P < H || 2 * Q < W) return 1;
+  const size_t lds = stem_bwd_lds(Q, C);
+  if (lds > 64 * 1024) return 2;
+  hipLaunchKernelGGL(stem_pool_bwd_reduce_kernel, dim3(N * P), dim3(256), lds, st, dout, arg, y, params, red,
+                     N, H, W, C, P, Q, l);
   return 0;
 }
 
@@ -261,18 +292,15 @@ int stem_pool_bwd_elemt_launch(const bf16_t* dout, const uint8_t* arg, const bf1
                                bf16_t* dy, int N, int H, int W, int C, int P, int Q, bool eval_mode,
                                hipStream_t st) {
   const int l = l2e(C / 8);
-  if (C % 8 || l < 0 || (C / 8) > 256) return 1;
-#ifndef PMD_STEM_RPB
-#define PMD_STEM_RPB 4
-#endif
-  const int rpb = PMD_STEM_RPB;
-  const dim3 grid((N * H + rpb - 1) / rpb);
+  if (C % 8 || l < 0 || (C / 8) > 256 || 2 * P < H || 2 * Q < W) return 1;
+  const size_t lds = stem_bwd_lds(Q, C);
+  if (lds > 64 * 1024) return 2;
   if (eval_mode)
-    hipLaunchKernelGGL(stem_pool_bwd_elemt_kernel<true>, grid, dim3(256), 0, st, dout, arg, y, params, gamma,
-                       red, count, count_h, dy, N, H, W, C, P, Q, rpb, l);
+    hipLaunchKernelGGL(stem_pool_bwd_elemt_kernel<true>, dim3(N * P), dim3(256), lds, st, dout, arg, y, params,
+                       gamma, red, count, count_h, dy, N, H, W, C, P, Q, l);
   else
-    hipLaunchKernelGGL(stem_pool_bwd_elemt_kernel<false>, grid, dim3(256), 0, st, dout, arg, y, params,
-                       gamma, red, count, count_h, dy, N, H, W, C, P, Q, rpb, l);
+    hipLaunchKernelGGL(stem_pool_bwd_elemt_kernel<false>, dim3(N * P), dim3(256), lds, st, dout, arg, y,
+                       params, gamma, red, count, count_h, dy, N, H, W, C, P, Q, l);
   return 0;
 }
 

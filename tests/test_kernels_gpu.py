@@ -174,12 +174,13 @@ def test_conv_big_tiles(shape, tile, pipe):
 
 
 @pytest.mark.parametrize("train", [True, False])
-def test_fused_stem_pool_matches_composite(train):
+@pytest.mark.parametrize("N,H,C", [(4, 112, 64), (2, 15, 64), (2, 20, 128)])
+def test_fused_stem_pool_matches_composite(train, N, H, C):
     """BN+ReLU+maxpool (one kernel) and its two-pass backward == bn_apply ->
-    maxpool_fwd and maxpool_bwd -> bn_bwd_reduce -> bn_bwd_elemt on the same data."""
+    maxpool_fwd and maxpool_bwd -> bn_bwd_reduce -> bn_bwd_elemt on the same data
+    (odd sizes: a last block with one input row and no second pooled row)."""
     HP = _hp()
     torch.manual_seed(6)
-    N, H, C = 4, 112, 64
     y = torch.randn(N, H, H, C, device=DEV).to(torch.bfloat16)
     p = torch.stack([torch.randn(C, device=DEV) * 0.1, torch.rand(C, device=DEV) + 0.5,
                      torch.randn(C, device=DEV), torch.randn(C, device=DEV) * 0.5]).contiguous()
