@@ -117,7 +117,7 @@ def bench_rank(rank, world, a):
         out = model(x)
         loss = OF.cross_entropy(out, y)
         opt.zero_grad()
-        loss.backward()
+        loss.backward(OF.loss_seed(loss))
         opt.step()
         return loss
 
@@ -129,7 +129,7 @@ def bench_rank(rank, world, a):
             out = model(sx)
             loss = OF.cross_entropy(out, sy)
             opt.zero_grad()
-            loss.backward()
+            loss.backward(OF.loss_seed(loss))
             opt.step()
             return loss
 

@@ -86,7 +86,7 @@ def train_epoch(loader, model, optimizer, epoch, logger, args, rank, dev, comm=N
             loss = OF.cross_entropy(output, target)
         optimizer.zero_grad()
         with region("bwd"):
-            loss.backward()
+            loss.backward(OF.loss_seed(loss))
         with region("opt"):
             optimizer.step()
         if comm is not None:

@@ -539,10 +539,13 @@ class _ConvFn(torch.autograd.Function):
         if stats is None:
             stats = _empty(x.device)
         ctx.mark_non_differentiable(stats)
+        ctx.set_materialize_grads(False)   # no zeros_like(stats) fill for the unused grad
         return y, stats
 
     @staticmethod
     def backward(ctx, dy, _dstats):
+        if dy is None:
+            return None, None, None, None, None
         x, *wpack = ctx.saved_tensors
         stride, pad, w = ctx.conf
         P = prims_for(x)
@@ -576,6 +579,7 @@ class _StemS2DConvFn(torch.autograd.Function):
         ctx.save_for_backward(xs)
         ctx.w = w
         ctx.mark_non_differentiable(stats)
+        ctx.set_materialize_grads(False)   # no zeros_like(stats) fill for the unused grad
         return y, stats
 
     @staticmethod
@@ -583,7 +587,7 @@ class _StemS2DConvFn(torch.autograd.Function):
         from .native import C
         (xs,) = ctx.saved_tensors
         w = ctx.w
-        if not ctx.needs_input_grad[1] or not w.requires_grad:
+        if dy is None or not ctx.needs_input_grad[1] or not w.requires_grad:
             return None, None, None
         dws = C.conv_wgrad(dy.contiguous(), xs, 4, 4, 1, 2, None)   # fp32 [K, 4, 4, 16]
         tgt = _grad_target(w)
@@ -1050,6 +1054,20 @@ class _XentFn(torch.autograd.Function):
 def cross_entropy(logits, target):
     """Mean softmax cross-entropy (== nn.CrossEntropyLoss(), reference main.py:48)."""
     return _XentFn.apply(logits, target)
+
+
+_SEEDS: dict = {}
+
+
+def loss_seed(loss):
+    """d(loss)/d(loss) = 1 as a cached device scalar: ``loss.backward(loss_seed(loss))``
+    is ``loss.backward()`` without the ATen fill autograd launches for its
+    implicit ones_like seed every step (read-only: the loss backward only reads it)."""
+    key = (loss.device, loss.dtype)
+    t = _SEEDS.get(key)
+    if t is None:
+        t = _SEEDS[key] = torch.ones((), dtype=loss.dtype, device=loss.device)
+    return t
 
 
 def correct_count(logits, target):

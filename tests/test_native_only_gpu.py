@@ -1,0 +1,51 @@
+"""Every GPU kernel of a steady-state training step is one of the framework's
+own gfx950 kernels (namespace ``pmd::``): no hipBLASLt / MIOpen / ATen
+elementwise, fill or reduce kernels left on the step.
+
+One ResNet-50 (ImageNet stem) step through DataParallel + FusedSGD at a small
+batch, after two warm-up steps (autotuning, pool growth), profiled with
+torch.profiler; the kernel list must contain only ``pmd::`` names."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_step_runs_only_framework_kernels():
+    from torch.profiler import ProfilerActivity, profile
+
+    from pytorch_multiprocessing_distributed_amd.data.loader import SyntheticImageNet
+    from pytorch_multiprocessing_distributed_amd.engine.optim import FusedSGD
+    from pytorch_multiprocessing_distributed_amd.models import build_model
+    from pytorch_multiprocessing_distributed_amd.ops import functional as OF
+    from pytorch_multiprocessing_distributed_amd.parallel.dp import DataParallel
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = DataParallel(build_model("resnet50", num_classes=1000, stem="imagenet").to(dev), None)
+    opt = FusedSGD(model, lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    data = SyntheticImageNet(16, 112, 1000, steps=4, device=dev, dtype=torch.bfloat16, cpad=8, seed=0)
+    model.train()
+
+    def step(i):
+        x, y = data.batch_at(i)
+        loss = OF.cross_entropy(model(x), y)
+        opt.zero_grad()
+        loss.backward(OF.loss_seed(loss))
+        opt.step()
+
+    for i in range(2):
+        step(i)
+    torch.cuda.synchronize()
+    try:
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            step(2)
+            torch.cuda.synchronize()
+    except Exception as e:  # noqa: BLE001 -- no GPU tracer in this build
+        pytest.skip(f"torch.profiler CUDA activity unavailable: {e}")
+    names = {e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA}
+    kernels = {n for n in names if not n.lower().startswith(("memcpy", "memset", "__amd_rocclr"))}
+    if not kernels:
+        pytest.skip("profiler recorded no device kernels")
+    foreign = sorted(n for n in kernels if "pmd::" not in n)
+    assert not foreign, f"non-framework kernels on the step: {foreign[:10]}"
