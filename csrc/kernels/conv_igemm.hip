@@ -86,6 +86,9 @@ __device__ __forceinline__ void wait_vmcnt() {
 #ifndef PMD_CONV_SWZ
 #define PMD_CONV_SWZ 0
 #endif
+#ifndef PMD_CONV_SWAPC
+#define PMD_CONV_SWAPC 1
+#endif
 template <int BK>
 __device__ __forceinline__ int swz(int row) {
   if constexpr (PMD_CONV_SWZ) {
@@ -121,6 +124,12 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
   static_assert(DMA || (BK == 64 && NST == 2 && NW == 4), "register staging: BK=64, 2 stages, 4 waves");
   static_assert(!MF32 || (DMA && BK == 64), "32x32 MFMA path: LDS-DMA, BK=64");
   static_assert(!P8 || (DMA && BK == 64 && NST == 2 && !MF32), "P8: LDS-DMA, BK=64, 2 buffers, 16x16 MFMA");
+  // SWAPC: without the BN-statistics epilogue the 16x16 MFMAs compute C^T (weights as
+  // the first operand): a lane then holds 4 consecutive output CHANNELS of one pixel,
+  // so the C tile is staged with one ds_write_b64 per accumulator instead of four
+  // ds_write_b16 (the statistics epilogue keeps the channel-per-lane layout, whose
+  // per-channel sums need 4x fewer cross-lane steps)
+  constexpr bool SWAPC = PMD_CONV_SWAPC && !STATS && !MF32;
   constexpr int CH = BK / 8;                      // 16-B chunks per LDS row
   constexpr int RPI = DMA ? 64 / CH : 32;         // rows per load instruction (wave / block)
   constexpr int PA = DMA ? BM / (NW * RPI) : BM / 32;  // A load instructions per thread per tile
@@ -440,7 +449,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = SWAPC ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0)
+                            : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
     }
   };
 
@@ -493,7 +503,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
           for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
             for (int j = 0; j < NI; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kh], fb[j][kh], acc[i][j], 0, 0, 0);
+              acc[i][j] = SWAPC ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][kh], fa[i][kh], acc[i][j], 0, 0, 0)
+                                : __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kh], fb[j][kh], acc[i][j], 0, 0, 0);
         };
         // prologue: tiles 0 and 1 in flight, tile 0's fragments in registers
         load_tile_uni(0, 0);
@@ -591,6 +602,19 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
             csq[j] += v * v;
           }
         }
+  } else if constexpr (SWAPC) {
+    // C^T layout: pixel = lane & 15, channels (lane >> 4) * 4 + 0..3 (8-B aligned:
+    // LDC * 2 = 2 BN + 16 bytes per row)
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int row = wm * (BM / WM) + i * 16 + (lane & 15);
+        const int col = wn * (BN / WN) + j * 16 + (lane >> 4) * 4;
+        const uint32_t lo = (uint32_t)f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16);
+        const uint32_t hi = (uint32_t)f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16);
+        *reinterpret_cast<uint2*>(Cs + row * LDC + col) = make_uint2(lo, hi);
+      }
   } else {
 #pragma unroll
     for (int i = 0; i < MI; ++i)
