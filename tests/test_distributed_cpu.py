@@ -110,6 +110,26 @@ def test_two_rank_step_equals_single_process(tmp_path, reducer):
 
 
 @pytest.mark.slow
+def test_four_rank_step_equals_single_process(tmp_path):
+    """W=4 (2 samples per rank): the native reducer + SyncBN over gloo still give
+    the exact global-batch step (bucket launch order, rebuild and SyncBN
+    statistics with more than two peers)."""
+    from pytorch_multiprocessing_distributed_amd.models import build_model
+    out = str(tmp_path / "r0.pt")
+    mp.spawn(_worker, args=(4, _free_port(), out, "native"), nprocs=4, join=True)
+    got = torch.load(out, weights_only=True)
+    torch.manual_seed(0)
+    ref_model = build_model("res").double()
+    x, y = _data()
+    dp, losses = _run_steps(ref_model, x, y, 2, None)
+    for k, v in dp.module.state_dict().items():
+        torch.testing.assert_close(got["state"][k], v, rtol=1e-7, atol=1e-9, msg=k)
+    torch.testing.assert_close(got["loss"], torch.stack(losses), rtol=1e-9, atol=1e-9)
+    for n, g in _grads(dp).items():
+        torch.testing.assert_close(got["grad"][n], g, rtol=1e-6, atol=1e-9, msg=n)
+
+
+@pytest.mark.slow
 def test_two_rank_bf16_wire_compression(tmp_path):
     """compress="bf16": buckets travel in bf16, the fp32/fp64 arena receives
     the average -- equal to the exact step up to bf16 rounding."""
