@@ -89,6 +89,9 @@ __device__ __forceinline__ void wait_vmcnt() {
 #ifndef PMD_CONV_SWAPC
 #define PMD_CONV_SWAPC 1
 #endif
+#ifndef PMD_CONV_MINB4
+#define PMD_CONV_MINB4 2  // __launch_bounds__ min blocks per CU of the 4-wave tiles (VGPR cap A/B knob)
+#endif
 template <int BK>
 __device__ __forceinline__ int swz(int row) {
   if constexpr (PMD_CONV_SWZ) {
@@ -119,7 +122,7 @@ __device__ __forceinline__ int swz(int row) {
 // (cdna_hip_programming.md §5 "Pipelining across barriers", T3/T4, T5).
 template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA, bool MF32 = false,
           int WM = 2, int WN = 2, bool P8 = false>
-__global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a) {
+__global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) void conv_igemm_kernel(ConvArgs a) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   static_assert(DMA || (BK == 64 && NST == 2 && NW == 4), "register staging: BK=64, 2 stages, 4 waves");
   static_assert(!MF32 || (DMA && BK == 64), "32x32 MFMA path: LDS-DMA, BK=64");
@@ -146,7 +149,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
   constexpr int LDC = BN + 8;
   constexpr int SMEM_MAIN = NST * STAGE * 2;
   constexpr int SMEM_EPI = BM * LDC * 2;
-  constexpr int SMEM_PART = DGRAD ? NT * 33 * 4 : 0;  // fused BN-reduce partials [NT][33]
+  constexpr int PSTR = 17;                          // fused BN-reduce partials [NT][17] (odd stride)
+  constexpr int SMEM_PART = DGRAD ? NT * PSTR * 4 : 0;
   constexpr int SMEM0 = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
   constexpr int SMEM = SMEM0 > SMEM_PART ? SMEM0 : SMEM_PART;
   static_assert(SMEM + (STATS ? WM * 2 * BN * 4 : 0) <= 160 * 1024, "exceeds the 160 KiB LDS of a CU");
@@ -677,7 +681,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
   // fused BN-backward reduce: each thread owns one 8-channel chunk column (NT % CPR == 0)
   static_assert(NT % CPR == 0, "chunk column per thread");
   const int nbn = (DGRAD && a.bn_red[0]) ? (a.bn_red[1] ? 2 : 1) : 0;
-  float bsum[2][8], bdot[2][8], bmean[2][8], binv[2][8];
+  // (invstd is applied once after the loop, loaded there: 16 fewer live VGPRs in
+  // the streaming loop, which sets the kernel's occupancy)
+  float bsum[2][8], bdot[2][8], bmean[2][8];
   {
     const int n = n0 + (tid % CPR) * 8;
 #pragma unroll
@@ -685,17 +691,14 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         bsum[t][e] = bdot[t][e] = 0.f;
-        bmean[t][e] = binv[t][e] = 0.f;
+        bmean[t][e] = 0.f;
       }
     if (nbn && n < a.Nout) {
 #pragma unroll
       for (int t = 0; t < 2; ++t)
         if (t < nbn)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            bmean[t][e] = a.bn_p[t][n + e];
-            binv[t][e] = a.bn_p[t][a.Nout + n + e];
-          }
+          for (int e = 0; e < 8; ++e) bmean[t][e] = a.bn_p[t][n + e];
     }
   }
   // Output rows in groups of G per thread: every global load of a group (addend,
@@ -791,26 +794,29 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvArgs a)
       }
     }
   }
+  if (nbn && n_ok) {
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < 2; ++t)
+      if (t < nbn)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) bdot[t][e] *= binv[t][e];
+        for (int e = 0; e < 8; ++e) bdot[t][e] *= a.bn_p[t][a.Nout + n + e];
+  }
   if (nbn) {
     // block-level combine of the 256/CPR threads sharing a chunk column, then one
     // fp32 atomic per channel per block into a kStatSlots slot (like conv_fwd stats)
     __syncthreads();  // everyone is done reading Cs
-    float* part = reinterpret_cast<float*>(smem);  // [NT][33]
+    float* part = reinterpret_cast<float*>(smem);  // [NT][PSTR]
     for (int t = 0; t < nbn; ++t) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        part[tid * 33 + e] = bsum[t][e];
-        part[tid * 33 + 8 + e] = bdot[t][e];
+        part[tid * PSTR + e] = bsum[t][e];
+        part[tid * PSTR + 8 + e] = bdot[t][e];
       }
       __syncthreads();
       for (int q = tid; q < CPR * 16; q += NT) {
         const int col = q >> 4, k = q & 15;
         float acc2 = 0.f;
-        for (int r = col; r < NT; r += CPR) acc2 += part[r * 33 + k];
+        for (int r = col; r < NT; r += CPR) acc2 += part[r * PSTR + k];
         const int n = n0 + col * 8 + (k & 7);
         if (n < a.Nout)
           atomicAdd(a.bn_red[t] + ((size_t)((m0 / BM) % kStatSlots) * 2 + (k >> 3)) * a.Nout + n, acc2);
@@ -1024,9 +1030,14 @@ static bool p8_ok(int shape, const ConvArgs& a) {
   if (shape == 1) return a.Nout >= 128;
   return a.Nout > 64;
 }
+//   10 64x128 tile, LDS-DMA BK=32 x2 stages (Nout > 64): half the rows per block, so
+//      an epilogue-bound short-reduction dgrad gets twice the blocks (and half the
+//      serial epilogue rows per thread) in flight
 template <bool DGRAD, bool STATS>
 static void launch_choice(int c, const ConvArgs& a, hipStream_t st) {
-  if (c >= 6 && c <= 9 && p8_ok(c - 6, a)) {
+  if (c == 10 && a.Nout > 64) {
+    launch_k<64, 128, 32, 2, DGRAD, STATS, true>(a, st);
+  } else if (c >= 6 && c <= 9 && p8_ok(c - 6, a)) {
     launch_p8<DGRAD, STATS>(a, st, c - 6);
   } else if (c == 5 && a.Cs >= 64) {
     launch_w8<DGRAD, STATS>(a, st, 0);
@@ -1139,10 +1150,11 @@ static int tune(const ConvArgs& a0, hipStream_t st) {
   float best_ms = 1e30f;
   // the P8 shapes (6..9) measured equal or slower than 0..5 on every R50 layer
   // (profiles/conv_p8_r02.txt): forced-policy only, not timed by the tuner
-  const int ncand = 6;
-  for (int c = 0; c < ncand; ++c) {
+  // (10, the 64x128 tile, measured slower than 0..5 on every short-K dgrad --
+  // profiles/dgrad_epi_r02_tile10.txt -- so it is a forced policy only)
+  for (int c : {0, 1, 2, 3, 4, 5}) {
     if ((c == 2 && !(big_ok(a) && a.Nout >= 256)) || (c == 3 && !big_ok(a)) || (c == 4 && a.Nout <= 64) ||
-        (c == 5 && (DGRAD || a.Cs < 64)) || (c >= 6 && !p8_ok(c - 6, a)))
+        (c == 5 && (DGRAD || a.Cs < 64)) || (c == 10 && a.Nout <= 64))
       continue;
     launch_choice<DGRAD, STATS>(c, a, st);  // warm (code object load, caches)
     float t = 1e30f;
@@ -1196,7 +1208,9 @@ static void launch_sel(const ConvArgs& a, hipStream_t st) {
     }
   }
   const int t = conv_tile();
-  if (t >= 6 && p8_ok(t - 6, a)) {
+  if (t == 10 && a.Nout > 64) {
+    launch_choice<DGRAD, STATS>(10, a, st);
+  } else if (t >= 6 && t <= 9 && p8_ok(t - 6, a)) {
     launch_p8<DGRAD, STATS>(a, st, t - 6);
   } else if ((t == 4 || t == 5) && a.Cs >= 64) {
     launch_w8<DGRAD, STATS>(a, st, t - 4);
