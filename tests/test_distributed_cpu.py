@@ -110,13 +110,15 @@ def test_two_rank_step_equals_single_process(tmp_path, reducer):
 
 
 @pytest.mark.slow
-def test_four_rank_step_equals_single_process(tmp_path):
-    """W=4 (2 samples per rank): the native reducer + SyncBN over gloo still give
-    the exact global-batch step (bucket launch order, rebuild and SyncBN
-    statistics with more than two peers)."""
+@pytest.mark.parametrize("world", [4, 8])
+def test_multi_rank_step_equals_single_process(tmp_path, world):
+    """W=4 and W=8 (2 / 1 samples per rank, the dp8 rank count of the scaling
+    bench): the native reducer + SyncBN over gloo still give the exact
+    global-batch step (bucket launch order, rebuild and SyncBN statistics with
+    more than two peers)."""
     from pytorch_multiprocessing_distributed_amd.models import build_model
     out = str(tmp_path / "r0.pt")
-    mp.spawn(_worker, args=(4, _free_port(), out, "native"), nprocs=4, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out, "native"), nprocs=world, join=True)
     got = torch.load(out, weights_only=True)
     torch.manual_seed(0)
     ref_model = build_model("res").double()
