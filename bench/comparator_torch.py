@@ -51,9 +51,14 @@ def measure_stock(model_name="resnet50", batch=256, image=224, steps=20, warmup=
         opt.step()
         return loss
 
-    for _ in range(warmup):
+    import sys
+    tw = time.perf_counter()
+    for i in range(warmup):
         step()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        # progress (the first steps run MIOpen's find for every conv shape: minutes)
+        print(f"[stock] warmup step {i + 1}/{warmup} done at {time.perf_counter() - tw:.0f} s",
+              file=sys.stderr, flush=True)
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
