@@ -52,13 +52,21 @@ def measure_stock(model_name="resnet50", batch=256, image=224, steps=20, warmup=
         return loss
 
     import sys
+    import threading
     tw = time.perf_counter()
+    done = threading.Event()
+
+    def heartbeat():                      # MIOpen's find prints nothing for minutes
+        while not done.wait(30.0):
+            print(f"[stock] ... {time.perf_counter() - tw:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=heartbeat, daemon=True).start()
     for i in range(warmup):
         step()
         torch.cuda.synchronize()
         # progress (the first steps run MIOpen's find for every conv shape: minutes)
         print(f"[stock] warmup step {i + 1}/{warmup} done at {time.perf_counter() - tw:.0f} s",
               file=sys.stderr, flush=True)
+    done.set()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
