@@ -11,17 +11,20 @@
 // chunk of an A row is one contiguous load for any C % 8 == 0 -- no im2col
 // buffer, and the 3-channel stem only needs zero-padding to C = 8.
 //
-// Tile: BM x BN x 64, 256 threads = 4 waves in a 2x2 grid, each wave owns a
-// (BM/2)x(BN/2) sub-tile of 16x16 MFMA accumulators.  Operands are register-
-// staged global->VGPR->LDS (double-buffered LDS, one barrier per K-tile; the
-// next tile's global loads are in flight while the current tile's MFMAs run).
-// LDS rows are padded to 144 B so the 16 rows read by one ds_read_b128 lane
-// group hit 16 distinct 16-B bank slots.
+// Tile: BM x BN x BK (128x128, 128x64, 256x256, 256x128; 4 or 8 waves, each wave
+// owning a sub-tile of 16x16x32 (or 32x32x16) MFMA accumulators).  Operands are
+// copied global->LDS by LDS-DMA into an NST-stage ring (XOR-swizzled rows, one
+// barrier per K-tile, counted vmcnt so later tiles stay in flight); a register-
+// staged variant and the P8 register-resident-fragment pipeline are kept for
+// A/B.  A per-shape autotuner picks the variant (the framework's
+// cudnn.benchmark), persisted / broadcast as a tuning table (ops/tuning.py).
 //
-// Epilogue (fwd): optional per-output-channel (sum, sum^2) of the bf16-rounded
-// outputs for BatchNorm (combined across the block's waves in LDS, one fp32
-// atomic per channel per block), then the tile is staged through LDS and
-// written with coalesced 16-byte row stores.
+// Epilogue: fwd -- optional per-output-channel (sum, sum^2) of the bf16-rounded
+// outputs about the BN shift K (combined across the block's waves in LDS, one
+// fp32 atomic per channel per block into 64 slot copies); dgrad -- optional
+// addend (+ReLU-mask gate) and the fused BN-backward reduce over 1-2 BN inputs.
+// The tile is staged through LDS (C^T layout with 8-byte writes when no
+// statistics are taken) and written with coalesced 16-byte row stores.
 #include "common.h"
 #include <stdio.h>
 #include <stdlib.h>
