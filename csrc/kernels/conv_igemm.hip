@@ -123,13 +123,22 @@ __device__ __forceinline__ int swz(int row) {
 // the next tile's loads in flight across both barriers of a K-tile), and the next
 // tile's fragments are read into each register set as soon as its MFMAs retire
 // (cdna_hip_programming.md §5 "Pipelining across barriers", T3/T4, T5).
+//
+// HALO: 3x3 / stride 1 / pad 1 (fwd, or dgrad with flipped taps), Cs % 64 == 0, 7 <= W <= 56.
+// A tile of BM output pixels of ONE image needs a few input rows: those rows (+1-pixel
+// halo, zero borders) are copied to LDS once per 64-channel block and all 9 taps read
+// their A fragments from that halo image at a wave-uniform pixel offset, instead of
+// gathering every input pixel 9 times from L2 (the 64/128-channel 3x3 layers are
+// bound by that L2->LDS gather traffic); only the weight tiles stream per K-tile.
 template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA, bool MF32 = false,
-          int WM = 2, int WN = 2, bool P8 = false>
+          int WM = 2, int WN = 2, bool P8 = false, bool HALO = false>
 __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) void conv_igemm_kernel(ConvArgs a) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   static_assert(DMA || (BK == 64 && NST == 2 && NW == 4), "register staging: BK=64, 2 stages, 4 waves");
   static_assert(!MF32 || (DMA && BK == 64), "32x32 MFMA path: LDS-DMA, BK=64");
   static_assert(!P8 || (DMA && BK == 64 && NST == 2 && !MF32), "P8: LDS-DMA, BK=64, 2 buffers, 16x16 MFMA");
+  static_assert(!HALO || (DMA && BK == 64 && (NST == 2 || NST == 3) && !MF32 && !P8),
+                "HALO: LDS-DMA, BK=64, 2- or 3-deep weight ring");
   // SWAPC: without the BN-statistics epilogue the 16x16 MFMAs compute C^T (weights as
   // the first operand): a lane then holds 4 consecutive output CHANNELS of one pixel,
   // so the C tile is staged with one ds_write_b64 per accumulator instead of four
@@ -150,7 +159,15 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
   constexpr int B_ELEMS = BN * LDR;
   constexpr int STAGE = A_ELEMS + B_ELEMS;
   constexpr int LDC = BN + 8;
-  constexpr int SMEM_MAIN = NST * STAGE * 2;
+  // HALO image: at most ceil(BM / W) + 3 input rows of W + 2 pixels (a tile spans
+  // ceil(BM / W) + 1 rows, plus the two halo rows), 8 chunks each, rounded up to whole
+  // block-wide DMA rounds (NT chunks).  For BM = 128 and 7 <= W <= 56 (launcher
+  // guard) the maximum is 348 pixels (W = 56): 45 KB, 2 blocks per CU with the B ring.
+  static_assert(!HALO || BM == 128, "HALO sized for 128-pixel tiles");
+  constexpr int HALO_PIX = 348;
+  constexpr int HALO_CHUNKS = ((HALO_PIX * 8 + NT - 1) / NT) * NT;
+  constexpr int HALO_BYTES = HALO ? HALO_CHUNKS * 16 : 0;
+  constexpr int SMEM_MAIN = HALO ? HALO_BYTES + NST * B_ELEMS * 2 : NST * STAGE * 2;
   constexpr int SMEM_EPI = BM * LDC * 2;
   constexpr int PSTR = 17;                          // fused BN-reduce partials [NT][17] (odd stride)
   constexpr int SMEM_PART = DGRAD ? NT * PSTR * 4 : 0;
@@ -186,10 +203,15 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
   }
   const int tilesN = (a.Nout + BN - 1) / BN;
   const int Mgrid = (DGRAD && a.stride == 2) ? a.N * ((a.OH + 1) >> 1) * ((a.OW + 1) >> 1) : a.M;
-  const int tilesM = (Mgrid + BM - 1) / BM;  // grid.x sized for the largest phase
+  const int hw_out = a.OH * a.OW;
+  const int halo_T = HALO ? (hw_out + BM - 1) / BM : 1;  // HALO: M tiles never straddle images
+  const int tilesM = HALO ? a.N * halo_T : (Mgrid + BM - 1) / BM;  // grid.x sized for the largest phase
   const int L = xcd_remap(blockIdx.x, tilesM * tilesN);
-  const int m0 = (L / tilesN) * BM;
+  const int mt = L / tilesN;
+  const int halo_img = HALO ? mt / halo_T : 0, halo_t = HALO ? mt - (mt / halo_T) * halo_T : 0;
+  const int m0 = HALO ? halo_img * hw_out + halo_t * BM : mt * BM;
   const int n0 = (L % tilesN) * BN;
+  if (HALO) Mp = m0 + min(BM, hw_out - halo_t * BM);  // rows of this image only
   if (m0 >= Mp) return;  // uniform per block, before any barrier
 
   // ---- per-thread A-row precompute
@@ -488,7 +510,123 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
       compute(kt % NST);
     }
     };
-    if constexpr (P8) {
+    if constexpr (HALO) {
+      // ---- halo image of this tile (see the HALO note at the kernel template)
+      const int Wd = a.W + 2;
+      const int p0 = halo_t * BM;  // first output pixel of the tile (image-local)
+      const int hf = p0 / a.W;
+      const int hl = (min(p0 + BM, hw_out) - 1) / a.W;
+      const int HP = (hl - hf + 3) * Wd;  // input rows hf-1 .. hl+1, columns -1 .. W
+      bf16_t* halo = lds;                                  // [pixel][8 chunks], chunk ^= pixel & 7
+      bf16_t* Bring = lds + HALO_BYTES / 2;                // NST x [BN][64]
+      const bf16_t* img = a.src + (size_t)halo_img * a.H * a.W * a.Cs;
+      int hbase[MI];  // halo pixel of each of this lane's A-fragment rows at tap (0, 0)
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int p = min(p0 + wm * (BM / WM) + i * 16 + frow, hw_out - 1);  // rows past the image: clamped, masked
+        const int h = p / a.W, w = p - (p / a.W) * a.W;
+        hbase[i] = (h - hf) * Wd + w;
+      }
+      auto load_halo = [&](int cb) {
+#pragma unroll
+        for (int j = 0; j < HALO_CHUNKS / NT; ++j) {
+          const int ci = (j * NW + wid_s) * 64 + lane;  // chunk index: lane-linear within the wave
+          const int hp = ci >> 3, c = ci & 7;
+          const int hr = hp / Wd, hc = hp - hr * Wd;
+          const int ih = hf - 1 + hr, iw = hc - 1;
+          const bool ok = hp < HP && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+          const void* src = ok ? (const void*)(img + ((size_t)(ih * a.W + iw) << a.log2Cs) + cb + ((c ^ (hp & 7)) << 3))
+                               : (const void*)g_zero16;
+          bf16_t* dst = halo + (size_t)(j * NW + wid_s) * 64 * 8;
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                           (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+        }
+      };
+      auto load_b = [&](int kt, int buf) {
+        const int cbi = kt / 9, tap = kt - cbi * 9;
+        const int tapo = (tap << a.log2Cs) + cbi * 64;  // tap == r * 3 + s
+#pragma unroll
+        for (int i = 0; i < PB; ++i) {
+          const void* src = b_ok[i] ? (const void*)(b_row[i] + tapo + bchunk(i) * 8) : (const void*)g_zero16;
+          bf16_t* dst = Bring + buf * B_ELEMS + (wid_s * (BN / NW) + RPI * i) * LDR;
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                           (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+        }
+      };
+      auto compute_halo = [&](int buf, int kt) {
+        const int tap = kt % 9;
+        int r = tap / 3, sx = tap - (tap / 3) * 3;
+        if (DGRAD) {  // dX(h, w) gathers dY(h + 1 - r, w + 1 - s)
+          r = 2 - r;
+          sx = 2 - sx;
+        }
+        const int toff = r * Wd + sx;
+        const bf16_t* Bs = Bring + buf * B_ELEMS;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int q = ks * 4 + (lane >> 4);
+          bf16x8 af[MI], bfg[NI];
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            const int hp = hbase[i] + toff;
+            af[i] = *reinterpret_cast<const bf16x8*>(halo + hp * 64 + ((q ^ (hp & 7)) << 3));
+          }
+#pragma unroll
+          for (int j = 0; j < NI; ++j) bfg[j] = frag(Bs, wn * (BN / WN) + j * 16 + frow, q);
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j)
+              acc[i][j] = SWAPC ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0)
+                                : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+        }
+      };
+      const int nkt = (a.Cs >> 6) * 9;
+      if constexpr (NST == 3) {
+        // 3-deep weight ring: B(kt+1) stays in flight across the barrier (counted vmcnt);
+        // only a channel-block switch (halo refill) drains the queue
+        load_halo(0);
+        load_b(0, 0);
+        if (nkt > 1) load_b(1, 1);
+        bool drain = true;
+        for (int kt = 0; kt < nkt; ++kt) {
+          if (drain || kt + 1 >= nkt) wait_vmcnt<0>();
+          else wait_vmcnt<PB>();
+          // publishes B(kt) (+ the halo) and retires every wave's reads of B(kt-1)
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          drain = false;
+          if (kt + 2 < nkt) load_b(kt + 2, (kt + 2) % 3);
+          compute_halo(kt % 3, kt);
+          if (kt + 1 < nkt && (kt + 1) % 9 == 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            load_halo((kt + 1) / 9 * 64);
+            drain = true;
+          }
+        }
+      } else {
+      load_halo(0);
+      load_b(0, 0);
+      wait_vmcnt<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      for (int kt = 0; kt < nkt; ++kt) {
+        const bool next = kt + 1 < nkt;
+        const bool newcb = next && (kt + 1) % 9 == 0;
+        // B(kt+1) into the buffer B(kt-1) used: its reads were retired by the last barrier
+        if (next && !newcb) load_b(kt + 1, (kt + 1) & 1);
+        compute_halo(kt & 1, kt);
+        if (next) {
+          if (newcb) {
+            // every wave is done with this channel block's halo image: refill it
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            load_halo((kt + 1) / 9 * 64);
+            load_b(kt + 1, (kt + 1) & 1);
+          }
+          wait_vmcnt<0>();
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+      }
+      }
+    } else if constexpr (P8) {
       if (uni) {
         static_assert(MI % 2 == 0, "P8 splits the wave's row tiles in two halves");
         bf16x8 fa[MI][2], fb[NI][2];
@@ -917,14 +1055,31 @@ static int conv_impl() {
 }
 
 template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA, bool MF32 = false,
-          int WM = 2, int WN = 2, bool P8 = false>
+          int WM = 2, int WN = 2, bool P8 = false, bool HALO = false>
 static void launch_k(const ConvArgs& a, hipStream_t st) {
   const bool ph2 = DGRAD && a.stride == 2;
   const int Mgrid = ph2 ? a.N * ((a.OH + 1) >> 1) * ((a.OW + 1) >> 1) : a.M;
-  const int tiles = ((Mgrid + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
+  const int mtiles = HALO ? a.N * ((a.OH * a.OW + BM - 1) / BM) : (Mgrid + BM - 1) / BM;
+  const int tiles = mtiles * ((a.Nout + BN - 1) / BN);
   const int phases = ph2 ? 4 : 1;
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, NST, DGRAD, STATS, DMA, MF32, WM, WN, P8>),
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, NST, DGRAD, STATS, DMA, MF32, WM, WN, P8, HALO>),
                      dim3(tiles, phases), dim3(64 * WM * WN), 0, st, a);
+}
+
+// HALO conv (see the kernel): 3x3, stride 1, pad 1, Cs % 64 == 0, 7 <= W <= 56
+static bool halo_ok(const ConvArgs& a) {
+  return a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.Cs % 64 == 0 && a.W >= 7 && a.W <= 56 &&
+         a.OH == a.H && a.OW == a.W;
+}
+template <bool DGRAD, bool STATS>
+static void launch_halo(const ConvArgs& a, hipStream_t st, int depth) {
+  if (a.Nout <= 64) {
+    if (depth == 3) launch_k<128, 64, 64, 3, DGRAD, STATS, true, false, 2, 2, false, true>(a, st);
+    else launch_k<128, 64, 64, 2, DGRAD, STATS, true, false, 2, 2, false, true>(a, st);
+  } else {
+    if (depth == 3) launch_k<128, 128, 64, 3, DGRAD, STATS, true, false, 2, 2, false, true>(a, st);
+    else launch_k<128, 128, 64, 2, DGRAD, STATS, true, false, 2, 2, false, true>(a, st);
+  }
 }
 
 // P8 register-resident fragment pipeline (see the kernel): 0 = 256x256 (8 waves 2x4),
@@ -1038,7 +1193,9 @@ static bool p8_ok(int shape, const ConvArgs& a) {
 //      serial epilogue rows per thread) in flight
 template <bool DGRAD, bool STATS>
 static void launch_choice(int c, const ConvArgs& a, hipStream_t st) {
-  if (c == 10 && a.Nout > 64) {
+  if ((c == 11 || c == 12) && halo_ok(a)) {
+    launch_halo<DGRAD, STATS>(a, st, c == 12 ? 3 : 2);
+  } else if (c == 10 && a.Nout > 64) {
     launch_k<64, 128, 32, 2, DGRAD, STATS, true>(a, st);
   } else if (c >= 6 && c <= 9 && p8_ok(c - 6, a)) {
     launch_p8<DGRAD, STATS>(a, st, c - 6);
@@ -1211,7 +1368,9 @@ static void launch_sel(const ConvArgs& a, hipStream_t st) {
     }
   }
   const int t = conv_tile();
-  if (t == 10 && a.Nout > 64) {
+  if ((t == 11 || t == 12) && halo_ok(a)) {
+    launch_choice<DGRAD, STATS>(t, a, st);
+  } else if (t == 10 && a.Nout > 64) {
     launch_choice<DGRAD, STATS>(10, a, st);
   } else if (t >= 6 && t <= 9 && p8_ok(t - 6, a)) {
     launch_p8<DGRAD, STATS>(a, st, t - 6);

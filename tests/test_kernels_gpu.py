@@ -138,7 +138,7 @@ def test_conv_pipeline_variants(shape, impl):
 
 
 @pytest.mark.parametrize("tile,pipe", [(2, 0), (2, 1), (2, 2), (2, 3), (3, 0), (3, 2), (3, 3), (4, 0), (5, 0),
-                                       (6, 0), (7, 0), (8, 0), (9, 0), (10, 0)])
+                                       (6, 0), (7, 0), (8, 0), (9, 0), (10, 0), (11, 0), (12, 0)])
 @pytest.mark.parametrize("shape", R50_SHAPES + CIFAR_SHAPES, ids=lambda s: "C%d_H%d_K%d_R%d_s%d" % s)
 def test_conv_big_tiles(shape, tile, pipe):
     """8-wave 256x128 / 256x256 tiles (forced wherever legal: Cs >= 64, Nout >= 128)
@@ -482,7 +482,7 @@ def test_resnet50_trains_on_gpu():
                                    (256, 28, 256, 3, 2), (512, 7, 2048, 1, 1)],
                          ids=lambda s: "C%d_H%d_K%d_R%d_s%d" % s)
 @pytest.mark.parametrize("two", [False, True])
-@pytest.mark.parametrize("tile", [1, 2, 3, 6, 7, 8, 10])
+@pytest.mark.parametrize("tile", [1, 2, 3, 6, 7, 8, 10, 11, 12])
 def test_dgrad_fused_bn_reduce(shape, two, tile):
     """BN-backward reduce fused into the dgrad epilogue (one or two BN sets
     sharing the ReLU mask, with a residual addend) == dgrad then bn_bwd_reduce,
