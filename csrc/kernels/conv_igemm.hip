@@ -131,7 +131,7 @@ __device__ __forceinline__ int swz(int row) {
 // gathering every input pixel 9 times from L2 (the 64/128-channel 3x3 layers are
 // bound by that L2->LDS gather traffic); only the weight tiles stream per K-tile.
 template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA, bool MF32 = false,
-          int WM = 2, int WN = 2, bool P8 = false, bool HALO = false>
+          int WM = 2, int WN = 2, bool P8 = false, bool HALO = false, int NB = 2>
 __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) void conv_igemm_kernel(ConvArgs a) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   static_assert(DMA || (BK == 64 && NST == 2 && NW == 4), "register staging: BK=64, 2 stages, 4 waves");
@@ -821,14 +821,17 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
   constexpr int CPR = BN / 8;  // 16-B chunks per output row
   // fused BN-backward reduce: each thread owns one 8-channel chunk column (NT % CPR == 0)
   static_assert(NT % CPR == 0, "chunk column per thread");
-  const int nbn = (DGRAD && a.bn_red[0]) ? (a.bn_red[1] ? 2 : 1) : 0;
-  // (invstd is applied once after the loop, loaded there: 16 fewer live VGPRs in
-  // the streaming loop, which sets the kernel's occupancy)
-  float bsum[2][8], bdot[2][8], bmean[2][8];
+  // NB = the BN-input sets this instantiation handles (launch_k instantiates 0 / 1 / 2
+  // to the call's count): the per-set reduce state is the epilogue's register peak,
+  // so a one-set dgrad (the common case) carries half of it.  The invstd is applied
+  // once after the loop, loaded there, for the same reason.
+  constexpr int NBA = NB > 0 ? NB : 1;
+  const int nbn = (DGRAD && NB > 0 && a.bn_red[0]) ? (NB > 1 && a.bn_red[1] ? 2 : 1) : 0;
+  float bsum[NBA][8], bdot[NBA][8], bmean[NBA][8];
   {
     const int n = n0 + (tid % CPR) * 8;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < NBA; ++t)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         bsum[t][e] = bdot[t][e] = 0.f;
@@ -836,7 +839,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
       }
     if (nbn && n < a.Nout) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < NBA; ++t)
         if (t < nbn)
 #pragma unroll
           for (int e = 0; e < 8; ++e) bmean[t][e] = a.bn_p[t][n + e];
@@ -873,7 +876,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
   for (int it0 = 0; it0 < ITERS; it0 += G) {
     size_t off[G];
     bool ok[G];
-    uint4 v[G], ad[G], yy[2][G];
+    uint4 v[G], ad[G], yy[NBA][G];
     uint32_t am[G], mb[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -896,7 +899,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
       if (nbn && ok[g]) {
         mb[g] = a.bn_mask ? a.bn_mask[off[g] >> 3] : 0xffu;
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < NBA; ++t)
           if (t < nbn) yy[t][g] = *reinterpret_cast<const uint4*>(a.bn_y[t] + off[g]);
       }
     }
@@ -921,7 +924,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
 #pragma unroll
         for (int e = 0; e < 8; ++e) d[e] = ((mb[g] >> e) & 1u) ? d[e] : 0.f;
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < NBA; ++t) {
           if (t < nbn) {
             float yv[8];
             unpack8(yy[t][g], yv);
@@ -937,7 +940,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
   }
   if (nbn && n_ok) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < NBA; ++t)
       if (t < nbn)
 #pragma unroll
         for (int e = 0; e < 8; ++e) bdot[t][e] *= a.bn_p[t][a.Nout + n + e];
@@ -947,7 +950,9 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
     // fp32 atomic per channel per block into a kStatSlots slot (like conv_fwd stats)
     __syncthreads();  // everyone is done reading Cs
     float* part = reinterpret_cast<float*>(smem);  // [NT][PSTR]
-    for (int t = 0; t < nbn; ++t) {
+#pragma unroll
+    for (int t = 0; t < NBA; ++t) {
+      if (t >= nbn) break;  // uniform
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         part[tid * PSTR + e] = bsum[t][e];
@@ -1062,8 +1067,22 @@ static void launch_k(const ConvArgs& a, hipStream_t st) {
   const int mtiles = HALO ? a.N * ((a.OH * a.OW + BM - 1) / BM) : (Mgrid + BM - 1) / BM;
   const int tiles = mtiles * ((a.Nout + BN - 1) / BN);
   const int phases = ph2 ? 4 : 1;
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, NST, DGRAD, STATS, DMA, MF32, WM, WN, P8, HALO>),
-                     dim3(tiles, phases), dim3(64 * WM * WN), 0, st, a);
+  const dim3 grid(tiles, phases), block(64 * WM * WN);
+  if constexpr (DGRAD) {  // instantiation per count of fused BN-reduce input sets (register peak)
+    const int nb = a.bn_red[0] ? (a.bn_red[1] ? 2 : 1) : 0;
+    if (nb == 2)
+      hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, NST, DGRAD, STATS, DMA, MF32, WM, WN, P8, HALO, 2>), grid,
+                         block, 0, st, a);
+    else if (nb == 1)
+      hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, NST, DGRAD, STATS, DMA, MF32, WM, WN, P8, HALO, 1>), grid,
+                         block, 0, st, a);
+    else
+      hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, NST, DGRAD, STATS, DMA, MF32, WM, WN, P8, HALO, 0>), grid,
+                         block, 0, st, a);
+  } else {
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, NST, DGRAD, STATS, DMA, MF32, WM, WN, P8, HALO, 0>), grid,
+                       block, 0, st, a);
+  }
 }
 
 // HALO conv (see the kernel): 3x3, stride 1, pad 1, Cs % 64 == 0, 7 <= W <= 56
