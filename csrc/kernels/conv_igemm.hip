@@ -159,6 +159,17 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
   constexpr int B_ELEMS = BN * LDR;
   constexpr int STAGE = A_ELEMS + B_ELEMS;
   constexpr int LDC = BN + 8;
+  // epilogue C-staging layout (SWAPC only): EPI_SW = 8-B half swap in rows with bit 3
+  // set (conflict-free ds_write_b64); EPI_RM = row order of the ds_read_b128 row reads
+  // for 16-chunk rows read by 16 thread rows (BN = 128, 4 waves): the two 16-lane
+  // halves of a 32-lane read group take rows 16 apart (64 dwords = the same bank
+  // phase) instead of adjacent rows, whose 4-dword skew overlapped two chunks
+#ifndef PMD_EPI_SW
+#define PMD_EPI_SW 1
+#endif
+  constexpr bool EPI_SW = PMD_EPI_SW && SWAPC;
+  constexpr bool EPI_RM = PMD_EPI_SW && SWAPC && BN == 128 && NT == 256;
+  constexpr bool EPI_RM64 = PMD_EPI_SW >= 2 && SWAPC && BN == 64 && NT == 256;
   // HALO image: at most ceil(BM / W) + 3 input rows of W + 2 pixels (a tile spans
   // ceil(BM / W) + 1 rows, plus the two halo rows), 8 chunks each, rounded up to whole
   // block-wide DMA rounds (NT chunks).  For BM = 128 and 7 <= W <= 56 (launcher
@@ -749,13 +760,16 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
         }
   } else if constexpr (SWAPC) {
     // C^T layout: pixel = lane & 15, channels (lane >> 4) * 4 + 0..3 (8-B aligned:
-    // LDC * 2 = 2 BN + 16 bytes per row)
+    // LDC * 2 = 2 BN + 16 bytes per row).  A ds_write_b64 is served in groups of 16
+    // lanes on 32 banks: the 16 rows of a group, 4 dwords apart, would pair up rows
+    // r and r + 8 on the same two banks, so rows with bit 3 set store their two 8-B
+    // halves of every 16-B chunk swapped (EPI_SW; the row reads swap them back).
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const int row = wm * (BM / WM) + i * 16 + (lane & 15);
-        const int col = wn * (BN / WN) + j * 16 + (lane >> 4) * 4;
+        const int col = (wn * (BN / WN) + j * 16 + (lane >> 4) * 4) ^ (EPI_SW ? ((lane >> 1) & 4) : 0);
         const uint32_t lo = (uint32_t)f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16);
         const uint32_t hi = (uint32_t)f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16);
         *reinterpret_cast<uint2*>(Cs + row * LDC + col) = make_uint2(lo, hi);
@@ -863,13 +877,22 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
   // RSTEP per iteration, so for every layer but the strided dgrads the global
   // element offset is one base plus a uniform stride: no per-row integer
   // division / 64-bit multiply in the loop (they were ~1/3 of its VALU issue).
+  // EPI_RM: thread row group q reads rows (q >> 1) + 16 (q & 1) + 8 (it & 1) + 32 (it >> 1)
   constexpr int RSTEP = NT / CPR;
-  const int cc = tid % CPR, row0 = tid / CPR;
+  static_assert(!EPI_RM || (RSTEP == 16 && ITERS % 2 == 0), "EPI_RM row order: 16 thread rows");
+  auto row_delta = [](int it) { return EPI_RM ? 8 * (it & 1) + 32 * (it >> 1) : it * RSTEP; };
+  // EPI_RM64 (8-chunk rows, 36-dword row skew): the 4 thread rows of a 32-lane read
+  // group take rows {0, 16, 24, 8} + (q >> 2), which puts both 16-lane halves of every
+  // ds_read_b128 group on 4 disjoint 16-dword bank ranges
+  const int qr = tid / CPR;
+  const int row0 = EPI_RM ? (qr >> 1) + 16 * (qr & 1)
+                          : EPI_RM64 ? (qr >> 2) + 8 * ((0x1320 >> (4 * (qr & 3))) & 0xF) : qr;
+  const int cc = tid % CPR;
   const int n = n0 + cc * 8;
   const bool n_ok = n < a.Nout;
   const bool phased = DGRAD && a.stride == 2;
   const size_t off0 = (size_t)(m0 + row0) * a.Nout + (n_ok ? n : 0);
-  const size_t ostep = (size_t)RSTEP * a.Nout;
+  const size_t ostep = (size_t)a.Nout;
   // fully unrolled (A/B: +0.8% step over the rolled loop with per-row index
   // math; an LDS lookup table expanding the ReLU mask bytes measured -2.7%)
 #pragma unroll
@@ -880,10 +903,10 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
     uint32_t am[G], mb[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const int row = row0 + (it0 + g) * RSTEP;
+      const int row = row0 + row_delta(it0 + g);
       const int m = m0 + row;
       ok[g] = m < Mp && n_ok;
-      off[g] = off0 + (size_t)(it0 + g) * ostep;
+      off[g] = off0 + (size_t)row_delta(it0 + g) * ostep;
       if (phased) {
         const int mm = ok[g] ? m : 0;
         const int nb = mm / ohw, rem = mm - nb * ohw;
@@ -892,6 +915,11 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
       }
       if (!ok[g]) off[g] = 0;
       v[g] = *reinterpret_cast<const uint4*>(Cs + row * LDC + cc * 8);
+      if constexpr (EPI_SW) {
+        // rows with bit 3 set hold their 8-B halves swapped (compile-time under EPI_RM)
+        const bool sw = EPI_RM ? ((it0 + g) & 1) != 0 : ((row >> 3) & 1) != 0;
+        if (sw) v[g] = make_uint4(v[g].z, v[g].w, v[g].x, v[g].y);
+      }
       if (has_add && ok[g]) {
         ad[g] = *reinterpret_cast<const uint4*>(a.addend + off[g]);
         am[g] = has_amask ? a.addend_mask[off[g] >> 3] : 0xffu;
