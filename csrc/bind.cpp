@@ -178,7 +178,7 @@ Tensor stem_s2d_wgrad_fold(Tensor dws, int64_t C, c10::optional<Tensor> out) {
 // ------------------------------------------------------------- winograd
 // F(2x2,3x3) for stride-1 pad-1 3x3 convs: U = filter transform of the forward
 // weight image wk [K,3,3,Cp] (flip: the dgrad filter, [16,Cp,K]); the 16 GEMMs
-// between the input and output transforms are torch.bmm (hipBLASLt).
+// between the input and output transforms are winograd_gemm below.
 Tensor winograd_filter(Tensor wk, bool flip) {
   CHECK_DEV(wk); CHECK_BF16(wk); CHECK_CONT(wk);
   TORCH_CHECK(wk.dim() == 4 && wk.size(1) == 3 && wk.size(2) == 3, "wk must be [K,3,3,Cp]");
@@ -198,6 +198,28 @@ Tensor winograd_input(Tensor x) {
   Tensor V = torch::empty({16, T, C}, x.options());
   CHECK_RC(pmd::winograd_input_launch(bfp(x), bfp_mut(V), N, H, W, C, cur_stream()), "winograd_input");
   return V;
+}
+
+// The 16 transformed-domain products M[b] = V[b] . U[b]^T ([T,C] x [K,C] -> [T,K]):
+// each is a 1x1 stride-1 "convolution" of T pixels with C channels by the K x C
+// filter slice U[b], so all 16 run as ONE batched launch (grid.z) of the implicit-GEMM
+// MFMA kernel (LDS-DMA ring, per-shape autotuned tile) -- no library GEMM.
+Tensor winograd_gemm(Tensor V, Tensor U) {
+  CHECK_DEV(V); CHECK_BF16(V); CHECK_CONT(V);
+  CHECK_DEV(U); CHECK_BF16(U); CHECK_CONT(U);
+  TORCH_CHECK(V.dim() == 3 && U.dim() == 3 && V.size(0) == 16 && U.size(0) == 16 && V.size(2) == U.size(2),
+              "winograd_gemm: V [16,T,C], U [16,K,C]");
+  TORCH_CHECK(V.size(1) < (int64_t)1 << 31, "winograd_gemm: too many tiles");
+  const int T = V.size(1), C = V.size(2), K = U.size(1);
+  c10::DeviceGuard g(V.device());
+  Tensor M = torch::empty({16, T, K}, V.options());
+  const pmd::bf16_t* v = bfp(V);
+  const pmd::bf16_t* u = bfp(U);
+  pmd::bf16_t* m = bfp_mut(M);
+  CHECK_RC(pmd::conv_igemm_batched_launch(v, u, m, 16, (long long)T * C, (long long)K * C, (long long)T * K, 1, T, 1,
+                                          C, T, 1, K, 1, 1, 1, 0, cur_stream()),
+           "winograd_gemm");
+  return M;
 }
 
 std::vector<Tensor> winograd_output(Tensor M, int64_t N, int64_t H, int64_t W, bool want_stats,
@@ -841,6 +863,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_s2d_wgrad_fold", &stem_s2d_wgrad_fold);
   m.def("winograd_filter", &winograd_filter);
   m.def("winograd_input", &winograd_input);
+  m.def("winograd_gemm", &winograd_gemm, py::arg("V"), py::arg("U"));
   m.def("winograd_output", &winograd_output, py::arg("M"), py::arg("N"), py::arg("H"), py::arg("W"),
         py::arg("want_stats"), py::arg("stats_buf"), py::arg("shift") = py::none());
   m.def("conv_dgrad", &conv_dgrad);

@@ -56,6 +56,10 @@ struct ConvArgs {
   int OH, OW;
   int Nout, R, S, stride, log2stride, pad;
   int M, Kg;
+  // grid.z batch of independent problems (Winograd's 16 transformed-domain GEMMs):
+  // problem z reads src + z * bs_src, wt + z * bs_wt and writes out + z * bs_out
+  int batch;
+  long long bs_src, bs_wt, bs_out;
 };
 
 constexpr int LDA_REG = 64 + 8;  // padded LDS row of the register-staged path (elements)
@@ -188,6 +192,11 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
   __shared__ __attribute__((aligned(16))) char smem[SMEM + (STATS ? WM * 2 * BN * 4 : 0)];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
 
+  if (blockIdx.z) {  // batched launch (no statistics / addend / fused reduce: launcher contract)
+    a.src += blockIdx.z * a.bs_src;
+    a.wt += blockIdx.z * a.bs_wt;
+    a.out += blockIdx.z * a.bs_out;
+  }
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
@@ -1095,7 +1104,7 @@ static void launch_k(const ConvArgs& a, hipStream_t st) {
   const int mtiles = HALO ? a.N * ((a.OH * a.OW + BM - 1) / BM) : (Mgrid + BM - 1) / BM;
   const int tiles = mtiles * ((a.Nout + BN - 1) / BN);
   const int phases = ph2 ? 4 : 1;
-  const dim3 grid(tiles, phases), block(64 * WM * WN);
+  const dim3 grid(tiles, phases, a.batch), block(64 * WM * WN);
   if constexpr (DGRAD) {  // instantiation per count of fused BN-reduce input sets (register peak)
     const int nb = a.bn_red[0] ? (a.bn_red[1] ? 2 : 1) : 0;
     if (nb == 2)
@@ -1434,15 +1443,20 @@ static void launch_sel(const ConvArgs& a, hipStream_t st) {
   }
 }
 
-// Returns 0 on success, nonzero on unsupported shape.
-int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* stats, int N, int H,
-                      int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
-                      bool dgrad, const bf16_t* addend, const uint8_t* addend_mask,
-                      const BnReduceArgs* bnr, hipStream_t st, const float* shift) {
+static int conv_igemm_launch_b(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* stats, int N, int H,
+                               int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
+                               bool dgrad, const bf16_t* addend, const uint8_t* addend_mask,
+                               const BnReduceArgs* bnr, hipStream_t st, const float* shift, int batch,
+                               long long bs_src, long long bs_wt, long long bs_out) {
   if (Cs % 8 != 0 || (Cs & (Cs - 1)) != 0) return 1;  // power-of-two channels (>= 8)
   if (Nout % 8 != 0) return 2;
   if (stride != 1 && stride != 2) return 3;
+  if (batch < 1 || batch > 65535 || (batch > 1 && (dgrad || stats || addend || bnr))) return 6;
   ConvArgs a;
+  a.batch = batch;
+  a.bs_src = bs_src;
+  a.bs_wt = bs_wt;
+  a.bs_out = bs_out;
   a.src = src;
   a.wt = wt;
   a.out = out;
@@ -1490,6 +1504,24 @@ int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* s
     else launch_sel<false, false>(a, st);
   }
   return 0;
+}
+
+// Returns 0 on success, nonzero on unsupported shape.
+int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* stats, int N, int H,
+                      int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
+                      bool dgrad, const bf16_t* addend, const uint8_t* addend_mask,
+                      const BnReduceArgs* bnr, hipStream_t st, const float* shift) {
+  return conv_igemm_launch_b(src, wt, out, stats, N, H, W, Cs, OH, OW, Nout, R, S, stride, pad, dgrad, addend,
+                             addend_mask, bnr, st, shift, 1, 0, 0, 0);
+}
+
+// `batch` independent forward convolutions of one shape in ONE launch (grid.z), no
+// epilogue fusions: problem z = (src + z bs_src, wt + z bs_wt) -> out + z bs_out.
+int conv_igemm_batched_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, int batch, long long bs_src,
+                              long long bs_wt, long long bs_out, int N, int H, int W, int Cs, int OH, int OW,
+                              int Nout, int R, int S, int stride, int pad, hipStream_t st) {
+  return conv_igemm_launch_b(src, wt, out, nullptr, N, H, W, Cs, OH, OW, Nout, R, S, stride, pad, false, nullptr,
+                             nullptr, nullptr, st, nullptr, batch, bs_src, bs_wt, bs_out);
 }
 
 void conv_weight_prep_launch(const float* w, bf16_t* wk, bf16_t* wkt, int K, int RS, int C, int Cp,

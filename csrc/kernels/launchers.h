@@ -22,7 +22,11 @@ int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* s
                       int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
                       bool dgrad, const bf16_t* addend, const uint8_t* addend_mask,
                       const BnReduceArgs* bnr, hipStream_t st, const float* shift = nullptr);
-// Winograd F(2x2,3x3) transforms (stride-1 pad-1 3x3; the 16 GEMMs run on hipBLASLt)
+// `batch` same-shape forward convolutions in one launch (grid.z), no epilogue fusions
+int conv_igemm_batched_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, int batch, long long bs_src,
+                              long long bs_wt, long long bs_out, int N, int H, int W, int Cs, int OH, int OW,
+                              int Nout, int R, int S, int stride, int pad, hipStream_t st);
+// Winograd F(2x2,3x3) transforms (stride-1 pad-1 3x3; the 16 GEMMs run on conv_igemm as 1x1 convs)
 int winograd_filter_launch(const bf16_t* wk, bf16_t* U, int K, int Cp, bool flip, hipStream_t st);
 int winograd_input_launch(const bf16_t* x, bf16_t* V, int N, int H, int W, int C, hipStream_t st);
 int winograd_output_launch(const bf16_t* M, bf16_t* y, float* stats, int N, int H, int W, int K,

@@ -230,7 +230,7 @@ class ResNet(nn.Module):
                     entries.append((mod, mod.in_channels, True))
             ws = OF.WeightImageSet(entries)
             if f8 is not None:   # config 5: every block conv's e4m3 image in the same per-step refresh
-                ws.fp8 = OF.Fp8WeightSet([(m, cp) for m, cp, _ in entries[1:]], f8)
+                ws.fp8 = OF.Fp8WeightSet([(m, cp) for m, cp, _ in entries[1:] if OF.fp8_eligible(m, cp)], f8)
             self.__dict__["_pmd_wset"] = ws
             self.__dict__["_pmd_wset_key"] = key
         return ws

@@ -155,6 +155,17 @@ def _fp8_for(P):
     return f if (f is not None and getattr(P, "SUPPORTS_FP8", False)) else None
 
 
+# A conv runs its forward in fp8 only when its reduction Kg = R*S*Cin fills at least one
+# 128-deep e4m3 K-tile: the 1x1 convs over 64 channels (layer-1 expand / projection)
+# would multiply half a tile of zero padding and measured slower than bf16, and then
+# the BN-apply feeding them skips its e4m3 copy (PMD_FP8_MIN_KG=0: every block conv).
+FP8_MIN_KG = int(os.environ.get("PMD_FP8_MIN_KG", "128"))
+
+
+def fp8_eligible(conv_m, cin) -> bool:
+    return int(cin) * conv_m.weight.shape[2] * conv_m.weight.shape[3] >= FP8_MIN_KG
+
+
 def _conv_fwd_any(P, f8, h, hq, wp, conv_m, want_stats):
     """bf16 conv, or the fp8 one when ``hq = (e4m3 input, scale)`` is given."""
     if f8 is None or hq is None:
@@ -785,32 +796,38 @@ class _ResidualBlockFn(torch.autograd.Function):
             hq = getattr(x, "_pmd_q8", None)
             if hq is not None:
                 x._pmd_q8 = None                # consumed: do not keep it alive with x
-            else:
+            elif (fp8_eligible(stages[0][0], x.shape[-1])
+                  or (shortcut is not None and fp8_eligible(shortcut[0], x.shape[-1]))):
                 sx, ax = f8.site(("in", id(stages[0][0])))
                 hq = (P.quant_bf16_fp8(x, sx, ax), sx)
         xq = hq
         h = x
         recs = []
-        for conv_m, bn in stages:
+        nxt_convs = [c for c, _ in stages[1:]] + [final[0]]
+        for si, (conv_m, bn) in enumerate(stages):
             wp = _conv_weight(P, conv_m, x.dtype, h.shape[-1], True)
-            y, st = _conv_fwd_any(P, f8, h, hq, wp, conv_m, _stats_req(bn, training))
+            y, st = _conv_fwd_any(P, f8, h, hq if (hq is not None and fp8_eligible(conv_m, h.shape[-1])) else None,
+                                  wp, conv_m, _stats_req(bn, training))
             p, _, count = _bn_forward_params(P, y, st, bn, training, sync)
-            if f8 is not None:
+            if f8 is not None and fp8_eligible(nxt_convs[si], y.shape[-1]):
                 site = f8.site(("a", id(bn)))
                 z, zmask, zq = P.bn_apply(y, p, relu=True, fp8=site)
                 hq = (zq, site[0])
             else:
                 z, zmask = P.bn_apply(y, p, relu=True)
+                hq = None
             recs.append((h, wp, y, p, zmask, count))
             h = z
         fconv, fbn = final
         wpf = _conv_weight(P, fconv, x.dtype, h.shape[-1], True)
-        yf, stf = _conv_fwd_any(P, f8, h, hq, wpf, fconv, _stats_req(fbn, training))
+        yf, stf = _conv_fwd_any(P, f8, h, hq if (hq is not None and fp8_eligible(fconv, h.shape[-1])) else None,
+                                wpf, fconv, _stats_req(fbn, training))
         osite = f8.site(("a", id(fbn))) if f8 is not None else None
         if shortcut is not None:
             sconv, sbn = shortcut
             wps = _conv_weight(P, sconv, x.dtype, x.shape[-1], x.requires_grad)
-            ys, sts = _conv_fwd_any(P, f8, x, xq, wps, sconv, _stats_req(sbn, training))
+            ys, sts = _conv_fwd_any(P, f8, x, xq if (xq is not None and fp8_eligible(sconv, x.shape[-1])) else None,
+                                    wps, sconv, _stats_req(sbn, training))
             pf, ps, countf = _bn_forward_params(P, yf, stf, fbn, training, sync, ys, sts, sbn)
             r = P.bn_apply(yf, pf, None, ys, ps, relu=True, **({"fp8": osite} if osite else {}))
         else:

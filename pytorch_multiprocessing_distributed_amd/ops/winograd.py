@@ -3,12 +3,12 @@
 Bottleneck conv2 at stride 1: model/resnet.py:20-24, 50-51).
 
 GPU path: three gfx950 transform kernels (csrc/kernels/winograd.hip) around the
-16 per-position GEMMs, which are plain batched library GEMMs (torch.bmm ->
-hipBLASLt):
+16 per-position GEMMs, each run as a 1x1 convolution on the framework's
+implicit-GEMM MFMA kernel (``C.winograd_gemm``; no library GEMM):
 
     U  = winograd_filter(wk)            [16, K, C]   (G g G^T)
     V  = winograd_input(x)              [16, T, C]   (B^T d B), T = N ceil(H/2) ceil(W/2)
-    M  = bmm(V, U^T)                    [16, T, K]
+    M  = winograd_gemm(V, U)            [16, T, K]   M[b] = V[b] U[b]^T
     y  = winograd_output(M)             [N, H, W, K] (A^T M A) + fused BN statistics
 
 Dgrad of the same layer is the same pipeline on dY with the flipped,
@@ -91,9 +91,9 @@ def conv_fwd(x, wk, want_stats, stats_buf=None, shift=None):
     C = _c()
     U = C.winograd_filter(wk, False)                 # [16, K, C]
     V = C.winograd_input(x)                          # [16, T, C]
-    M = torch.bmm(V, U.transpose(1, 2))              # [16, T, K]  hipBLASLt
+    M = C.winograd_gemm(V, U)                        # [16, T, K]  MFMA igemm
     N, H, W, _ = x.shape
-    out = C.winograd_output(M.contiguous(), N, H, W, bool(want_stats), stats_buf, shift)
+    out = C.winograd_output(M, N, H, W, bool(want_stats), stats_buf, shift)
     return (out[0], out[1]) if want_stats else (out[0], None)
 
 
@@ -102,6 +102,6 @@ def conv_dgrad(dy, wk, x_shape):
     C = _c()
     U = C.winograd_filter(wk, True)                  # [16, Cp, K]
     V = C.winograd_input(dy)                         # [16, T, K]
-    M = torch.bmm(V, U.transpose(1, 2))              # [16, T, Cp]
+    M = C.winograd_gemm(V, U)                        # [16, T, Cp]
     N, H, W, _ = x_shape
-    return C.winograd_output(M.contiguous(), N, H, W, False, None)[0]
+    return C.winograd_output(M, N, H, W, False, None)[0]

@@ -129,7 +129,9 @@ def test_resnet50_fp8_trains():
         assert all(v == v for v in losses), losses
         assert losses[-1] < 0.1 * losses[0], (mode, losses)
         if f8 is not None:
-            assert len(f8.sites) > 100 and f8.steps == 24     # first update() precedes any site
+            # weight + activation sites of the fp8-eligible convs (Kg >= 128: the layer-1
+            # 1x1 convs over 64 channels stay bf16): 92 for ResNet-50
+            assert len(f8.sites) > 80 and f8.steps == 24     # first update() precedes any site
             n = len(f8.sites)
             assert torch.isfinite(f8.scale[:n]).all() and (f8.scale[:n] > 0).all()
     assert abs(first["fp8"] - first["bf16"]) < 0.05 * first["bf16"], first

@@ -1,4 +1,4 @@
-"""gfx950 Winograd F(2x2,3x3) path (csrc/kernels/winograd.hip + hipBLASLt bmm)
+"""gfx950 Winograd F(2x2,3x3) path (csrc/kernels/winograd.hip + the 16 GEMMs on conv_igemm)
 against the PyTorch fp32 conv of the same bf16 operands: forward with the fused
 BN statistics, dgrad, dispatch through hip_prims, and a ResNet step."""
 import pytest
@@ -14,6 +14,20 @@ DEV = "cuda"
 def _rel(a, b):
     a, b = a.float(), b.float()
     return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+@pytest.mark.parametrize("t,c,k", [(3136, 64, 64), (1000, 128, 256), (96, 512, 512), (17, 64, 32)])
+def test_winograd_gemm_native(t, c, k):
+    """The 16 transformed-domain GEMMs on the implicit-GEMM MFMA kernel vs fp32 bmm of
+    the same bf16 operands (bf16 output: one rounding, rel-L2 < 1e-2)."""
+    from pytorch_multiprocessing_distributed_amd.ops.native import C
+    torch.manual_seed(0)
+    V = torch.randn(16, t, c, device=DEV).to(torch.bfloat16)
+    U = (torch.randn(16, k, c, device=DEV) / c ** 0.5).to(torch.bfloat16)
+    M = C.winograd_gemm(V, U)
+    ref = torch.bmm(V.float(), U.float().transpose(1, 2))
+    assert M.shape == (16, t, k) and M.dtype == torch.bfloat16
+    assert _rel(M, ref) < 1e-2
 
 
 @pytest.mark.parametrize("n,h,c,k", [(4, 56, 64, 64), (4, 28, 128, 128), (8, 14, 256, 256),
