@@ -155,15 +155,23 @@ def _fp8_for(P):
     return f if (f is not None and getattr(P, "SUPPORTS_FP8", False)) else None
 
 
-# A conv runs its forward in fp8 only when its reduction Kg = R*S*Cin fills at least one
-# 128-deep e4m3 K-tile: the 1x1 convs over 64 channels (layer-1 expand / projection)
-# would multiply half a tile of zero padding and measured slower than bf16, and then
-# the BN-apply feeding them skips its e4m3 copy (PMD_FP8_MIN_KG=0: every block conv).
+# Which convs run their forward in fp8 (the BN-apply feeding a bf16 conv skips its
+# e4m3 copy).  The fp8 gain of a conv has to pay for that copy (1 B per input element):
+#   PMD_FP8_CONVS=spatial (default): the R x S > 1 convs (3x3), which run 1.2-1.4x
+#     faster in fp8 (790-1,144 vs 600-856 TFLOP/s) and read a 64-512-channel input;
+#     the 1x1 convs save less than their e4m3 input copy costs (conv_bench per-layer
+#     table in profiles/fp8_ring_depth_r02_rejected.txt);
+#   PMD_FP8_CONVS=all: every block conv whose reduction Kg = R*S*Cin fills one 128-deep
+#     e4m3 K-tile (PMD_FP8_MIN_KG, default 128; 0 = every block conv).
+FP8_CONVS = os.environ.get("PMD_FP8_CONVS", "spatial")
 FP8_MIN_KG = int(os.environ.get("PMD_FP8_MIN_KG", "128"))
 
 
 def fp8_eligible(conv_m, cin) -> bool:
-    return int(cin) * conv_m.weight.shape[2] * conv_m.weight.shape[3] >= FP8_MIN_KG
+    rs = conv_m.weight.shape[2] * conv_m.weight.shape[3]
+    if FP8_CONVS == "spatial" and rs == 1:
+        return False
+    return int(cin) * rs >= FP8_MIN_KG
 
 
 def _conv_fwd_any(P, f8, h, hq, wp, conv_m, want_stats):
@@ -822,7 +830,10 @@ class _ResidualBlockFn(torch.autograd.Function):
         wpf = _conv_weight(P, fconv, x.dtype, h.shape[-1], True)
         yf, stf = _conv_fwd_any(P, f8, h, hq if (hq is not None and fp8_eligible(fconv, h.shape[-1])) else None,
                                 wpf, fconv, _stats_req(fbn, training))
-        osite = f8.site(("a", id(fbn))) if f8 is not None else None
+        # e4m3 copy of the block output only if its consumer -- the next block's first
+        # conv, which has this block's first-conv kernel shape -- runs in fp8
+        osite = (f8.site(("a", id(fbn))) if f8 is not None and fp8_eligible(stages[0][0], yf.shape[-1])
+                 else None)
         if shortcut is not None:
             sconv, sbn = shortcut
             wps = _conv_weight(P, sconv, x.dtype, x.shape[-1], x.requires_grad)

@@ -129,12 +129,21 @@ def test_resnet50_fp8_trains():
         assert all(v == v for v in losses), losses
         assert losses[-1] < 0.1 * losses[0], (mode, losses)
         if f8 is not None:
-            # weight + activation sites of the fp8-eligible convs (Kg >= 128: the layer-1
-            # 1x1 convs over 64 channels stay bf16): 92 for ResNet-50
-            assert len(f8.sites) > 80 and f8.steps == 24     # first update() precedes any site
+            # a weight site per fp8-eligible conv (default policy: the 16 3x3 convs of
+            # ResNet-50) plus the activation sites of their inputs
+            n_elig = sum(1 for mod in m.modules() if getattr(mod, "weight", None) is not None
+                         and mod.weight.dim() == 4 and mod is not m.conv1
+                         and OF.fp8_eligible(mod, mod.weight.shape[1]))
+            assert n_elig >= 16 and len(f8.sites) > n_elig, (n_elig, len(f8.sites))
+            assert f8.steps == 24                              # first update() precedes any site
             n = len(f8.sites)
             assert torch.isfinite(f8.scale[:n]).all() and (f8.scale[:n] > 0).all()
-    assert abs(first["fp8"] - first["bf16"]) < 0.05 * first["bf16"], first
+    # At 64 px / batch 16 the random-init network is numerically chaotic (layer-4 BN
+    # over 64 values per channel): any fp8 quantisation pattern moves the first
+    # logits by rel-L2 ~0.45 vs bf16 and the first loss by a few percent
+    # (bench/fp8_probe.py -> profiles/fp8_probe_r02.txt: 2.4% with every eligible
+    # conv in fp8, 8.0% with the 3x3 convs only, whose logits are the closer ones)
+    assert abs(first["fp8"] - first["bf16"]) < 0.12 * first["bf16"], first
 
 
 def test_grouped_fp8_weight_images_match_per_conv():
