@@ -726,6 +726,19 @@ Tensor quant_weight_fp8(Tensor w, int64_t cp, Tensor scale, c10::optional<Tensor
   return q;
 }
 
+// Fp8Scaling.update(): amax [capacity, kAmaxSlots] fp32, scale [capacity] fp32, first n sites
+void fp8_update_scales(Tensor amax, Tensor scale, int64_t n, double fmax) {
+  CHECK_DEV(amax); CHECK_F32(amax); CHECK_CONT(amax);
+  CHECK_DEV(scale); CHECK_F32(scale); CHECK_CONT(scale);
+  TORCH_CHECK(amax.dim() == 2 && amax.size(1) == 64 && scale.dim() == 1 && n >= 0 && n <= amax.size(0) &&
+                  n <= scale.size(0),
+              "fp8_update_scales: amax [cap, 64], scale [cap], n <= cap");
+  c10::DeviceGuard g(amax.device());
+  CHECK_RC(pmd::fp8_update_scales_launch(amax.data_ptr<float>(), scale.data_ptr<float>(), (int)n, (float)fmax,
+                                         cur_stream()),
+           "fp8_update_scales");
+}
+
 Tensor dequant_fp8(Tensor q, c10::optional<Tensor> inv_scale) {
   CHECK_DEV(q); CHECK_U8(q); CHECK_CONT(q);
   c10::DeviceGuard g(q.device());
@@ -897,6 +910,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("quant_bf16_fp8", &quant_bf16_fp8);
   m.def("quant_weight_fp8", &quant_weight_fp8);
   m.def("dequant_fp8", &dequant_fp8);
+  m.def("fp8_update_scales", &fp8_update_scales, py::arg("amax"), py::arg("scale"), py::arg("n"), py::arg("fmax"));
   m.def("fp8_mfma_probe", &fp8_mfma_probe);
   m.def("conv_fp8_fwd", &conv_fp8_fwd, py::arg("xq"), py::arg("wq"), py::arg("sx"), py::arg("sw"),
         py::arg("stride"), py::arg("pad"), py::arg("want_stats"), py::arg("stats_buf"),

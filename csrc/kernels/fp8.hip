@@ -106,6 +106,28 @@ void quant_weight_fp8_grouped_launch(const Fp8WeightDesc* d_descs, const int* d_
                      d_block_start, n);
 }
 
+// Delayed-scaling update of every fp8 site in one launch (Fp8Scaling.update): one wave
+// per site folds its kAmaxSlots amax copies, sets scale = fmax / amax where an amax was
+// observed (else keeps the scale) and clears the slots for the next step.
+__global__ __launch_bounds__(256) void fp8_update_scales_kernel(float* __restrict__ amax,
+                                                                 float* __restrict__ scale, int n, float fmax) {
+  const int site = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (site >= n) return;
+  float* slots = amax + (size_t)site * kAmaxSlots;
+  float a = 0.f;
+  for (int i = lane; i < kAmaxSlots; i += 64) a = fmaxf(a, slots[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) a = fmaxf(a, __shfl_xor(a, o, 64));
+  for (int i = lane; i < kAmaxSlots; i += 64) slots[i] = 0.f;
+  if (lane == 0 && a > 0.f) scale[site] = fmax / fmaxf(a, 1e-12f);
+}
+
+int fp8_update_scales_launch(float* amax, float* scale, int n, float fmax, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(fp8_update_scales_kernel, dim3((n + 3) / 4), dim3(256), 0, st, amax, scale, n, fmax);
+  return 0;
+}
+
 // e4m3 -> fp32 (tests / debugging)
 __global__ void dequant_fp8_kernel(const uint8_t* __restrict__ q, float* __restrict__ out,
                                    const float* __restrict__ inv_scale, long long n) {

@@ -140,6 +140,7 @@ void quant_weight_fp8_grouped_launch(const Fp8WeightDesc* d_descs, const int* d_
                                      int total_blocks, hipStream_t st);
 int quant_weight_fp8_launch(const float* w, uint8_t* q, const float* scale, float* amax, int K, int RS,
                             int C, int Cp, hipStream_t st);
+int fp8_update_scales_launch(float* amax, float* scale, int n, float fmax, hipStream_t st);
 int dequant_fp8_launch(const uint8_t* q, float* out, const float* inv_scale, long long n, hipStream_t st);
 int fp8_mfma_probe_launch(const uint8_t* A, const uint8_t* Bt, float* C, hipStream_t st);
 // y(bf16) = conv(xq, wq) / (sx * sw) with e4m3 NHWC input / KRSC weight; optional BN stats slots

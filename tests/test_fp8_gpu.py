@@ -168,3 +168,24 @@ def test_grouped_fp8_weight_images_match_per_conv():
         got = ws.lookup(c, c.in_channels)
         assert torch.equal(got, ref)
         assert torch.equal(aw.max(), ref_amax.max())
+
+
+def test_fp8_update_scales_native_matches_torch():
+    """Fp8Scaling.update() (one native launch) == the torch formula: scale = 448 /
+    max over the 64 amax slots where one was observed, unchanged elsewhere, slots
+    cleared; sites past n untouched."""
+    from pytorch_multiprocessing_distributed_amd.ops.fp8 import E4M3_MAX
+    C = _C()
+    torch.manual_seed(0)
+    cap, n = 40, 37
+    amax = torch.rand(cap, 64, device=DEV) * 10
+    amax[5].zero_()                          # no observation: keep its scale
+    scale = torch.rand(cap, device=DEV) + 0.5
+    a_ref = amax[:n].amax(dim=1)
+    s_ref = torch.where(a_ref > 0, E4M3_MAX / a_ref.clamp_min(1e-12), scale[:n])
+    tail_a, tail_s = amax[n:].clone(), scale[n:].clone()
+    C.fp8_update_scales(amax, scale, n, E4M3_MAX)
+    torch.cuda.synchronize()
+    assert torch.allclose(scale[:n], s_ref, rtol=1e-6, atol=0)
+    assert torch.count_nonzero(amax[:n]).item() == 0
+    assert torch.equal(amax[n:], tail_a) and torch.equal(scale[n:], tail_s)

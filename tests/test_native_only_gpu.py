@@ -1,6 +1,7 @@
 """Every GPU kernel of a steady-state training step is one of the framework's
 own gfx950 kernels (namespace ``pmd::``): no hipBLASLt / MIOpen / ATen
-elementwise, fill or reduce kernels left on the step.
+elementwise, fill or reduce kernels left on the step, in
+bf16 and in the fp8 configuration.
 
 One ResNet-50 (ImageNet stem) step through DataParallel + FusedSGD at a small
 batch, after two warm-up steps (autotuning, pool growth), profiled with
@@ -11,7 +12,8 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def test_step_runs_only_framework_kernels():
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+def test_step_runs_only_framework_kernels(dtype):
     from torch.profiler import ProfilerActivity, profile
 
     from pytorch_multiprocessing_distributed_amd.data.loader import SyntheticImageNet
@@ -20,8 +22,11 @@ def test_step_runs_only_framework_kernels():
     from pytorch_multiprocessing_distributed_amd.ops import functional as OF
     from pytorch_multiprocessing_distributed_amd.parallel.dp import DataParallel
 
+    from pytorch_multiprocessing_distributed_amd.ops.fp8 import Fp8Scaling
+
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
+    OF.set_fp8(Fp8Scaling(dev) if dtype == "fp8" else None)   # fp8: delayed-scaling update is native too
     model = DataParallel(build_model("resnet50", num_classes=1000, stem="imagenet").to(dev), None)
     opt = FusedSGD(model, lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
     data = SyntheticImageNet(16, 112, 1000, steps=4, device=dev, dtype=torch.bfloat16, cpad=8, seed=0)
@@ -34,15 +39,18 @@ def test_step_runs_only_framework_kernels():
         loss.backward(OF.loss_seed(loss))
         opt.step()
 
-    for i in range(2):
-        step(i)
-    torch.cuda.synchronize()
     try:
-        with profile(activities=[ProfilerActivity.CUDA]) as prof:
-            step(2)
-            torch.cuda.synchronize()
-    except Exception as e:  # noqa: BLE001 -- no GPU tracer in this build
-        pytest.skip(f"torch.profiler CUDA activity unavailable: {e}")
+        for i in range(2):
+            step(i)
+        torch.cuda.synchronize()
+        try:
+            with profile(activities=[ProfilerActivity.CUDA]) as prof:
+                step(2)
+                torch.cuda.synchronize()
+        except Exception as e:  # noqa: BLE001 -- no GPU tracer in this build
+            pytest.skip(f"torch.profiler CUDA activity unavailable: {e}")
+    finally:
+        OF.set_fp8(None)
     names = {e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA}
     kernels = {n for n in names if not n.lower().startswith(("memcpy", "memset", "__amd_rocclr"))}
     if not kernels:
