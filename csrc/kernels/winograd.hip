@@ -10,7 +10,8 @@
 //
 // Three memory-bound transform kernels around 16 independent GEMMs
 //   M[xi][t][k] = sum_c V[xi][t][c] * U[xi][k][c]     (xi = 4x4 transform position)
-// which are plain batched library GEMMs (hipBLASLt via torch.bmm).  The output
+// which run as one grid.z-batched launch of the implicit-GEMM MFMA conv kernel
+// (conv_igemm_batched_launch: each is a 1x1 conv of T tiles by the K x C slice).  The output
 // transform fuses the BatchNorm statistics epilogue of conv_fwd (same [slot][2][K]
 // contract), so the Winograd path is a drop-in forward for a BN-followed conv.
 // Dgrad of the same layer is the forward of dY with the spatially flipped,
