@@ -189,3 +189,36 @@ def test_fp8_update_scales_native_matches_torch():
     assert torch.allclose(scale[:n], s_ref, rtol=1e-6, atol=0)
     assert torch.count_nonzero(amax[:n]).item() == 0
     assert torch.equal(amax[n:], tail_a) and torch.equal(scale[n:], tail_s)
+
+
+def test_basicblock_resnet_fp8_step():
+    """fp8 in BasicBlock networks (ResNet-34, ImageNet stem): every block conv is 3x3,
+    so block outputs carry e4m3 copies to the next block; a few SGD steps stay finite
+    and reduce the loss on a fixed batch, and fp8 sites exist for the 3x3 convs."""
+    from pytorch_multiprocessing_distributed_amd.engine.optim import FusedSGD
+    from pytorch_multiprocessing_distributed_amd.models import build_model
+    from pytorch_multiprocessing_distributed_amd.ops import functional as OF
+    from pytorch_multiprocessing_distributed_amd.ops.fp8 import Fp8Scaling
+    C = _C()
+    x, _ = C.synth_images(16, 64, 64, 8, 3, 10, 5, 0)
+    y = torch.arange(16, device=DEV) % 10
+    torch.manual_seed(0)
+    m = build_model("resnet34", num_classes=10, stem="imagenet").to(DEV)
+    f8 = Fp8Scaling(DEV)
+    OF.set_fp8(f8)
+    try:
+        opt = FusedSGD(m, lr=0.01, momentum=0.9, weight_decay=0.0, nesterov=True)
+        losses = []
+        for _ in range(15):
+            loss = OF.cross_entropy(m(x), y)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            losses.append(loss.item())
+    finally:
+        OF.set_fp8(None)
+    assert all(v == v for v in losses), losses
+    assert losses[-1] < 0.5 * losses[0], losses
+    n33 = sum(1 for mod in m.modules() if getattr(mod, "weight", None) is not None
+              and mod.weight.dim() == 4 and mod is not m.conv1 and tuple(mod.weight.shape[2:]) == (3, 3))
+    assert n33 == 32 and len(f8.sites) >= n33, (n33, len(f8.sites))
