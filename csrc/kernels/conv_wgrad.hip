@@ -451,18 +451,21 @@ static int ilog2w(int v) {
   return l;
 }
 
-// Total blocks the split-K plan aims for, by filter size (measured on the R50
-// layers, profiles/conv_bench_r01_wgrad_blocks.txt): 1x1 filters do best with
-// fewer, longer splits (less fp32 partial traffic), 3x3 with 1024, the 7x7 stem
-// with 2048.  Overridable: PMD_WGRAD_BLOCKS_R1 / _R3 / _R7.
+// Total blocks the split-K plan aims for, by filter size.  Isolated per-layer timing
+// (profiles/conv_bench_r01_wgrad_blocks.txt) favoured 512 (1x1) / 1024 (3x3) / 2048
+// (7x7 stem); in the step, where the wgrads run on the side stream next to the
+// main-stream kernels, fewer, longer splits win (less fp32 partial + reduce traffic,
+// fewer co-resident blocks): 384 / 384 measured +0.9% step over 512 / 1024 in three
+// interleaved A/B sessions (profiles/wgrad_blocks_step_ab_r02.txt).  Overridable:
+// PMD_WGRAD_BLOCKS_R1 / _R3 / _R7.
 static int env_int(const char* k, int dflt) {
   const char* e = getenv(k);
   const int v = e ? atoi(e) : 0;
   return v > 0 ? v : dflt;
 }
 static int wgrad_target_blocks(int R) {
-  static const int t1 = env_int("PMD_WGRAD_BLOCKS_R1", 512);
-  static const int t3 = env_int("PMD_WGRAD_BLOCKS_R3", 1024);
+  static const int t1 = env_int("PMD_WGRAD_BLOCKS_R1", 384);
+  static const int t3 = env_int("PMD_WGRAD_BLOCKS_R3", 384);
   static const int t7 = env_int("PMD_WGRAD_BLOCKS_R7", 2048);
   return R == 1 ? t1 : (R <= 3 ? t3 : t7);
 }
