@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--sync_bn", default="on", choices=["on", "off"])
     ap.add_argument("--bucket_mb", type=float, default=25.0)
     ap.add_argument("--first_bucket_mb", type=float, default=1.0)
+    ap.add_argument("--last_bucket_mb", type=float, default=2.0,
+                    help="cap of the last bucket (earliest layers, launched at the end of backward)")
     ap.add_argument("--syncbn_comm", default="auto", choices=["auto", "xgmi", "rccl"],
                     help="SyncBN statistics transport (auto: one-shot xGMI kernel when W>1)")
     ap.add_argument("--grad_compress", default="none", choices=["none", "bf16"])
@@ -66,7 +68,9 @@ def parse():
                     help="gradient-bucket transport: torch ProcessGroupNCCL or the native "
                          "RCCL communicator (csrc/runtime/rccl_comm.cpp)")
     ap.add_argument("--tune_table", default="",
-                    help="load a per-shape kernel tuning table (JSON, ops/tuning.py) before warmup")
+                    help="kernel tuning table loaded before warmup: '' = the committed table(s) for "
+                         "this device (ops/tables/, deterministic kernel choices), 'online' = "
+                         "autotune every shape in step 0, or a JSON path (ops/tuning.py)")
     ap.add_argument("--save_tune_table", default="", help="rank 0 writes the tuning table after warmup")
     ap.add_argument("--with_stock", action="store_true",
                     help="also measure the stock PyTorch-ROCm comparator in this run (W=1)")
@@ -77,6 +81,16 @@ def parse():
                     help="capture the whole training step (fwd+bwd+SGD) in a HIP graph and replay it "
                          "(single GPU); each replay is a full step on a freshly generated batch")
     return ap.parse_args()
+
+
+def syncbn_label(comm, sync_bn):
+    """What actually carried the SyncBN statistics: the one-shot xGMI kernel, or
+    the process group's own backend (RCCL = torch 'nccl', or gloo)."""
+    if comm is None or sync_bn != "on":
+        return None
+    if comm.xgmi is not None:
+        return "xgmi"
+    return {"nccl": "rccl"}.get(comm.backend, comm.backend)
 
 
 def bench_rank(rank, world, a):
@@ -103,7 +117,7 @@ def bench_rank(rank, world, a):
     setup_syncbn(comm, a.sync_bn, a.syncbn_comm, True)
     model = DataParallel(model, comm, bucket_mb=a.bucket_mb, first_bucket_mb=a.first_bucket_mb,
                          compress=a.grad_compress, transport=a.comm if comm is not None else "c10d",
-                         timeline=a.timeline)
+                         timeline=a.timeline, last_bucket_mb=a.last_bucket_mb)
     if a.dtype == "fp8":
         from pytorch_multiprocessing_distributed_amd.ops.fp8 import Fp8Scaling
         OF.set_fp8(Fp8Scaling(dev))
@@ -111,6 +125,15 @@ def bench_rank(rank, world, a):
     data = SyntheticImageNet(a.batch, a.image, a.classes, steps=a.warmup + a.steps, device=dev,
                              dtype=torch.bfloat16, cpad=8, seed=rank)
     model.train()
+    # kernel choices fixed before anything runs (also before a graph capture)
+    from pytorch_multiprocessing_distributed_amd.ops import tuning
+    if a.tune_table == "online":
+        tune_source = "online"
+    elif a.tune_table:
+        tuning.load(a.tune_table)
+        tune_source = "table:" + os.path.basename(a.tune_table)
+    else:
+        tune_source, _ = tuning.load_default()
 
     def step(i):
         x, y = data.batch_at(i)
@@ -149,9 +172,6 @@ def bench_rank(rank, world, a):
             sy.copy_(y)
             graph.replay()
             return static_loss
-    from pytorch_multiprocessing_distributed_amd.ops import tuning
-    if a.tune_table:
-        tuning.load(a.tune_table)
     for i in range(a.warmup):
         step(i)
         if i == 0 and comm is not None:
@@ -179,6 +199,7 @@ def bench_rank(rank, world, a):
     final_loss = float(loss.item())
     if comm is not None and comm.xgmi is not None:
         comm.xgmi.check()         # raises if any statistics exchange timed out
+    choice_hash = tuning.table_hash()
     if a.timeline and rank == 0 and comm is not None:
         for row in model.bucket_timeline():
             print("[bench] bucket %d: host launch %.0f us after first grad, finalize at %.0f us; "
@@ -208,11 +229,14 @@ def bench_rank(rank, world, a):
                        "image_size": a.image, "per_gpu_batch": a.batch,
                        "parallelism": parallelism, "sync_bn": a.sync_bn == "on" and world > 1,
                        "bucket_mb": a.bucket_mb, "hip_graph": bool(a.graph and world == 1),
-                       "syncbn_comm": ("xgmi" if comm is not None and comm.xgmi is not None
-                                       else "rccl" if world > 1 else None),
+                       "syncbn_comm": syncbn_label(comm, a.sync_bn),
                        "grad_compress": a.grad_compress,
-                       "grad_transport": model.transport},
+                       "grad_transport": model.transport,
+                       "grad_buckets_mb": ([round(m, 2) for m in model.bucket_sizes_mb()]
+                                           if comm is not None else None)},
             "final_loss": round(final_loss, 4),
+            "tune_source": tune_source,
+            "kernel_choice_hash": choice_hash,
         }
         if stock is not None:
             rec["stock_pytorch_rocm_ips_measured"] = round(stock, 1)

@@ -796,6 +796,14 @@ static void chk_lin(const Tensor& t, const char* what) {
 }
 
 // out[N][V] = x[N][K] . w[V][K]^T (+ b)
+// split-K workspace of one classifier product (stream-ordered via the caching allocator)
+float* linear_ws(Tensor& holder, const Tensor& like, int M, int Nc, int R) {
+  const long long n = pmd::linear_workspace_floats(M, Nc, R);
+  if (n == 0) return nullptr;
+  holder = torch::empty({n}, like.options().dtype(torch::kFloat32));
+  return holder.data_ptr<float>();
+}
+
 Tensor linear_fwd(Tensor x, Tensor w, c10::optional<Tensor> b) {
   chk_lin(x, "x");
   chk_lin(w, "w");
@@ -805,8 +813,10 @@ Tensor linear_fwd(Tensor x, Tensor w, c10::optional<Tensor> b) {
   if (bp) TORCH_CHECK(b->numel() == V, "linear: bias size");
   c10::DeviceGuard g(x.device());
   Tensor out = torch::empty({N, V}, x.options());
+  Tensor ws;
+  float* wsp = linear_ws(ws, x, N, V, K);
   CHECK_RC(pmd::linear_mfma_launch(x.data_ptr<float>(), w.data_ptr<float>(), out.data_ptr<float>(), bp,
-                                   K, 1, 1, K, N, V, K, false, cur_stream()), "linear_fwd");
+                                   K, 1, 1, K, N, V, K, false, wsp, cur_stream()), "linear_fwd");
   return out;
 }
 
@@ -818,8 +828,10 @@ Tensor linear_dgrad(Tensor dout, Tensor w) {
   const int N = dout.size(0), V = w.size(0), K = w.size(1);
   c10::DeviceGuard g(dout.device());
   Tensor dx = torch::empty({N, K}, dout.options());
+  Tensor ws;
+  float* wsp = linear_ws(ws, dout, N, K, V);
   CHECK_RC(pmd::linear_mfma_launch(dout.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(), nullptr,
-                                   V, 1, K, 1, N, K, V, false, cur_stream()), "linear_dgrad");
+                                   V, 1, K, 1, N, K, V, false, wsp, cur_stream()), "linear_dgrad");
   return dx;
 }
 
@@ -832,8 +844,10 @@ void linear_wgrad(Tensor dout, Tensor x, Tensor dw, c10::optional<Tensor> db, bo
   const int N = dout.size(0), V = dout.size(1), K = x.size(1);
   TORCH_CHECK(x.size(0) == N && dw.size(0) == V && dw.size(1) == K, "linear wgrad: shapes");
   c10::DeviceGuard g(dout.device());
+  Tensor ws;
+  float* wsp = linear_ws(ws, dout, V, K, N);
   CHECK_RC(pmd::linear_mfma_launch(dout.data_ptr<float>(), x.data_ptr<float>(), dw.data_ptr<float>(), nullptr,
-                                   1, V, K, 1, V, K, N, accumulate, cur_stream()), "linear_wgrad");
+                                   1, V, K, 1, V, K, N, accumulate, wsp, cur_stream()), "linear_wgrad");
   float* dbp = opt_f32(db, "db");
   if (dbp) {
     TORCH_CHECK(db->numel() == V, "linear wgrad: bias grad size");

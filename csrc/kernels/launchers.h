@@ -116,7 +116,9 @@ int sgd_launch(float* p, const float* g, float* buf, long long n, float lr, cons
 // classifier GEMMs (kernels/linear.hip): C[i][j] (+)= sum_r A(i,r) B(r,j) on bf16 MFMA, fp32 I/O
 int linear_mfma_launch(const float* A, const float* B, float* C, const float* bias, long long sai,
                        long long sar, long long sbr, long long sbj, int M, int Nc, int R, bool accumulate,
-                       hipStream_t st);
+                       float* ws, hipStream_t st);
+// fp32 workspace the split-K combine needs for this product (0: single split)
+long long linear_workspace_floats(int M, int Nc, int R);
 int linear_colsum_launch(const float* g, float* db, int rows, int cols, bool accumulate, hipStream_t st);
 
 int synth_images_launch(bf16_t* x, long long* labels, int N, int H, int W, int Cp, int Creal,

@@ -12,8 +12,12 @@
 // fp32 accumulation.  Each operand's loader walks its unit-stride dimension with
 // consecutive threads, so every layout above reads coalesced.  Tile 64x64x32,
 // 256 threads = 2x2 waves of 32x32; the reduction is split over grid.z so these
-// small-M products (M = the batch) still put ~1024 blocks on the chip, and the
-// splits add into the fp32 output with atomics (init pass: bias or zeros).
+// small-M products (M = the batch) still put ~1024 blocks on the chip.  The
+// splits are combined DETERMINISTICALLY: each writes its fp32 partial tile to a
+// workspace slab and one combine pass adds the slabs in split order (plus the
+// bias or the accumulation target), so logits, loss and dW are bitwise
+// reproducible run to run (fp32 atomics would make them order-dependent).
+// With a single split the MFMA kernel writes C itself.
 // The bias gradient (column sums of dout) is a separate one-pass kernel.
 #include "common.h"
 
@@ -60,10 +64,10 @@ struct LinTile {
   }
 };
 
-// grid.z splits the reduction: block z covers [z*rchunk, min(R, (z+1)*rchunk)) and
-// ADDS its partial product into C with fp32 atomics (C initialised by the caller:
-// bias / zeros, or an accumulation target); the bias is added by the init pass.
-__global__ __launch_bounds__(256) void linear_mfma_kernel(LinArgs a, int rchunk) {
+// grid.z splits the reduction: block z covers [z*rchunk, min(R, (z+1)*rchunk)).
+// ws == nullptr (one split): C = [C +] bias? + product.  Else the partial product
+// goes to slab z of ws ([splits][M][Nc]) and linear_combine_kernel finishes.
+__global__ __launch_bounds__(256) void linear_mfma_kernel(LinArgs a, int rchunk, float* __restrict__ ws) {
   __shared__ __attribute__((aligned(16))) bf16_t As[LT][LK + LPAD];
   __shared__ __attribute__((aligned(16))) bf16_t Bs[LT][LK + LPAD];  // Bs[j][k] = B(k, j)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -113,15 +117,28 @@ __global__ __launch_bounds__(256) void linear_mfma_kernel(LinArgs a, int rchunk)
       for (int e = 0; e < 4; ++e) {
         const int i = i0 + wm * 32 + p * 16 + (lane >> 4) * 4 + e;
         const int j = j0 + wn * 32 + q * 16 + (lane & 15);
-        if (i < a.M && j < a.Nc) atomicAdd(a.C + (long long)i * a.Nc + j, acc[p][q][e]);
+        if (i < a.M && j < a.Nc) {
+          const long long o = (long long)i * a.Nc + j;
+          if (ws) {
+            ws[(long long)blockIdx.z * a.M * a.Nc + o] = acc[p][q][e];
+          } else {
+            const float base = a.accumulate ? a.C[o] : (a.bias ? a.bias[j] : 0.f);
+            a.C[o] = base + acc[p][q][e];
+          }
+        }
       }
 }
 
-// C[i][j] = bias[j] (or 0): the init pass of a non-accumulating product
-__global__ __launch_bounds__(256) void linear_init_kernel(float* __restrict__ C, const float* __restrict__ bias,
-                                                          long long n, int Nc) {
-  for (long long t = blockIdx.x * 256ll + threadIdx.x; t < n; t += (long long)gridDim.x * 256)
-    C[t] = bias ? bias[t % Nc] : 0.f;
+// C[t] = (accumulate ? C[t] : bias[t % Nc] or 0) + sum_z ws[z][t], z in order
+__global__ __launch_bounds__(256) void linear_combine_kernel(float* __restrict__ C, const float* __restrict__ bias,
+                                                             const float* __restrict__ ws, long long n, int Nc,
+                                                             int splits, int accumulate) {
+  for (long long t = blockIdx.x * 256ll + threadIdx.x; t < n; t += (long long)gridDim.x * 256) {
+    float s = 0.f;
+    for (int z = 0; z < splits; ++z) s += ws[(long long)z * n + t];
+    const float base = accumulate ? C[t] : (bias ? bias[t % Nc] : 0.f);
+    C[t] = base + s;
+  }
 }
 
 // db[j] (+)= sum_i g[i][j]: 64 columns x 4 row lanes per block, LDS combine
@@ -141,19 +158,8 @@ __global__ __launch_bounds__(256) void linear_colsum_kernel(const float* __restr
   }
 }
 
-int linear_mfma_launch(const float* A, const float* B, float* C, const float* bias, long long sai,
-                       long long sar, long long sbr, long long sbj, int M, int Nc, int R, bool accumulate,
-                       hipStream_t st) {
-  if (M <= 0 || Nc <= 0 || R <= 0) return 1;
-  if (accumulate && bias) return 2;
-  LinArgs a{A, B, C, bias, sai, sar, sbr, sbj, M, Nc, R, accumulate ? 1 : 0};
-  if (!accumulate) {
-    const long long n = (long long)M * Nc;
-    long long nb = (n + 255) / 256;
-    hipLaunchKernelGGL(linear_init_kernel, dim3((int)(nb < 1024 ? nb : 1024)), dim3(256), 0, st, C, bias,
-                       n, Nc);
-  }
-  // split the reduction so the grid covers the chip (>= ~1024 blocks), 4+ K-steps per split
+// split plan: the grid covers the chip (>= ~1024 blocks), 4+ K-steps per split
+static void linear_plan(int M, int Nc, int R, int* splits_out, int* rchunk_out) {
   const int tiles = ((Nc + LT - 1) / LT) * ((M + LT - 1) / LT);
   int splits = (1024 + tiles - 1) / tiles;
   const int max_splits = (R + 4 * LK - 1) / (4 * LK);
@@ -161,9 +167,34 @@ int linear_mfma_launch(const float* A, const float* B, float* C, const float* bi
   if (splits < 1) splits = 1;
   int rchunk = (R + splits - 1) / splits;
   rchunk = (rchunk + LK - 1) / LK * LK;
-  splits = (R + rchunk - 1) / rchunk;
+  *splits_out = (R + rchunk - 1) / rchunk;
+  *rchunk_out = rchunk;
+}
+
+long long linear_workspace_floats(int M, int Nc, int R) {
+  if (M <= 0 || Nc <= 0 || R <= 0) return 0;
+  int splits, rchunk;
+  linear_plan(M, Nc, R, &splits, &rchunk);
+  return splits > 1 ? (long long)splits * M * Nc : 0;
+}
+
+int linear_mfma_launch(const float* A, const float* B, float* C, const float* bias, long long sai,
+                       long long sar, long long sbr, long long sbj, int M, int Nc, int R, bool accumulate,
+                       float* ws, hipStream_t st) {
+  if (M <= 0 || Nc <= 0 || R <= 0) return 1;
+  if (accumulate && bias) return 2;
+  LinArgs a{A, B, C, bias, sai, sar, sbr, sbj, M, Nc, R, accumulate ? 1 : 0};
+  int splits, rchunk;
+  linear_plan(M, Nc, R, &splits, &rchunk);
+  if (splits > 1 && !ws) return 3;
   const dim3 grid((Nc + LT - 1) / LT, (M + LT - 1) / LT, splits);
-  hipLaunchKernelGGL(linear_mfma_kernel, grid, dim3(256), 0, st, a, rchunk);
+  hipLaunchKernelGGL(linear_mfma_kernel, grid, dim3(256), 0, st, a, rchunk, splits > 1 ? ws : nullptr);
+  if (splits > 1) {
+    const long long n = (long long)M * Nc;
+    const long long nb = (n + 255) / 256;
+    hipLaunchKernelGGL(linear_combine_kernel, dim3((int)(nb < 2048 ? nb : 2048)), dim3(256), 0, st, C, bias, ws,
+                       n, Nc, splits, accumulate ? 1 : 0);
+  }
   return 0;
 }
 

@@ -17,10 +17,16 @@
 // reading call e).  Spins are bounded in WALL time (s_memrealtime, the
 // constant 100 MHz clock -- not an iteration count): on timeout the kernel
 // sets an error word in device memory AND a host-mapped word, then returns
-// instead of hanging the GPU.  The training loop reads the host-mapped word
-// after every step without any device sync (XgmiAllReduce.raise_if_failed)
-// and raises, so a timed-out exchange can never feed wrong statistics into
-// more than the step that produced them.
+// instead of hanging the GPU, and POISONS its outputs: every value it would
+// have produced (the summed vector; BN params / global backward sums) is
+// written as NaN, so whatever consumes it -- activations, loss, gradients,
+// weights after the SGD step -- is visibly invalid rather than silently
+// wrong (running statistics and the shift are left untouched).  Detection:
+// the training loop reads the host-mapped word after every step without a
+// device sync (XgmiAllReduce.raise_if_failed), so a failure is raised within
+// the host's run-ahead window (the steps already queued when the word is set;
+// bounded by the next synchronising print), and the epoch-end synchronise +
+// check runs before any checkpoint is written: a poisoned state is never saved.
 #include "common.h"
 
 namespace pmd {
@@ -53,10 +59,12 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(XgmiPeers peers, fl
                                                             uint32_t* err_host,
                                                             unsigned long long timeout_ticks) {
   __shared__ uint32_t e_sh;
+  __shared__ int bad_sh;
   const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x;
   if (tid == 0) {
     e_sh = epochs[b] + 1;
     epochs[b] = e_sh;
+    bad_sh = 0;
   }
   __syncthreads();
   const uint32_t e = e_sh;
@@ -84,15 +92,16 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(XgmiPeers peers, fl
   // 3) wait until every rank's chunk for epoch e has landed in MY buffer
   if (tid < world) {
     const uint32_t* f = peers.flags[rank] + tid * kXgmiMaxBlocks + b;
-    (void)xgmi_wait_flag(f, e, timeout_ticks, err, err_host);
+    if (!xgmi_wait_flag(f, e, timeout_ticks, err, err_host)) bad_sh = 1;
   }
   __syncthreads();
-  // 4) sum the W slots in rank order (identical on every rank)
+  // 4) sum the W slots in rank order (identical on every rank); NaN on timeout
   const float* mine = peers.data[rank] + (size_t)p * world * kXgmiCap + lo;
+  const bool bad = bad_sh != 0;
   for (int i = tid; i < len; i += 256) {
     float s = 0.f;
     for (int r = 0; r < world; ++r) s += mine[(size_t)r * kXgmiCap + i];
-    x[lo + i] = s;
+    x[lo + i] = bad ? __builtin_nanf("") : s;
   }
   (void)nb;
 }
@@ -138,10 +147,12 @@ __global__ __launch_bounds__(256) void xgmi_bn_kernel(XgmiPeers peers, XgmiBnArg
                                                      unsigned long long timeout_ticks) {
   __shared__ float loc[kXgmiChunk];
   __shared__ uint32_t e_sh;
+  __shared__ int bad_sh;
   const int b = blockIdx.x, tid = threadIdx.x;
   if (tid == 0) {
     e_sh = epochs[b] + 1;
     epochs[b] = e_sh;
+    bad_sh = 0;
   }
   const int P = a.CA + a.CB;
   const int p0 = b * a.pairs;
@@ -202,10 +213,11 @@ __global__ __launch_bounds__(256) void xgmi_bn_kernel(XgmiPeers peers, XgmiBnArg
                        __HIP_MEMORY_SCOPE_SYSTEM);
   if (tid < world) {
     const uint32_t* f = peers.flags[rank] + tid * kXgmiMaxBlocks + b;
-    (void)xgmi_wait_flag(f, e, timeout_ticks, err, err_host);
+    if (!xgmi_wait_flag(f, e, timeout_ticks, err, err_host)) bad_sh = 1;
   }
   __syncthreads();
-  // 4) global sums in rank order, then finalize / publish
+  const bool bad = bad_sh != 0;
+  // 4) global sums in rank order, then finalize / publish (NaN outputs on timeout)
   const float* mine = peers.data[rank] + (size_t)par * world * kXgmiCap + (size_t)b * kXgmiChunk;
   float cnt = 0.f;
   for (int r = 0; r < world; ++r) cnt += mine[(size_t)r * kXgmiCap + 2 * kBnPairs];
@@ -219,7 +231,20 @@ __global__ __launch_bounds__(256) void xgmi_bn_kernel(XgmiPeers peers, XgmiBnArg
     const bool isA = pi < a.CA;
     const int C = isA ? a.CA : a.CB;
     const int c = isA ? pi : pi - a.CA;
-    if (a.mode == 0) {
+    if (bad) {
+      const float qn = __builtin_nanf("");
+      if (a.mode == 0) {
+        const BnFinalizeOut& o = isA ? a.fA : a.fB;
+        o.params[c] = qn;
+        o.params[C + c] = qn;
+        o.params[2 * C + c] = qn;
+        o.params[3 * C + c] = qn;
+      } else {
+        float* out = isA ? a.outA : a.outB;
+        out[c] = qn;
+        out[C + c] = qn;
+      }
+    } else if (a.mode == 0) {
       const BnFinalizeOut& o = isA ? a.fA : a.fB;
       // every rank shifted its sums by the same K (the previous step's global mean)
       float mean, var;
@@ -243,7 +268,7 @@ __global__ __launch_bounds__(256) void xgmi_bn_kernel(XgmiPeers peers, XgmiBnArg
       out[C + c] = g1;
     }
   }
-  if (a.mode == 0 && b == 0 && tid == 0 && a.count_out) a.count_out[0] = cnt;
+  if (a.mode == 0 && b == 0 && tid == 0 && a.count_out) a.count_out[0] = bad ? __builtin_nanf("") : cnt;
 }
 
 int xgmi_bn_launch(float* const* data, uint32_t* const* flags, const XgmiBnArgs& args, int rank, int world,

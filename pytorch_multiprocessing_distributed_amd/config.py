@@ -63,13 +63,21 @@ def build_parser():
                    help="SyncBN statistics transport: one-shot xGMI IPC kernel or the process "
                         "group (auto: xgmi on multi-GPU runs)")
     p.add_argument("--tune_table", default="", type=str,
-                   help="load a per-shape kernel tuning table (JSON, ops/tuning.py) before training")
+                   help="per-shape kernel tuning table (JSON, ops/tuning.py) loaded before training; "
+                        "default: the committed table for this device; 'online': autotune in step 0")
     p.add_argument("--save_tune_table", default="", type=str,
                    help="rank 0 writes the tuning table after the first training step")
     p.add_argument("--reducer", default="native", choices=["native", "python"],
                    help="gradient bucket reducer implementation")
     p.add_argument("--grad_compress", default="none", choices=["none", "bf16"],
                    help="wire dtype of the gradient all-reduce")
+    p.add_argument("--comm", default="c10d", choices=["c10d", "rccl"],
+                   help="gradient-bucket transport: torch ProcessGroupNCCL (c10d, default) or the "
+                        "framework's own RCCL communicator (csrc/runtime/rccl_comm.cpp; "
+                        "experimental: needs the xGMI SyncBN transport or --sync_bn off)")
+    p.add_argument("--last_bucket_mb", default=2.0, type=float,
+                   help="cap of the LAST gradient bucket (earliest layers: its all-reduce is "
+                        "launched at the end of backward, fully exposed)")
     return p
 
 

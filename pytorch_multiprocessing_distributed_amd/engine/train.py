@@ -217,16 +217,28 @@ def _run(rank, world_size, args, dev):
     train_loader, test_loader = build_loaders(args, rank, world_size, dev, dtype, cpad)
     if args.seed is not None:
         torch.manual_seed(args.seed)
-    if on_gpu and getattr(args, "tune_table", ""):
+    if on_gpu:
+        # deterministic kernel choices: the committed per-device table unless a
+        # table (or 'online' step-0 autotuning) is asked for
         from ..ops import tuning
-        tuning.load(args.tune_table)
+        tt = getattr(args, "tune_table", "")
+        if tt and tt != "online":
+            tuning.load(tt)
+        elif not tt:
+            tuning.load_default()
     model = build_model(args.model, num_classes=args.num_classes, stem=args.stem).to(dev)
     comm = get_comm()
     setup_syncbn(comm, args.sync_bn, getattr(args, "syncbn_comm", "auto"), on_gpu)
     model = DataParallel(model, comm, bucket_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb,
                          broadcast_buffers=args.broadcast_buffers,
                          reducer=getattr(args, "reducer", "native"),
-                         compress=getattr(args, "grad_compress", "none"))
+                         compress=getattr(args, "grad_compress", "none"),
+                         transport=getattr(args, "comm", "c10d") if on_gpu else "c10d",
+                         last_bucket_mb=getattr(args, "last_bucket_mb", 2.0))
+    if rank == 0 and comm is not None:
+        print("[pmd] gradient buckets (MiB, launch order): "
+              + " ".join(f"{m:.2f}" for m in model.bucket_sizes_mb())
+              + f" via {model.transport}", flush=True)
     optimizer = FusedSGD(model, lr=args.lr, momentum=args.momentum, weight_decay=args.wd,
                          nesterov=True)
     scheduler = torch.optim.lr_scheduler.MultiStepLR(optimizer, milestones=args.milestone_list,

@@ -67,7 +67,11 @@ def shutdown():
 def abort():
     """Abort the communicators of this rank (RCCL: ``ncclCommAbort``) after a
     local failure, so peers blocked in a collective fail fast instead of
-    waiting out the collective timeout.  Best effort."""
+    waiting out the collective timeout.  Best effort.  Covers the
+    framework's own communicators (``parallel.rccl``: the ``--comm rccl``
+    gradient transport) as well as the c10d process group."""
+    from .parallel import rccl
+    rccl.abort_all()
     if not (dist.is_available() and dist.is_initialized()):
         return
     try:

@@ -35,6 +35,7 @@ reducer averages them).  Unlike torch there is no device->host sync (B13).
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 
@@ -414,8 +415,21 @@ def _after_dgrad_event(t, sync):
 
 
 # ---------------------------------------------------------------- BN pieces
-def _bn_forward_params(P, y, st, bn, training, sync, y2=None, st2=None, bn2=None):
-    """-> (p1, p2, count); count is a host float (local) or device scalar (SyncBN)."""
+_UNSET = object()
+# stats object returned by the public conv() -> the shift its sums were taken about
+_SHIFT_USED: dict = {}
+
+
+def _pop_shift(st):
+    e = _SHIFT_USED.pop(id(st), None) if st is not None else None
+    return e[1] if (e is not None and e[0]() is st) else _UNSET
+
+
+def _bn_forward_params(P, y, st, bn, training, sync, y2=None, st2=None, bn2=None,
+                       k1=_UNSET, k2=_UNSET):
+    """-> (p1, p2, count); count is a host float (local) or device scalar (SyncBN).
+    ``k1``/``k2``: the shift the statistics were accumulated about (default: the
+    BN's own -- what every fused path requests from its producing conv)."""
     if not training:
         p1 = P.bn_eval_params(bn.running_mean, bn.running_var, bn.weight, bn.bias, bn.eps)
         p2 = None
@@ -424,8 +438,8 @@ def _bn_forward_params(P, y, st, bn, training, sync, y2=None, st2=None, bn2=None
         return p1, p2, None
     c1 = y.shape[-1]
     m_local = y.numel() // c1
-    k1 = _shift_of(bn)
-    k2 = _shift_of(bn2)
+    k1 = _shift_of(bn) if k1 is _UNSET else k1
+    k2 = _shift_of(bn2) if k2 is _UNSET else k2
     if sync is None:
         p1 = P.stats_finalize_local(st, float(m_local), bn.weight, bn.bias, bn.eps,
                                     bn.running_mean, bn.running_var, bn.momentum,
@@ -646,8 +660,15 @@ def conv(x, conv_mod, want_stats=None, bn=None):
         want_stats = conv_mod.training
     req = _stats_req(bn, True) if (bn is not None and want_stats) else bool(want_stats)
     if _s2d_stem_ok(x, conv_mod):
-        return _StemS2DConvFn.apply(x, conv_mod.weight, req)
-    return _ConvFn.apply(x, conv_mod.weight, conv_mod.stride, conv_mod.padding, req)
+        y, st = _StemS2DConvFn.apply(x, conv_mod.weight, req)
+    else:
+        y, st = _ConvFn.apply(x, conv_mod.weight, conv_mod.stride, conv_mod.padding, req)
+    # the shift the sums were taken about travels with them (keyed by the stats
+    # object this call returned; bn_add_act pops it): a BN finalize must use
+    # exactly this K (None: plain sums), not re-derive it from its module
+    if want_stats:
+        _SHIFT_USED[id(st)] = (weakref.ref(st), req if torch.is_tensor(req) else None)
+    return y, st
 
 
 # ------------------------------------------------------------------------ BN
@@ -656,12 +677,12 @@ class _BNActFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, cfg, y1, s1, g1, b1, res, y2, s2, g2, b2):
-        bn1, bn2, relu, training = cfg
+        bn1, bn2, relu, training, k1, k2 = cfg
         P = prims_for(y1)
         sync = _state["bn_sync"] if training else None
         two = y2 is not None
         p1, p2, count = _bn_forward_params(P, y1, s1, bn1, training, sync, y2, s2,
-                                           bn2 if two else None)
+                                           bn2 if two else None, k1=k1, k2=k2)
         out, mask = P.bn_apply(y1, p1, res, y2, p2, relu)
         ctx.cfg = (bn1, bn2 if two else None, relu, training, res is not None, sync, count)
         ctx.save_for_backward(y1, mask if relu else _empty(y1.device), p1,
@@ -681,7 +702,8 @@ class _BNActFn(torch.autograd.Function):
 
 
 def bn_add_act(y, stats, bn, residual=None, res_y=None, res_stats=None, res_bn=None, relu=True):
-    cfg = (bn, res_bn, relu, bn.training)
+    k1, k2 = _pop_shift(stats), _pop_shift(res_stats)
+    cfg = (bn, res_bn, relu, bn.training, k1, k2)
     if res_y is not None:
         return _BNActFn.apply(cfg, y, stats, bn.weight, bn.bias, None,
                               res_y, res_stats, res_bn.weight, res_bn.bias)

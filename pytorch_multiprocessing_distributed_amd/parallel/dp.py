@@ -67,6 +67,27 @@ class _Bucket:
         self.fired = 0
 
 
+def _check_single_in_step_communicator(comm):
+    """``transport='rccl'`` puts the bucket all-reduces on a SECOND communicator
+    (the native ``RcclComm``, its own HIP stream).  Two communicators with
+    blocking collective kernels in flight at once on different streams can
+    deadlock across ranks, so the only other in-step traffic allowed next to it
+    is the one-shot xGMI SyncBN exchange (a kernel of ours with a wall-clock
+    bounded spin, not a c10d collective).  SyncBN statistics over c10d (gloo or
+    ProcessGroupNCCL) inside the step would be concurrent with the bucket
+    all-reduces: refused.  (The once-per-run c10d traffic -- the bucket-rebuild
+    order broadcast and the tuning-table broadcast -- is issued from the
+    forward / after the step, i.e. after the finalize made the compute stream
+    wait on every bucket, and c10d fences its stream on the compute stream, so
+    it is serialised behind the native collectives.)"""
+    from ..ops import functional as OF
+    sync = OF.get_bn_sync()
+    if sync is not None and getattr(sync, "xgmi", None) is None:
+        raise ValueError("transport='rccl' (--comm rccl) with SyncBN over the process group would run "
+                         "collectives of two communicators concurrently; use --syncbn_comm xgmi, "
+                         "--sync_bn off, or --comm c10d")
+
+
 def _flush_wgrads():
     from ..ops.functional import flush_pending_wgrads
     flush_pending_wgrads()
@@ -76,8 +97,10 @@ class DataParallel(nn.Module):
     def __init__(self, module: nn.Module, comm: Comm | None = None, bucket_mb: float = 25.0,
                  first_bucket_mb: float = 1.0, broadcast_buffers: bool = False,
                  check_collectives: bool = True, reducer: str = "native", compress: str = "none",
-                 transport: str = "c10d", rebuild_buckets: bool = True, timeline: bool | None = None):
+                 transport: str = "c10d", rebuild_buckets: bool = True, timeline: bool | None = None,
+                 last_bucket_mb: float | None = 2.0):
         super().__init__()
+        self.last_bucket_mb = last_bucket_mb
         self.module = module
         self.comm = comm
         self.world_size = comm.world_size if comm is not None else 1
@@ -96,6 +119,7 @@ class DataParallel(nn.Module):
         if comm is not None and transport == "rccl":
             if reducer != "native" or comm.backend != "nccl":
                 raise ValueError("transport='rccl' needs the native reducer and GPU ranks")
+            _check_single_in_step_communicator(comm)
             from . import rccl
             self.rccl = rccl.create(comm.group)
         if comm is not None:
@@ -130,18 +154,38 @@ class DataParallel(nn.Module):
 
     # ------------------------------------------------------------ buckets
     def _build_buckets(self):
+        """Contiguous arena slices in arena (= expected gradient-ready) order: a
+        small first bucket so the first all-reduce starts early, ``bucket_mb``
+        after that, and a small LAST bucket.  The last-ready parameters (stem and
+        first stage) only get their gradients at the very end of backward, so
+        their all-reduce cannot overlap anything; capping that tail bounds the
+        exposed collective (at W=8 a ring all-reduce moves 2(W-1)/W of the bucket
+        over each xGMI link: 2 MiB fp32 -> 3.7 MB at ~150 GB/s ~ 25 us + launch
+        latency, vs ~9 MB / 60 us for the uncapped R50 tail)."""
         fp = self.flat
+        n = len(fp.params)
+        nb = [p.numel() * p.element_size() for p in fp.params]
+        tail_start = n
+        if self.last_bucket_mb and n > 1:
+            cap, acc = int(self.last_bucket_mb * 2 ** 20), 0
+            while tail_start > 1 and acc + nb[tail_start - 1] <= cap:
+                tail_start -= 1
+                acc += nb[tail_start]
+            if tail_start == n:          # the last parameter alone exceeds the cap
+                tail_start = n - 1
         groups, cur, nbytes = [], [], 0
         cap = int(self.first_bucket_mb * 2 ** 20)
-        for i, p in enumerate(fp.params):
+        for i in range(tail_start):
             cur.append(i)
-            nbytes += p.numel() * p.element_size()
+            nbytes += nb[i]
             if nbytes >= cap:
                 groups.append(cur)
                 cur, nbytes = [], 0
                 cap = int(self.bucket_mb * 2 ** 20)
         if cur:
             groups.append(cur)
+        if tail_start < n:
+            groups.append(list(range(tail_start, n)))
         # bucket = contiguous arena slice from its first param to the next bucket's start
         starts = [fp.offsets[g[0]] for g in groups] + [fp.numel]
         self.buckets = [_Bucket(j, starts[j], starts[j + 1], g) for j, g in enumerate(groups)]

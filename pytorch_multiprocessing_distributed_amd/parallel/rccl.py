@@ -12,11 +12,45 @@ all-reduces there, fenced with HIP events (no host blocking).
 from __future__ import annotations
 
 import itertools
+import weakref
 
 import torch
 import torch.distributed as dist
 
 _SEQ = itertools.count()
+# every live native communicator of this process, so a failing rank can abort
+# them all (launch.abort) and its peers' RCCL kernels error out instead of
+# waiting for a rank that will never arrive
+_LIVE: "weakref.WeakSet" = weakref.WeakSet()
+_STRONG: list = []          # objects that cannot be weakly referenced
+
+
+def register(comm):
+    """Track ``comm`` (anything with ``abort()``) for :func:`abort_all`."""
+    try:
+        _LIVE.add(comm)
+    except TypeError:
+        _STRONG.append(comm)
+    return comm
+
+
+def live():
+    return list(_LIVE) + list(_STRONG)
+
+
+def abort_all() -> int:
+    """``ncclCommAbort`` every live native communicator; returns how many.
+    Best effort: one communicator failing to abort never stops the others."""
+    n = 0
+    for c in live():
+        try:
+            c.abort()
+            n += 1
+        except Exception:  # noqa: BLE001 -- already failing; never mask the original error
+            pass
+    _LIVE.clear()
+    _STRONG.clear()
+    return n
 
 
 def _store():
@@ -38,7 +72,7 @@ def create(group=None, priority: int = 0, store=None):
     uid = store.get(key)                      # blocks until rank 0 published it
     dev = torch.cuda.current_device()
     comm = C.RcclComm(bytes(uid), rank, world, dev, priority)
-    return comm
+    return register(comm)
 
 
 def create_single(device: int | None = None, priority: int = 0):
@@ -46,4 +80,4 @@ def create_single(device: int | None = None, priority: int = 0):
     RCCL launch / stream / event path on one GPU (tests, W=1 benches)."""
     from ..ops.native import C
     dev = torch.cuda.current_device() if device is None else device
-    return C.RcclComm(bytes(C.RcclComm.unique_id()), 0, 1, dev, priority)
+    return register(C.RcclComm(bytes(C.RcclComm.unique_id()), 0, 1, dev, priority))

@@ -597,6 +597,30 @@ def test_linear_mfma(N, K, V):
     _close(db0, db1, 1e-5)
 
 
+@pytest.mark.parametrize("N,K,V", [(256, 2048, 1000), (64, 512, 10)])
+def test_linear_split_k_deterministic(N, K, V):
+    """The split-K classifier combines its partial products in a fixed order
+    (workspace slabs, no fp32 atomics): repeated products are bitwise equal,
+    including dW accumulated into an existing target."""
+    HP = _hp()
+    torch.manual_seed(4)
+    x = torch.randn(N, K, device=DEV)
+    w = torch.randn(V, K, device=DEV) / K ** 0.5
+    b = torch.randn(V, device=DEV)
+    dout = torch.randn(N, V, device=DEV)
+    f = [HP.linear_fwd(x, w, b) for _ in range(3)]
+    d = [HP.linear_dgrad(dout, w) for _ in range(3)]
+    base = torch.randn(V, K, device=DEV)
+    g = []
+    for _ in range(3):
+        t = base.clone()
+        HP.linear_wgrad(dout, x, t, None, True)
+        g.append(t)
+    for seq in (f, d, g):
+        for t in seq[1:]:
+            assert torch.equal(t, seq[0])
+
+
 @pytest.mark.parametrize("n,off", [(1, 0), (15, 3), (4096, 0), (1000003, 5)])
 def test_zero_kernel(n, off):
     """The framework's fill kernel (gradient-arena zero_grad, fresh accumulators):

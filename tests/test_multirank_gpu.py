@@ -224,6 +224,7 @@ def _straggler_worker(rank, world, port, out):
     x, y = _data(8, 32)
     err = ""
     steps_done = 0
+    finite = []
     try:
         for i in range(4):
             launch.maybe_inject_fault(rank, i)
@@ -232,6 +233,8 @@ def _straggler_worker(rank, world, port, out):
             loss.backward()
             opt.step()
             torch.cuda.synchronize()
+            finite.append(bool(torch.isfinite(loss).item())
+                          and bool(torch.isfinite(dp.flat.param_arena).all().item()))
             comm.raise_if_failed()
             steps_done += 1
             if i == 1:
@@ -240,7 +243,7 @@ def _straggler_worker(rank, world, port, out):
     except Exception as e:  # noqa: BLE001
         err = str(e)
     with open(f"{out}.{rank}", "w") as f:
-        json.dump({"err": err, "steps": steps_done}, f)
+        json.dump({"err": err, "steps": steps_done, "finite": finite}, f)
     OF.set_bn_sync(None)
     os._exit(0)          # do not wait in a collective on a peer that already left
 
@@ -252,6 +255,9 @@ def test_straggler_timeout_raises(tmp_path):
     r0 = json.load(open(f"{out}.0"))
     assert "timed out" in r0["err"], r0
     assert r0["steps"] == 2, r0      # steps 0-1 fine, step 2 detected, no step 3
+    # the timed-out exchange poisoned its outputs: the failing step's loss /
+    # updated weights are NaN, not silently wrong (kernels/xgmi.hip)
+    assert r0["finite"] == [True, True, False], r0
 
 
 # ------------------------------------------- spinning kernels on two streams
