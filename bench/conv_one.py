@@ -1,6 +1,7 @@
 """Run ONE conv layer configuration repeatedly (for rocprofv3 --pmc passes).
 
-    python bench/conv_one.py C H K R stride [--tile T] [--pipe P] [--impl I] [--pass fwd|dgrad]
+    python bench/conv_one.py C H K R stride [--tile T] [--pipe P] [--impl I] [--pass fwd|dgrad|wgrad]
+                             [--wimpl W]   (wgrad staging variant, conv_wgrad.hip; -1 = autotuned)
 """
 import argparse
 import os
@@ -24,6 +25,7 @@ def main():
     ap.add_argument("--pass", dest="which", default="fwd")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--nostats", action="store_true", help="forward without BN statistics")
+    ap.add_argument("--wimpl", type=int, default=-1, help="wgrad staging variant (-1: autotuned)")
     a = ap.parse_args()
     _C.conv_set_autotune(0)
     _C.conv_set_tile(a.tile)
@@ -36,6 +38,9 @@ def main():
     wp = HP.conv_weight(w, torch.bfloat16, a.C, True)
     y, s = HP.conv_fwd(x, wp, a.stride, pad, True)
     dy = torch.randn_like(y)
+    dw = torch.zeros(tuple(wp[0].shape), device="cuda", dtype=torch.float32)
+    if a.which == "wgrad" and a.wimpl >= 0:
+        _C.conv_wgrad_set_impl(a.wimpl)
     ts = []
     for _ in range(a.iters):
         e0 = torch.cuda.Event(enable_timing=True)
@@ -45,6 +50,8 @@ def main():
             y, s = HP.conv_fwd(x, wp, a.stride, pad, not a.nostats)
             if s is not None:
                 HP._release(s)
+        elif a.which == "wgrad":
+            HP.conv_wgrad(dy, x, tuple(wp[0].shape), a.stride, pad, out=dw)
         else:
             HP.conv_dgrad(dy, wp, tuple(x.shape), a.stride, pad)
         e1.record()

@@ -1,6 +1,8 @@
 """Per-kernel gfx950 counter summary of bench/pmc_step.sh (last training step).
 
-    python bench/pmc_summary.py gpurun_out/pmc > profiles/pmc_r50_step_r01.txt
+    python bench/pmc_summary.py gpurun_out/pmc [--all] [--title TEXT] > profiles/pmc_r50_step_r01.txt
+
+(--all: every dispatch of the run instead of the last training step)
 
 Columns (summed over the step's dispatches of each kernel):
   ms          kernel time (kernel trace of the pass-A run)
@@ -54,11 +56,17 @@ def last_step(per, marker="synth_images_kernel"):
 
 
 def main():
-    root = sys.argv[1]
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root")
+    ap.add_argument("--all", action="store_true")
+    ap.add_argument("--title", default="one ResNet-50 bs256 bf16 training step")
+    a = ap.parse_args()
+    root = a.root
     agg = defaultdict(lambda: defaultdict(float))
     for p in "ABC":
         per, dur = load_pass(os.path.join(root, "pass" + p))
-        for i in last_step(per):
+        for i in (sorted(per) if a.all else last_step(per)):
             k = short(per[i]["name"])
             for c, v in per[i].items():
                 if c != "name" and (p == "A" or c != "GRBM_GUI_ACTIVE"):
@@ -68,7 +76,7 @@ def main():
                 agg[k]["calls"] += 1
     rows = sorted(agg.items(), key=lambda kv: -kv[1]["ms"])
     tot = sum(v["ms"] for _, v in rows)
-    print(f"# one ResNet-50 bs256 bf16 training step, MI355X, rocprofv3 --pmc (3 passes); total {tot:.2f} ms "
+    print(f"# {a.title}, MI355X, rocprofv3 --pmc (3 passes); total {tot:.2f} ms "
           f"(counter runs serialise kernels)")
     print(f"{'kernel':58s} {'calls':>5s} {'ms':>7s} {'MFMA%':>6s} {'TF':>5s} {'VALU/MFMA':>9s} {'LDSconf%':>8s} "
           f"{'rdGB':>6s} {'wrGB':>6s} {'TB/s':>5s} {'L2hit%':>6s}")

@@ -16,7 +16,6 @@ from __future__ import annotations
 import torch
 
 from . import torch_prims as _TP
-from . import winograd as _WG
 from .native import C as _C
 
 SLOTS = 64
@@ -68,9 +67,6 @@ def conv_fwd(x, wpack, stride, pad, want_stats):
     """``want_stats``: False, True, or the BN statistics shift (fp32 [K], see
     torch_prims.conv_fwd): the slots then hold sums about that shift."""
     want, shift = _TP.stats_request(want_stats)
-    if _WG.get_algo() == "winograd" and _WG.eligible(tuple(wpack[0].shape), stride, pad, x.shape[-1]):
-        return _WG.conv_fwd(x, wpack[0], want,
-                            _acquire(wpack[0].shape[0], x.device) if want else None, shift)
     if want:
         buf = _acquire(wpack[0].shape[0], x.device)
         y, st = _C.conv_fwd(x, wpack[0], int(stride), int(pad), True, buf, shift)
@@ -84,9 +80,6 @@ def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None, bnred=None, addend_
     and returns ``(dx, [slot buffers])`` (same contract as :func:`bn_bwd_reduce`)."""
     if len(wpack) < 2:
         raise RuntimeError("dgrad image was not prepared (input did not require grad)")
-    if (bnred is None and addend is None and _WG.get_algo() == "winograd"
-            and _WG.eligible(tuple(wpack[0].shape), stride, pad)):
-        return _WG.conv_dgrad(dy, wpack[0], x_shape)
     if bnred is None:
         return _C.conv_dgrad(dy, wpack[1], int(x_shape[1]), int(x_shape[2]), int(stride), int(pad),
                              addend, None, None, None, None, None, None, None, addend_mask)

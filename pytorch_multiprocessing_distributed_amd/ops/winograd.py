@@ -12,36 +12,23 @@ implicit-GEMM MFMA kernel (``C.winograd_gemm``; no library GEMM):
     y  = winograd_output(M)             [N, H, W, K] (A^T M A) + fused BN statistics
 
 Dgrad of the same layer is the same pipeline on dY with the flipped,
-channel-transposed filter.  Selected with ``PMD_CONV_ALGO=winograd`` (or
-:func:`set_algo`); the default stays the implicit-GEMM MFMA kernel, which the
-measurements in ``profiles/winograd_r01.txt`` show is faster on MI355X (the
-transformed operands are 4x the activation bytes; see docs/ARCHITECTURE.md).
+channel-transposed filter.  NOT on the training path: an explicit API
+(:func:`conv_fwd` / :func:`conv_dgrad`, tests and bench/winograd_bench.py only).
+The implicit-GEMM MFMA kernel is faster on every ResNet-50 layer on MI355X: the
+transformed operands are 4x the activation bytes and the transforms alone run at
+the HBM roofline (profiles/winograd_r02_native_gemm.txt, counters in
+profiles/pmc_winograd_r03.txt; the fused-kernel bound in docs/ARCHITECTURE.md).
 
 ``conv_ref`` is the same algorithm in plain torch fp32 -- the CPU numerics
 reference of the transforms (tests/test_winograd_cpu.py).
 """
 from __future__ import annotations
 
-import os
-
 import torch
 
 BT = torch.tensor([[1., 0., -1., 0.], [0., 1., 1., 0.], [0., -1., 1., 0.], [0., 1., 0., -1.]])
 G = torch.tensor([[1., 0., 0.], [.5, .5, .5], [.5, -.5, .5], [0., 0., 1.]])
 AT = torch.tensor([[1., 1., 1., 0.], [0., 1., -1., -1.]])
-
-_ALGO = os.environ.get("PMD_CONV_ALGO", "igemm")
-
-
-def set_algo(name: str):
-    global _ALGO
-    if name not in ("igemm", "winograd"):
-        raise ValueError(f"unknown conv algorithm {name!r}")
-    _ALGO = name
-
-
-def get_algo() -> str:
-    return _ALGO
 
 
 def eligible(wk_shape, stride, pad, cin=None) -> bool:
