@@ -39,6 +39,11 @@ struct WgradArgs {
   int P, Q, K, R, S, stride, pad;
   int M, Kg;
   int chunks_per_split;  // 64-row chunks per block
+  // TX: dy holds dzm and the operand is a[k] dzm + b[k] tx_y + c[k] (BN backward on
+  // load, coef [3][tx_cp]); register-staged kernel only
+  const bf16_t* tx_y;
+  const float* tx_coef;
+  int tx_cp;
 };
 
 constexpr int BR = 64;  // reduction rows per stage
@@ -59,7 +64,7 @@ __device__ __forceinline__ int toff(int row, int col) {
   return row * ROWB + (((byte >> 5) ^ swz<ROWB>(row)) << 5) + (byte & 31);
 }
 
-template <int BM, int BN>
+template <int BM, int BN, bool TX = false>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
   constexpr int MI = BM / 32, NI = BN / 32;
   constexpr int A_BYTES = BR * BM * 2, B_BYTES = BR * BN * 2;
@@ -108,6 +113,17 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
     bq_[i] = rem - bp_[i] * a.Q;
   }
   const int dq = BR % a.Q, dp = (BR / a.Q) % a.P, dn = BR / pq;
+  // TX: this thread's 8 dY channels are fixed for the whole kernel
+  float ta[8], tb[8], tc[8];
+  if constexpr (TX) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = a_colok ? k0 + a_col + e : 0;
+      ta[e] = a.tx_coef[k];
+      tb[e] = a.tx_coef[a.tx_cp + k];
+      tc[e] = a.tx_coef[2 * a.tx_cp + k];
+    }
+  }
 
   uint4 ra[PA], rb[PB];
   auto load = [&](int ch) {
@@ -116,7 +132,18 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
     for (int i = 0; i < PA; ++i) {
       const int m = mb + a_row + RA * i;
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (a_colok && m < mend) v = *reinterpret_cast<const uint4*>(a.dy + (size_t)m * a.K + k0 + a_col);
+      if (a_colok && m < mend) {
+        v = *reinterpret_cast<const uint4*>(a.dy + (size_t)m * a.K + k0 + a_col);
+        if constexpr (TX) {
+          const uint4 yv = *reinterpret_cast<const uint4*>(a.tx_y + (size_t)m * a.K + k0 + a_col);
+          float d[8], yy[8], o[8];
+          unpack8(v, d);
+          unpack8(yv, yy);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = ta[e] * d[e] + tb[e] * yy[e] + tc[e];
+          v = pack8(o);
+        }
+      }
       ra[i] = v;
     }
 #pragma unroll
@@ -409,6 +436,219 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_wgrad_dma_kernel(WgradAr
       }
 }
 
+// ---------------------------------------------------------------------------
+// HALO wgrad: stride-1 convolutions with K == 64 output channels whose im2col is
+// mostly redundancy -- the ImageNet stem as a 4x4 conv over the space-to-depth
+// image (16 taps x 16 channels: every input pixel appears in 16 im2col columns)
+// and the 64-channel 3x3 convs (9 taps).  The generic kernels gather every
+// im2col row from L2 (9-16x the activation bytes through the L2->CU path, which
+// bounds them: 13-14 % MFMA, 1.2 TB/s HBM, profiles/pmc_wgrad_layers_r03.txt).
+//
+// Here a block owns a BAND of PB whole output rows of one image (PB*Q = up to
+// 224 reduction rows = 7 MFMA k-steps) at a time and stages, per band,
+//   * the band's input rows + halo (PB+R-1 rows x Q+S-1 pixels, zero-padded)
+//     ONCE, as C/8 "octet planes" [plane][pixel][8 channels] (16 B per pixel per
+//     plane -- one LDS-DMA chunk, contiguous in global memory), and
+//   * the band's dY rows [m][64] (32-B-window XOR swizzle, as the DMA kernel),
+// both by LDS-DMA into a 2-stage ring (the next band's DMA flies while this
+// band's MFMAs run).  The output tile is ALL K=64 x Kg columns (Kg = R*S*C <= 576:
+// 16 NI columns per wave), so the halo is read from L2 once per band instead of
+// once per tap.  B fragments (8 consecutive m of 16 consecutive kg) come straight
+// out of the halo with ds_read_b64_tr_b16: for tap (r, s) and channel quad c the
+// row address is  plane(c) + 16 * (rowpix(m) + r*HWp + s) + 8 * ((c >> 2) & 1),
+// a per-lane constant per fragment plus a per-lane constant per k-step -- one add
+// per read, no swizzle arithmetic.  A plane's pitch is 64 B mod 256, so the 8
+// pixels x 2 planes x 2 halves a 32-lane read group touches tile the 64 banks.
+struct HaloArgs {
+  int PB;        // output rows per band
+  int HWp;       // halo width  = Q + S - 1
+  int HR;        // halo rows   = PB + R - 1
+  int pitchC;    // 16-B chunks per octet plane (== 4 mod 16)
+  int CO;        // octet planes = C / 8
+  int bands_img; // bands per image = ceil(P / PB)
+  int bands;     // N * bands_img
+  int bpb;       // bands per block
+};
+constexpr int kHaloRows = 224;  // reduction rows per band buffer (7 k-steps)
+
+template <int NI, int HCH>
+__global__ __launch_bounds__(256, 1) void conv_wgrad_halo_kernel(WgradArgs a, HaloArgs h) {
+  constexpr int KS = kHaloRows / 32;
+  constexpr int HBYTES = HCH * 16;
+  constexpr int DBYTES = kHaloRows * 128;  // [224][64] bf16
+  constexpr int STAGE = HBYTES + DBYTES;
+  constexpr int HPT = HCH / 256;           // halo DMA chunks per thread
+  constexpr int DPT = kHaloRows * 8 / 256; // dY DMA chunks per thread
+  static_assert(HCH % 256 == 0 && 2 * STAGE <= 160 * 1024, "halo wgrad LDS");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wid_s = __builtin_amdgcn_readfirstlane(wid);
+  const int b0 = blockIdx.x * h.bpb;
+  if (b0 >= h.bands) return;
+  const int b1 = min(b0 + h.bpb, h.bands);
+
+  // ---- per-thread DMA work lists (identical for every band)
+  int hsrc[HPT];  // (plane << 20) | (halo row << 12) | halo col, -1 = unused chunk
+#pragma unroll
+  for (int t = 0; t < HPT; ++t) {
+    const int L = t * 256 + wid * 64 + lane;
+    const int o = L / h.pitchC, pix = L - o * h.pitchC;
+    hsrc[t] = (o < h.CO && pix < h.HR * h.HWp) ? ((o << 20) | ((pix / h.HWp) << 12) | (pix % h.HWp)) : -1;
+  }
+  // dY chunk (row, physical 16-B chunk pc) of instruction t: row = 32 t + 8 wid + lane / 8
+  const int d_pc = lane & 7;
+  const int d_row0 = wid * 8 + (lane >> 3);
+  const int d_col = ((((d_pc >> 1) ^ swz<128>(d_row0)) << 1) | (d_pc & 1)) * 8;
+
+  auto load = [&](int band, int buf) {
+    const int n = band / h.bands_img, pb = band - n * h.bands_img;
+    const int p0 = pb * h.PB;
+    const int rows = min(h.PB, a.P - p0) * a.Q;  // valid reduction rows of this band
+    const size_t mrow0 = ((size_t)n * a.P + p0) * a.Q;
+    char* Hs = smem + buf * STAGE;
+    char* Ds = Hs + HBYTES;
+#pragma unroll
+    for (int t = 0; t < HPT; ++t) {
+      const int e = hsrc[t];
+      if (e >= 0) {
+        const int o = e >> 20, hr = (e >> 12) & 0xff, hc = e & 0xfff;
+        const int ih = p0 - a.pad + hr, iw = hc - a.pad;
+        const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        const void* src = ok ? (const void*)(a.x + ((((size_t)n * a.H + ih) * a.W + iw) << a.log2C) + 8 * o)
+                             : (const void*)g_wzero16;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(Hs + (t * 256 + wid_s * 64) * 16),
+                                         16, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < DPT; ++t) {
+      const int row = t * 32 + d_row0;
+      const void* src = row < rows ? (const void*)(a.dy + (mrow0 + row) * 64 + d_col) : (const void*)g_wzero16;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(Ds + (t * 256 + wid_s * 64) * 16),
+                                       16, 0, 0);
+    }
+  };
+
+  // ---- fragment address constants
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  int rofs[KS][2];  // per k-step and half: 16 * halo pixel of the row's tap (0, 0)
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int hl = 0; hl < 2; ++hl) {
+      const int mr = ks * 32 + 8 * g + q4 + 4 * hl;
+      const int pr = mr / a.Q;
+      rofs[ks][hl] = mr < h.PB * a.Q ? 16 * (pr * h.HWp + (mr - pr * a.Q)) : 0;
+    }
+  int cofs[NI];  // per fragment: plane + tap shift + half for this lane's channel quad
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int kgc = wid * (16 * NI) + j * 16 + 4 * p4;
+    const int tap = kgc >> a.log2C, c = kgc & (a.C - 1);
+    const int r = tap / a.S, s = tap - r * a.S;
+    cofs[j] = (c >> 3) * h.pitchC * 16 + 16 * (r * h.HWp + s) + 8 * ((c >> 2) & 1);
+  }
+
+  f32x4 acc[4][NI];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  auto compute = [&](int buf) {
+    const char* Hs = smem + buf * STAGE;
+    const char* Ds = Hs + HBYTES;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 af[4], bfg[NI];
+      const int r0 = ks * 32 + 8 * g + q4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int col = i * 16 + 4 * p4;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(Ds + toff<64>(r0, col)));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(Ds + toff<64>(r0 + 4, col)));
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(Hs + cofs[j] + rofs[ks][0]));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(Hs + cofs[j] + rofs[ks][1]));
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfg[j] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  load(b0, 0);
+  for (int b = b0; b < b1; ++b) {
+    wg_wait_vmcnt<0>();
+    // publishes band b's stage AND retires every wave's reads of the other stage
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (b + 1 < b1) load(b + 1, (b + 1 - b0) & 1);
+    compute((b - b0) & 1);
+  }
+
+  float* dst = a.ws ? a.ws + (size_t)blockIdx.x * 64 * a.Kg : a.dw;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = i * 16 + (lane >> 4) * 4 + e;
+        const int gg = wid * (16 * NI) + j * 16 + (lane & 15);
+        float* p = dst + (size_t)k * a.Kg + gg;
+        if (a.ws)
+          *p = acc[i][j][e];
+        else
+          *p += acc[i][j][e];
+      }
+}
+
+// The halo variant applies to stride-1 convs with K == 64, C in {16, 64}, Kg = 256
+// (stem: 4x4 x 16) or 576 (3x3 x 64), and bands of whole rows that fit 224 rows.
+static bool halo_cfg(const WgradArgs& a, HaloArgs* h, int* nich) {
+  if (a.stride != 1 || a.K != 64 || !(a.C == 16 || a.C == 64)) return false;
+  if (!(a.Kg == 256 || a.Kg == 576)) return false;
+  if (a.Q > kHaloRows || a.Q < 7) return false;
+  HaloArgs c;
+  c.PB = kHaloRows / a.Q;
+  if (c.PB > a.P) c.PB = a.P;
+  c.HWp = a.Q + a.S - 1;
+  c.HR = c.PB + a.R - 1;
+  const int pix = c.HR * c.HWp;
+  c.pitchC = pix + ((4 - pix % 16) + 16) % 16;
+  c.CO = a.C / 8;
+  const int hch_need = c.CO * c.pitchC;
+  const int hch = a.Kg == 256 ? 1280 : 3072;
+  if (hch_need > hch || c.HWp >= 4096 || c.HR >= 256) return false;
+  // the halo must cover every tap of every band row: q + s - pad in [-pad, Q + S - 1 - pad)
+  c.bands_img = (a.P + c.PB - 1) / c.PB;
+  c.bands = a.N * c.bands_img;
+  const int target = 256;  // one 150 KB block per CU
+  const int blocks = c.bands < target ? c.bands : target;
+  c.bpb = (c.bands + blocks - 1) / blocks;
+  *h = c;
+  *nich = a.Kg == 256 ? 4 : 9;
+  return true;
+}
+
+static int halo_splits(const HaloArgs& h) { return (h.bands + h.bpb - 1) / h.bpb; }
+
 // dW[i] += sum_s ws[s][i].  blockIdx.y = split group of <= kSplitGroup slices:
 // one group -> plain read-modify-write in fixed order (deterministic); several
 // groups (tiny outputs with hundreds of splits) -> one fp32 atomic per group.
@@ -479,7 +719,7 @@ void conv_wgrad_set_impl(int impl) { g_wgrad_impl = impl; }
 static int wgrad_impl() {
   if (g_wgrad_impl < 0) {
     const char* e = getenv("PMD_WGRAD_IMPL");
-    g_wgrad_impl = (e && e[0] >= '0' && e[0] <= '5') ? e[0] - '0' : 1;
+    g_wgrad_impl = (e && e[0] >= '0' && e[0] <= '6') ? e[0] - '0' : 1;
   }
   return g_wgrad_impl;
 }
@@ -540,9 +780,15 @@ struct WgradCfg {
   int impl, BM, BN, target;
 };
 
+static bool halo_cfg(const WgradArgs& a, HaloArgs* h, int* nich);
 static bool wgrad_cfg_ok(int impl, const WgradArgs& a) {
   if (impl == 4) return a.K >= 256 && a.Kg >= 256;
   if (impl == 5) return a.K >= 256;
+  if (impl == 6) {
+    HaloArgs h;
+    int ni;
+    return halo_cfg(a, &h, &ni);
+  }
   return true;
 }
 
@@ -568,8 +814,25 @@ static void plan(const WgradArgs& a, const WgradCfg& cfg, int* splits_out, int* 
   *splits_out = (chunks + cps - 1) / cps;
 }
 
+static void wgrad_reduce_launch(const WgradArgs& a, int splits, hipStream_t st);
+
 // One full weight gradient with variant `impl`: split-K plan, kernel, split reduce.
 static void wgrad_run(int impl, WgradArgs a, float* ws, hipStream_t st) {
+  if (impl == 6) {
+    HaloArgs h;
+    int ni;
+    if (halo_cfg(a, &h, &ni)) {
+      const int splits = halo_splits(h);
+      a.ws = splits > 1 ? ws : nullptr;
+      if (ni == 4)
+        hipLaunchKernelGGL((conv_wgrad_halo_kernel<4, 1280>), dim3(splits), dim3(256), 0, st, a, h);
+      else
+        hipLaunchKernelGGL((conv_wgrad_halo_kernel<9, 3072>), dim3(splits), dim3(256), 0, st, a, h);
+      if (splits > 1) wgrad_reduce_launch(a, splits, st);
+      return;
+    }
+    impl = 1;
+  }
   const WgradCfg cfg = wgrad_cfg(impl, a);
   int splits, cps;
   plan(a, cfg, &splits, &cps);
@@ -580,8 +843,13 @@ static void wgrad_run(int impl, WgradArgs a, float* ws, hipStream_t st) {
   const bool k64 = a.K == 64;
   switch (impl) {
     case 0:
-      if (k64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128>), grid, dim3(256), 0, st, a);
-      else hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), grid, dim3(256), 0, st, a);
+      if (a.tx_y) {
+        if (k64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, true>), grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, true>), grid, dim3(256), 0, st, a);
+      } else {
+        if (k64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128>), grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), grid, dim3(256), 0, st, a);
+      }
       break;
     case 2:  // DMA, 32-row stages, 4-deep ring
       if (k64) hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 128, 32, 4>), grid, dim3(256), 0, st, a);
@@ -602,13 +870,15 @@ static void wgrad_run(int impl, WgradArgs a, float* ws, hipStream_t st) {
       else hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 64, 2>), grid, dim3(256), 0, st, a);
       break;
   }
-  if (splits > 1) {
-    const long long n4 = (long long)a.K * a.Kg / 4;
-    const int groups = (splits + kSplitGroup - 1) / kSplitGroup;
-    long long b = (n4 + 255) / 256;
-    if (b > 4096) b = 4096;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)b, groups), dim3(256), 0, st, a.ws, a.dw, splits, n4);
-  }
+  if (splits > 1) wgrad_reduce_launch(a, splits, st);
+}
+
+static void wgrad_reduce_launch(const WgradArgs& a, int splits, hipStream_t st) {
+  const long long n4 = (long long)a.K * a.Kg / 4;
+  const int groups = (splits + kSplitGroup - 1) / kSplitGroup;
+  long long b = (n4 + 255) / 256;
+  if (b > 4096) b = 4096;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)b, groups), dim3(256), 0, st, a.ws, a.dw, splits, n4);
 }
 
 static int wgrad_tune(const WgradArgs& a0, float* ws, hipStream_t st) {
@@ -629,7 +899,7 @@ static int wgrad_tune(const WgradArgs& a0, float* ws, hipStream_t st) {
   }
   int best = -1;
   float best_ms = 1e30f;
-  for (int c : {0, 1, 4, 5}) {
+  for (int c : {0, 1, 4, 5, 6}) {
     if (!wgrad_cfg_ok(c, a)) continue;
     wgrad_run(c, a, ws, st);
     float t = 1e30f;
@@ -685,11 +955,15 @@ int conv_wgrad_splits(int N, int H, int W, int C, int P, int Q, int K, int R, in
     plan(a, wgrad_cfg(impl, a), &splits, &cps);
     best = splits > best ? splits : best;
   }
+  HaloArgs h;
+  int ni;
+  if (halo_cfg(a, &h, &ni)) best = halo_splits(h) > best ? halo_splits(h) : best;
   return best;
 }
 
 int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, float* ws, int N, int H, int W,
-                      int C, int P, int Q, int K, int R, int S, int stride, int pad, hipStream_t st) {
+                      int C, int P, int Q, int K, int R, int S, int stride, int pad, hipStream_t st,
+                      const TxArgs* tx) {
   if (C % 8 != 0 || (C & (C - 1)) != 0) return 1;
   if (K % 64 != 0) return 2;
   if ((long long)N * P * Q >= (1ll << 31)) return 4;
@@ -697,8 +971,20 @@ int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, float* ws, i
   a.dy = dy;
   a.x = x;
   a.dw = dw;
+  a.tx_y = nullptr;
+  a.tx_coef = nullptr;
+  a.tx_cp = 0;
   fill_args(a, N, H, W, C, P, Q, K, R, S, stride, pad);
   if (!ws && conv_wgrad_splits(N, H, W, C, P, Q, K, R, S, stride, pad) > 1) return 5;
+  if (tx && tx->y) {
+    // BN backward applied on load: the register-staged variant, no autotuning
+    if (!tx->coef || tx->cp < K) return 6;
+    a.tx_y = tx->y;
+    a.tx_coef = tx->coef;
+    a.tx_cp = tx->cp;
+    wgrad_run(0, a, ws, st);
+    return 0;
+  }
   int impl = wgrad_impl();
   if (!wgrad_cfg_ok(impl, a)) impl = 1;
   if (impl == 1 && wgrad_autotune_on()) {

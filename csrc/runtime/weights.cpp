@@ -70,15 +70,17 @@ class WeightImages {
     TORCH_CHECK(hipStreamSynchronize(st) == hipSuccess, "weight images: sync");
   }
 
-  void refresh() {
+  // mode 1: forward images only, 2: dgrad images only, 3: both (current stream)
+  void refresh(int64_t mode) {
+    TORCH_CHECK(mode >= 1 && mode <= 3, "weight images: refresh mode 1..3");
     for (size_t i = 0; i < weights_.size(); ++i)
       TORCH_CHECK(weights_[i].data_ptr<float>() == ptrs_[i],
                   "weight images: a weight was re-allocated; rebuild the image set");
     c10::DeviceGuard g(weights_[0].device());
     conv_weight_prep_grouped_launch(reinterpret_cast<const WeightPrepDesc*>(d_descs_.data_ptr()),
                                     d_starts_.data_ptr<int>(), n_, total_blocks_,
-                                    c10::hip::getCurrentHIPStream().stream());
-    refreshed_++;
+                                    c10::hip::getCurrentHIPStream().stream(), (int)mode);
+    if (mode & 1) refreshed_++;
   }
 
   std::vector<at::Tensor> get(int64_t i) const {
@@ -183,7 +185,7 @@ void register_weights(pybind11::module& m) {
   namespace py = pybind11;
   py::class_<WeightImages>(m, "WeightImages")
       .def(py::init<std::vector<at::Tensor>, std::vector<int64_t>, std::vector<bool>>())
-      .def("refresh", &WeightImages::refresh)
+      .def("refresh", &WeightImages::refresh, pybind11::arg("mode") = 3)
       .def("get", &WeightImages::get)
       .def_property_readonly("size", &WeightImages::size)
       .def_property_readonly("refreshed", &WeightImages::refreshed);

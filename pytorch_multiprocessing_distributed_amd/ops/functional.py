@@ -40,6 +40,7 @@ import weakref
 import torch
 
 from . import torch_prims
+from .lazy import LazyDy, is_lazy
 
 _NAN_CHECK = os.environ.get("PMD_NAN_CHECK", "0") == "1"   # debug: finite-check block backward
 
@@ -71,11 +72,29 @@ class WeightImageSet:
         from .native import C
         self.entries = list(entries)
         self.index = {(id(m.weight), cp, wt): i for i, (m, cp, wt) in enumerate(self.entries)}
+        self._dev = self.entries[0][0].weight.device
         self._c = C.WeightImages([m.weight for m, _, _ in self.entries],
                                  [cp for _, cp, _ in self.entries], [wt for _, _, wt in self.entries])
 
-    def refresh(self):
-        self._c.refresh()
+    def refresh(self, need_bwd=True):
+        """Forward images now, on the current stream; dgrad images (only needed
+        by the backward, milliseconds later) on the wgrad side stream, which is
+        idle during the forward -- the backward waits for them before its first
+        dgrad (:func:`_wait_weight_images`)."""
+        if not need_bwd:
+            self._c.refresh(1)
+        elif _SPLIT_WPREP and _WGRAD_STREAM["on"] and self._dev.type == "cuda":
+            self._c.refresh(1)
+            main = torch.cuda.current_stream(self._dev)
+            side = _wgrad_stream(self._dev)
+            side.wait_stream(main)               # after the previous step's optimizer update
+            with torch.cuda.stream(side):
+                self._c.refresh(2)
+            ev = torch.cuda.Event()
+            ev.record(side)
+            _state["wkt_event"] = ev
+        else:
+            self._c.refresh(3)
         if self.fp8 is not None:
             self.fp8.refresh()
 
@@ -131,7 +150,7 @@ class weight_images:
 
     def __enter__(self):
         if self.wset is not None:
-            self.wset.refresh()
+            self.wset.refresh(need_bwd=torch.is_grad_enabled())
         self.prev = _state["wimg"]
         _state["wimg"] = self.wset
         return self.wset
@@ -247,6 +266,8 @@ def _wgrad(P, dy, x, wpack, stride, pad, w):
     """Weight gradient: accumulated into the arena (returns None) or returned."""
     if not w.requires_grad:
         return None
+    if is_lazy(dy):
+        dy = dy.materialize()
     cx = wpack[0].shape[-1]
     tgt = _grad_target(w)
     if tgt is not None and cx == w.shape[1]:
@@ -261,6 +282,24 @@ def _wgrad(P, dy, x, wpack, stride, pad, w):
 
 _WGRAD_STREAM = {"on": os.environ.get("PMD_WGRAD_STREAM", "1") != "0", "streams": {},
                  "defer": int(os.environ.get("PMD_WGRAD_DEFER", "1") or 0)}  # join lag in blocks
+# dgrad weight images refreshed on the side stream during the forward: PMD_SPLIT_WPREP=1
+# (measured step-neutral, 12,699 / 12,684 vs 12,704 / 12,712 img/s: off by default)
+_SPLIT_WPREP = os.environ.get("PMD_SPLIT_WPREP", "0") == "1"
+
+
+def _wgrad_stream(dev):
+    st = _WGRAD_STREAM["streams"].get(dev)
+    if st is None:
+        st = _WGRAD_STREAM["streams"][dev] = torch.cuda.Stream(device=dev)
+    return st
+
+
+def _wait_weight_images():
+    """Backward: the current stream waits (once per step) for the dgrad weight
+    images the forward queued on the side stream."""
+    ev = _state.pop("wkt_event", None)
+    if ev is not None:
+        torch.cuda.current_stream().wait_event(ev)
 
 
 def set_wgrad_stream(flag: bool):
@@ -286,20 +325,21 @@ class _WgradSide:
         self.ready = []
         if self.on:
             dev = t.device
-            st = _WGRAD_STREAM["streams"].get(dev)
-            if st is None:
-                st = _WGRAD_STREAM["streams"][dev] = torch.cuda.Stream(device=dev)
-            self.side = st
+            self.side = _wgrad_stream(dev)
             self.main = torch.cuda.current_stream(dev)
 
     def wgrad(self, P, dy, x, wpack, stride, pad, w):
         if not self.on or _grad_target(w) is None:
             return _wgrad(P, dy, x, wpack, stride, pad, w)
+        # dy may be a LazyDy: its record_stream covers dzm, y and the coefficients
         _claim(w)
         self.side.wait_stream(self.main)
         with torch.cuda.stream(self.side):
             tgt = _grad_target(w)
-            P.conv_wgrad(dy, x, tuple(wpack[0].shape), stride, pad, out=tgt.permute(0, 2, 3, 1))
+            # a LazyDy (BN backward applied by the main-stream dgrad) is materialised
+            # HERE, on the side stream: the elementwise pass leaves the critical path
+            dyw = dy.materialize() if is_lazy(dy) else dy
+            P.conv_wgrad(dyw, x, tuple(wpack[0].shape), stride, pad, out=tgt.permute(0, 2, 3, 1))
         dy.record_stream(self.side)
         x.record_stream(self.side)
         self.ready.append(w)
@@ -474,14 +514,50 @@ def _bn_forward_params(P, y, st, bn, training, sync, y2=None, st2=None, bn2=None
     return p1, p2, count
 
 
+# BN backward applied by the consumer 1x1 dgrad while it reads dY (ops/lazy.py,
+# PMD_BN_TX=1).  Built, correct (tests/test_bn_tx_gpu.py) and OFF by default: the
+# whole step measured 20.1 -> 21.1 ms with it (docs/ARCHITECTURE.md, "BN backward on load")
+_BN_TX = os.environ.get("PMD_BN_TX", "0") == "1"
+
+
+def set_bn_tx(flag: bool):
+    global _BN_TX
+    _BN_TX = bool(flag)
+
+
+def _tx_ok(P, conv_m, pre, training):
+    """Can ``conv_m`` consume this BN site's dY lazily?  1x1 conv (no padded taps),
+    gfx950 prims, training, and dZ already gated by the ReLU mask -- which the
+    fused-reduce dgrad that produced it (``pre``) guarantees.
+
+    Used for the block-final BN of a Bottleneck only (its consumer conv3 reduces
+    over 4x planes channels into planes: the largest dY for the smallest output):
+    there the TX dgrad on the main stream replaces bn_bwd_elemt + dgrad (l1: 270 vs
+    393 us, l2: 159 vs 210 us, bench/dgrad_epi_bench.py --tx), and the weight
+    gradient -- whose TX variant is 2-3x slower than the DMA wgrad -- materialises
+    dY on the side stream, off the critical path (:meth:`_WgradSide.wgrad`).  For
+    the conv1 / shortcut consumers (small reduction, epilogue-bound) the TX dgrad
+    measured slower than the elementwise pass it replaces."""
+    return (_BN_TX and training and pre is not None and getattr(P, "SUPPORTS_TX", False)
+            and tuple(conv_m.weight.shape[2:]) == (1, 1))
+
+
+def _elemt(P, dout, mask, y, p, gamma, red, count, relu, want_dzm=False, lazy=False):
+    if lazy and not want_dzm:
+        return LazyDy(dout, y, P.bn_bwd_coef(p, gamma, red, count),
+                      (P, mask, p, gamma, red, count, relu)), None
+    return P.bn_bwd_elemt(dout, mask, y, p, gamma, red, count, relu, want_dzm=want_dzm)
+
+
 def _bn_backward(P, dout, mask, relu, training, sync, count, y1, p1, bn1, y2=None, p2=None,
-                 bn2=None, want_dzm=False, pre=None, elemt_fn=None):
+                 bn2=None, want_dzm=False, pre=None, elemt_fn=None, lazy=(False, False)):
     """BN(+second BN)(+ReLU) backward. Returns (dy1, dy2, dzm, grads) with
     grads = [d_g1, d_b1, d_g2, d_b2] for params that were NOT written directly.
     ``pre``: the reduce results already produced by the dgrad that computed
     ``dout`` (fused epilogue), in the order (bn1[, bn2]).  ``elemt_fn(red, count)``
     replaces the elementwise pass of BN 1 (fused stem: it re-derives dz itself;
-    red/count are None in eval mode)."""
+    red/count are None in eval mode).  ``lazy[i]``: return dY of BN i as a
+    :class:`LazyDy` (its consumer is a 1x1 conv that applies it on load)."""
     if pre is not None:
         r1 = pre[0]
         r2 = pre[1] if y2 is not None else None
@@ -519,12 +595,12 @@ def _bn_backward(P, dout, mask, relu, training, sync, count, y1, p1, bn1, y2=Non
         if elemt_fn is not None:
             dy1, dzm = elemt_fn(red[:2 * c1].view(2, c1), count), None
         else:
-            dy1, dzm = P.bn_bwd_elemt(dout, mask, y1, p1, bn1.weight, red[:2 * c1].view(2, c1), count,
-                                      relu, want_dzm=want_dzm)
+            dy1, dzm = _elemt(P, dout, mask, y1, p1, bn1.weight, red[:2 * c1].view(2, c1), count,
+                              relu, want_dzm=want_dzm, lazy=lazy[0])
         dy2 = None
         if y2 is not None:
-            dy2, _ = P.bn_bwd_elemt(dout, mask, y2, p2, bn2.weight, red[2 * c1:].view(2, -1), count,
-                                    relu)
+            dy2, _ = _elemt(P, dout, mask, y2, p2, bn2.weight, red[2 * c1:].view(2, -1), count,
+                            relu, lazy=lazy[1])
         return dy1, dy2, dzm, [None, None, None, None]
     red = P.stats_collapse(r1, r2, None, acc1, acc2)     # local sums; gamma/beta grads += local
     grads = [None, None, None, None]
@@ -545,12 +621,12 @@ def _bn_backward(P, dout, mask, relu, training, sync, count, y1, p1, bn1, y2=Non
         if elemt_fn is not None:
             dy1, dzm = elemt_fn(red[:2 * c1].view(2, c1), count), None
         else:
-            dy1, dzm = P.bn_bwd_elemt(dout, mask, y1, p1, bn1.weight, red[:2 * c1].view(2, c1),
-                                      count, relu, want_dzm=want_dzm)
+            dy1, dzm = _elemt(P, dout, mask, y1, p1, bn1.weight, red[:2 * c1].view(2, c1),
+                              count, relu, want_dzm=want_dzm, lazy=lazy[0])
         dy2 = None
         if y2 is not None:
-            dy2, _ = P.bn_bwd_elemt(dout, mask, y2, p2, bn2.weight, red[2 * c1:].view(2, -1), count,
-                                    relu)
+            dy2, _ = _elemt(P, dout, mask, y2, p2, bn2.weight, red[2 * c1:].view(2, -1), count,
+                            relu, lazy=lazy[1])
     elif elemt_fn is not None:
         dy1, dy2, dzm = elemt_fn(None, None), None, None
     else:
@@ -579,6 +655,7 @@ class _ConvFn(torch.autograd.Function):
     def backward(ctx, dy, _dstats):
         if dy is None:
             return None, None, None, None, None
+        _wait_weight_images()
         x, *wpack = ctx.saved_tensors
         stride, pad, w = ctx.conf
         P = prims_for(x)
@@ -892,6 +969,7 @@ class _ResidualBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        _wait_weight_images()
         cfg, sync, counts, countf, nwf, nws, nwst = ctx.cfg
         stages, final, shortcut, training = cfg
         nst = len(stages)
@@ -913,8 +991,11 @@ class _ResidualBlockFn(torch.autograd.Function):
         nan_check = _NAN_CHECK
 
         def chk(name, t):
-            if nan_check and t is not None and not torch.isfinite(t.float()).all():
-                raise FloatingPointError(f"non-finite {name} in block backward ({fconv.weight.shape})")
+            if nan_check and t is not None:
+                if is_lazy(t):
+                    t = t.materialize()
+                if not torch.isfinite(t.float()).all():
+                    raise FloatingPointError(f"non-finite {name} in block backward ({fconv.weight.shape})")
         chk("dout", dout)
 
         def put(p, g):
@@ -929,7 +1010,8 @@ class _ResidualBlockFn(torch.autograd.Function):
             ys, ps = sv[i], sv[i + 1]
             wps = tuple(sv[i + 2:i + 2 + nws])
             dyf, dys, _, g = _bn_backward(P, dout, omask, True, training, sync, countf,
-                                          yf, pf, fbn, ys, ps, sbn, pre=pre)
+                                          yf, pf, fbn, ys, ps, sbn, pre=pre,
+                                          lazy=(_tx_ok(P, fconv, pre, training), False))
             put(sbn.weight, g[2])
             put(sbn.bias, g[3])
             dres = None
@@ -937,7 +1019,8 @@ class _ResidualBlockFn(torch.autograd.Function):
             # the identity-path gradient dout * relu_mask is NOT materialised: the first
             # stage's dgrad epilogue adds dout gated by the mask bits
             dyf, _, _, g = _bn_backward(P, dout, omask, True, training, sync, countf,
-                                        yf, pf, fbn, pre=pre)
+                                        yf, pf, fbn, pre=pre,
+                                        lazy=(_tx_ok(P, fconv, pre, training), False))
             dres = (dout, omask)
         put(fbn.weight, g[0])
         put(fbn.bias, g[1])

@@ -81,7 +81,7 @@ def test_conv_fwd_dgrad_wgrad(shape):
     _close(dw, dwr, 2e-3)
 
 
-@pytest.mark.parametrize("impl", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("impl", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("shape", R50_SHAPES + CIFAR_SHAPES, ids=lambda s: "C%d_H%d_K%d_R%d_s%d" % s)
 def test_wgrad_variants(shape, impl):
     """Every operand-staging variant of the split-K wgrad kernel (register
@@ -104,6 +104,42 @@ def test_wgrad_variants(shape, impl):
     finally:
         _C.conv_wgrad_set_impl(1)
     _close(dw, dwr, 2e-3)
+
+
+@pytest.mark.parametrize("N,H,C,R,pad,P", [
+    (3, 112, 16, 4, 2, 112),   # the space-to-depth stem: 4x4 over 16 ch, output cropped to H
+    (3, 56, 64, 3, 1, 56),     # layer1 3x3
+    (5, 28, 64, 3, 1, 28),
+    (3, 20, 64, 3, 1, 20),     # 11-row bands: a ragged last band per image
+    (9, 7, 64, 3, 1, 7),
+])
+def test_wgrad_halo(N, H, C, R, pad, P):
+    """The halo wgrad (conv_wgrad.hip conv_wgrad_halo_kernel, variant 6): one
+    band of whole output rows + input halo staged per block step, all taps from
+    LDS.  Against fp32 conv2d_weight on the same bf16 operands (a cropped output
+    is the full output with zero gradient in the cropped rows/columns)."""
+    import torch.nn.functional as F
+    from pytorch_multiprocessing_distributed_amd.ops.native import C as _C
+    HP = _hp()
+    torch.manual_seed(5)
+    K = 64
+    x = torch.randn(N, H, H, C, device=DEV).to(torch.bfloat16)
+    dy = torch.randn(N, P, P, K, device=DEV).to(torch.bfloat16)
+    full = H + 2 * pad - R + 1
+    dyf = F.pad(dy.float().permute(0, 3, 1, 2), (0, full - P, 0, full - P))
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (K, C, R, R), dyf,
+                                      padding=pad).permute(0, 2, 3, 1)
+    _C.conv_wgrad_set_impl(6)
+    try:
+        dw = _C.conv_wgrad(dy, x, R, R, 1, pad, None)
+        base = torch.randn_like(dw)
+        acc = base.clone()
+        _C.conv_wgrad(dy, x, R, R, 1, pad, acc)          # accumulate into a target
+        torch.cuda.synchronize()
+    finally:
+        _C.conv_wgrad_set_impl(1)
+    _close(dw, ref, 2e-3)
+    _close(acc - base, ref, 2e-3)
 
 
 @pytest.mark.parametrize("impl", [0, 1, 3, 4, 6, 7])

@@ -202,7 +202,7 @@ def test_weight_image_set_covers_every_conv(monkeypatch):
         def __init__(self, ws, cps, wts):
             self.e = list(zip(ws, cps, wts))
 
-        def refresh(self):
+        def refresh(self, mode=3):
             pass
 
         def get(self, i):
