@@ -553,7 +553,10 @@ def _dgrad_fused_bn_reduce(shape, two):
     _, mask = HP.bn_apply(sets[0][0], sets[0][1], relu=True)
     dx_f, reds = HP.conv_dgrad(dy, wp, tuple(x.shape), st, pad, add, bnred=(mask, sets))
     dx = HP.conv_dgrad(dy, wp, tuple(x.shape), st, pad, add)
-    assert torch.equal(dx_f, dx)
+    # the fused-reduce dgrad stores its output (a BN site's dz) already gated by that
+    # site's ReLU mask (bit k of byte i == element 8i+k), the form every consumer reads
+    bits = (mask.view(-1, 1).int() >> torch.arange(8, device=DEV).view(1, 8)) & 1
+    assert torch.equal(dx_f, dx * bits.view(dx.shape).to(dx.dtype))
     for (yb, p), r in zip(sets, reds):
         got = HP.stats_collapse(r).view(2, C)
         want = HP.stats_collapse(HP.bn_bwd_reduce(dx, mask, yb, p, True)).view(2, C)  # unfused
