@@ -364,6 +364,39 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int64_t R, int64_t S, int64_t stride, int
   return dw;
 }
 
+// FP8 weight gradient: dyq e5m2 [N,P,Q,K] (scale sdy) x xq e4m3 [N,H,W,C] (scale sx);
+// dW / (sdy * sx) is ADDED to out ([K,R,S,C] fp32) when given
+Tensor conv_wgrad_fp8(Tensor dyq, Tensor xq, Tensor sdy, Tensor sx, int64_t R, int64_t S, int64_t stride,
+                      int64_t pad, c10::optional<Tensor> out) {
+  CHECK_DEV(dyq); CHECK_CONT(dyq); CHECK_DEV(xq); CHECK_CONT(xq);
+  TORCH_CHECK(dyq.scalar_type() == torch::kUInt8 && xq.scalar_type() == torch::kUInt8,
+              "conv_wgrad_fp8: e5m2 / e4m3 operands as uint8");
+  CHECK_F32(sdy); CHECK_F32(sx);
+  const int N = xq.size(0), H = xq.size(1), W = xq.size(2), C = xq.size(3);
+  const int P = dyq.size(1), Q = dyq.size(2), K = dyq.size(3);
+  TORCH_CHECK(dyq.size(0) == N, "batch mismatch");
+  TORCH_CHECK((H + 2 * pad - R) / stride + 1 >= P && (W + 2 * pad - S) / stride + 1 >= Q && P >= 1 && Q >= 1,
+              "wgrad spatial mismatch");
+  c10::DeviceGuard g(xq.device());
+  Tensor dw;
+  if (out && out->defined()) {
+    TORCH_CHECK(out->sizes() == torch::IntArrayRef({K, R, S, C}), "wgrad out shape");
+    opt_f32(out, "wgrad out");
+    dw = *out;
+  } else {
+    dw = pmd_zeros({K, R, S, C}, xq.options().dtype(torch::kFloat32));
+  }
+  const int splits = pmd::conv_wgrad_fp8_splits(N, H, W, C, P, Q, K, (int)R, (int)S, (int)stride, (int)pad);
+  Tensor ws;
+  if (splits > 1) ws = torch::empty({splits, K, R * S * C}, xq.options().dtype(torch::kFloat32));
+  CHECK_RC(pmd::conv_wgrad_fp8_launch(dyq.data_ptr<uint8_t>(), xq.data_ptr<uint8_t>(), sdy.data_ptr<float>(),
+                                      sx.data_ptr<float>(), dw.data_ptr<float>(),
+                                      splits > 1 ? ws.data_ptr<float>() : nullptr, N, H, W, C, P, Q, K, (int)R,
+                                      (int)S, (int)stride, (int)pad, cur_stream()),
+           "conv_wgrad_fp8");
+  return dw;
+}
+
 // -------------------------------------------------------------------- BN
 Tensor bn_finalize(c10::optional<Tensor> sums, c10::optional<Tensor> count, Tensor gamma, Tensor beta, double eps,
                    c10::optional<Tensor> rm, c10::optional<Tensor> rv, double momentum,
@@ -447,7 +480,7 @@ Tensor stats_finalize_local(Tensor slots, double count, Tensor gamma, Tensor bet
 // q8_scale/q8_amax (optional): also return an e4m3 copy of the output (fp8 conv input)
 std::vector<Tensor> bn_apply(Tensor y1, Tensor p1, c10::optional<Tensor> res, c10::optional<Tensor> y2,
                              c10::optional<Tensor> p2, bool relu, bool want_mask,
-                             c10::optional<Tensor> q8_scale, c10::optional<Tensor> q8_amax) {
+                             c10::optional<Tensor> q8_scale, c10::optional<Tensor> q8_amax, bool q8_only) {
   CHECK_DEV(y1); CHECK_BF16(y1); CHECK_CONT(y1);
   const int C = y1.size(-1);
   const long long M = y1.numel() / C;
@@ -469,11 +502,13 @@ std::vector<Tensor> bn_apply(Tensor y1, Tensor p1, c10::optional<Tensor> res, c1
     r = bfp(*res);
   }
   c10::DeviceGuard g(y1.device());
-  Tensor out = torch::empty_like(y1);
+  const bool q8 = q8_scale && q8_scale->defined();
+  TORCH_CHECK(!q8_only || q8, "q8_only needs the fp8 output");
+  // q8_only: the e4m3 copy is the only activation written (returned out is None)
+  Tensor out = q8_only ? Tensor() : torch::empty_like(y1);
   Tensor mask;
   const bool wm = relu && want_mask;
   if (wm) mask = torch::empty({M * (C / 8)}, y1.options().dtype(torch::kUInt8));
-  const bool q8 = q8_scale && q8_scale->defined();
   Tensor q;
   if (q8) {
     TORCH_CHECK(q8_amax && q8_amax->defined(), "fp8 output needs an amax accumulator");
@@ -481,7 +516,7 @@ std::vector<Tensor> bn_apply(Tensor y1, Tensor p1, c10::optional<Tensor> res, c1
     TORCH_CHECK(q8_amax->numel() >= 64 && q8_amax->is_contiguous(), "amax must be [64] slots");
     q = torch::empty(y1.sizes(), y1.options().dtype(torch::kUInt8));
   }
-  const int rc = pmd::bn_apply_launch(bfp(y1), p1.data_ptr<float>(), r, pp2, bfp_mut(out),
+  const int rc = pmd::bn_apply_launch(bfp(y1), p1.data_ptr<float>(), r, pp2, q8_only ? nullptr : bfp_mut(out),
                                       wm ? mask.data_ptr<uint8_t>() : nullptr, M, C, mode, relu,
                                       q8 ? q.data_ptr<uint8_t>() : nullptr,
                                       q8 ? q8_scale->data_ptr<float>() : nullptr,
@@ -549,7 +584,8 @@ Tensor bn_bwd_coef(Tensor params, Tensor gamma, c10::optional<Tensor> red, c10::
 std::vector<Tensor> bn_bwd_elemt(Tensor dout, c10::optional<Tensor> mask, Tensor y, Tensor params,
                                  Tensor gamma, c10::optional<Tensor> red,
                                  c10::optional<Tensor> count, double count_h, bool relu,
-                                 bool want_dzm, bool eval_mode) {
+                                 bool want_dzm, bool eval_mode, c10::optional<Tensor> q8_scale,
+                                 c10::optional<Tensor> q8_amax) {
   CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONT(dout);
   const int C = dout.size(-1);
   const long long M = dout.numel() / C;
@@ -564,12 +600,25 @@ std::vector<Tensor> bn_bwd_elemt(Tensor dout, c10::optional<Tensor> mask, Tensor
     rr = red->contiguous();
     if (count && count->defined()) cc = count->contiguous();
   }
+  // q8: also the e5m2 copy of dy (scaled by q8_scale, amax into q8_amax) for the fp8 wgrad
+  const bool q8 = q8_scale && q8_scale->defined();
+  Tensor q;
+  if (q8) {
+    TORCH_CHECK(!want_dzm && !eval_mode, "e5m2 dY copy: training mode, no dzm");
+    TORCH_CHECK(q8_amax && q8_amax->defined() && q8_amax->numel() >= 64 && q8_amax->is_contiguous(),
+                "amax must be [64] slots");
+    CHECK_F32(*q8_scale); CHECK_F32(*q8_amax);
+    q = torch::empty(dout.sizes(), dout.options().dtype(torch::kUInt8));
+  }
   const int rc = pmd::bn_bwd_elemt_launch(
       bfp(dout), mask_ptr(mask, M * (C / 8), relu), eval_mode ? nullptr : bfp(y), params.data_ptr<float>(), gm.data_ptr<float>(),
       eval_mode ? nullptr : rr.data_ptr<float>(),
-      (eval_mode || !cc.defined()) ? nullptr : cc.data_ptr<float>(), (float)count_h, bfp_mut(dy), want_dzm ? bfp_mut(dzm) : nullptr, M, C, relu, eval_mode, cur_stream());
+      (eval_mode || !cc.defined()) ? nullptr : cc.data_ptr<float>(), (float)count_h, bfp_mut(dy), want_dzm ? bfp_mut(dzm) : nullptr, M, C, relu, eval_mode, cur_stream(),
+      q8 ? q.data_ptr<uint8_t>() : nullptr, q8 ? q8_scale->data_ptr<float>() : nullptr,
+      q8 ? q8_amax->data_ptr<float>() : nullptr);
   CHECK_RC(rc, "bn_bwd_elemt");
   if (want_dzm) return {dy, dzm};
+  if (q8) return {dy, q};
   return {dy};
 }
 
@@ -744,7 +793,7 @@ Tensor cifar_augment(Tensor data, Tensor idx, int64_t Cp, bool train, int64_t pa
 // ------------------------------------------------------------------ fp8 (e4m3)
 #define CHECK_U8(t) TORCH_CHECK((t).scalar_type() == torch::kUInt8, #t " must be uint8 (e4m3 bytes)")
 
-Tensor quant_bf16_fp8(Tensor x, Tensor scale, c10::optional<Tensor> amax) {
+Tensor quant_bf16_fp8(Tensor x, Tensor scale, c10::optional<Tensor> amax, bool bf8) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_CONT(x); CHECK_F32(scale);
   TORCH_CHECK(x.numel() % 16 == 0, "quant: numel must be a multiple of 16");
   c10::DeviceGuard g(x.device());
@@ -752,7 +801,7 @@ Tensor quant_bf16_fp8(Tensor x, Tensor scale, c10::optional<Tensor> amax) {
   float* am = (amax && amax->defined()) ? amax->data_ptr<float>() : nullptr;
   TORCH_CHECK(!am || (amax->numel() >= 64 && amax->is_contiguous()), "amax must be [64] slots");
   CHECK_RC(pmd::quant_bf16_fp8_launch(bfp(x), q.data_ptr<uint8_t>(), scale.data_ptr<float>(), am,
-                                      x.numel(), cur_stream()), "quant_bf16_fp8");
+                                      x.numel(), cur_stream(), bf8), "quant_bf16_fp8");
   return q;
 }
 
@@ -785,13 +834,13 @@ void fp8_update_scales(Tensor amax, Tensor scale, int64_t n, double fmax) {
            "fp8_update_scales");
 }
 
-Tensor dequant_fp8(Tensor q, c10::optional<Tensor> inv_scale) {
+Tensor dequant_fp8(Tensor q, c10::optional<Tensor> inv_scale, bool bf8) {
   CHECK_DEV(q); CHECK_U8(q); CHECK_CONT(q);
   c10::DeviceGuard g(q.device());
   Tensor out = torch::empty(q.sizes(), q.options().dtype(torch::kFloat32));
   CHECK_RC(pmd::dequant_fp8_launch(q.data_ptr<uint8_t>(), out.data_ptr<float>(),
                                    (inv_scale && inv_scale->defined()) ? inv_scale->data_ptr<float>() : nullptr,
-                                   q.numel(), cur_stream()), "dequant_fp8");
+                                   q.numel(), cur_stream(), bf8), "dequant_fp8");
   return out;
 }
 
@@ -949,13 +998,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_finalize", &bn_finalize, py::arg("sums"), py::arg("count"), py::arg("gamma"), py::arg("beta"),
         py::arg("eps"), py::arg("rm"), py::arg("rv"), py::arg("momentum"), py::arg("nbt"),
         py::arg("eval_mode"), py::arg("shift") = py::none());
-  m.def("bn_apply", &bn_apply);
+  m.def("bn_apply", &bn_apply, py::arg("y1"), py::arg("p1"), py::arg("res"), py::arg("y2"), py::arg("p2"),
+        py::arg("relu"), py::arg("want_mask"), py::arg("q8_scale"), py::arg("q8_amax"), py::arg("q8_only") = false);
   m.def("stats_collapse", &stats_collapse);
   m.def("stats_finalize_local", &stats_finalize_local, py::arg("slots"), py::arg("count"), py::arg("gamma"),
         py::arg("beta"), py::arg("eps"), py::arg("rm"), py::arg("rv"), py::arg("momentum"), py::arg("nbt"),
         py::arg("shift") = py::none());
   m.def("bn_bwd_reduce", &bn_bwd_reduce);
-  m.def("bn_bwd_elemt", &bn_bwd_elemt);
+  m.def("bn_bwd_elemt", &bn_bwd_elemt, py::arg("dout"), py::arg("mask"), py::arg("y"), py::arg("params"),
+        py::arg("gamma"), py::arg("red"), py::arg("count"), py::arg("count_h"), py::arg("relu"),
+        py::arg("want_dzm"), py::arg("eval_mode"), py::arg("q8_scale") = py::none(),
+        py::arg("q8_amax") = py::none());
   m.def("bn_bwd_coef", &bn_bwd_coef);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
@@ -973,9 +1026,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sgd_", &sgd_);
   m.def("synth_images", &synth_images);
   m.def("cifar_augment", &cifar_augment);
-  m.def("quant_bf16_fp8", &quant_bf16_fp8);
+  m.def("quant_bf16_fp8", &quant_bf16_fp8, py::arg("x"), py::arg("scale"), py::arg("amax") = py::none(),
+        py::arg("bf8") = false);
+  m.def("conv_wgrad_fp8", &conv_wgrad_fp8, py::arg("dyq"), py::arg("xq"), py::arg("sdy"), py::arg("sx"),
+        py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("out") = py::none());
   m.def("quant_weight_fp8", &quant_weight_fp8);
-  m.def("dequant_fp8", &dequant_fp8);
+  m.def("dequant_fp8", &dequant_fp8, py::arg("q"), py::arg("inv_scale") = py::none(), py::arg("bf8") = false);
   m.def("fp8_update_scales", &fp8_update_scales, py::arg("amax"), py::arg("scale"), py::arg("n"), py::arg("fmax"));
   m.def("fp8_mfma_probe", &fp8_mfma_probe);
   m.def("conv_fp8_fwd", &conv_fp8_fwd, py::arg("xq"), py::arg("wq"), py::arg("sx"), py::arg("sw"),

@@ -137,7 +137,9 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
         v[k] = o;
       }
       const uint4 pk = pack8(v);
-      st16(reinterpret_cast<uint4*>(out) + i, pk);
+      // Q8 with out == nullptr: the e4m3 copy is the ONLY activation (its consumers --
+      // the fp8 conv and the fp8 wgrad -- never read a bf16 one)
+      if (!Q8 || out) st16(reinterpret_cast<uint4*>(out) + i, pk);
       if (RELU && mask_out) mask_out[i] = (uint8_t)bits;
       if (Q8) {
         float o[8];
@@ -246,12 +248,19 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
 
 // dy = a*dzm + b*y + c.  train: a = g*inv, b = -a*inv*mdyx, c = a*(mean*inv*mdyx - mdy)
 //                        eval : a = scale, b = c = 0
-template <bool RELU, bool DZM, bool EVAL>
+// Q8: also write dy as OCP e5m2 (bf8) * qscale -- the fp8 weight gradient's dY operand
+// (kernels/conv_wgrad.hip) -- quantised from the bf16-rounded value the dgrad reads,
+// saturated to +-57344, and accumulate amax |dy| for the next step's scale.
+template <bool RELU, bool DZM, bool EVAL, bool Q8 = false>
 __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(
     const bf16_t* __restrict__ dout, const uint8_t* __restrict__ mask, const bf16_t* __restrict__ y,
     const float* __restrict__ params, const float* __restrict__ gamma,
     const float* __restrict__ red, const float* __restrict__ count, float count_h,
-    bf16_t* __restrict__ dy, bf16_t* __restrict__ dzm_out, long long nchunk, int C) {
+    bf16_t* __restrict__ dy, bf16_t* __restrict__ dzm_out, long long nchunk, int C,
+    uint8_t* __restrict__ q_out = nullptr, const float* __restrict__ qscale = nullptr,
+    float* __restrict__ qamax = nullptr) {
+  float qs = 0.f, qm = 0.f;
+  if (Q8) qs = qscale[0];
   const int C8 = C >> 3;
   const long long start = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long step = (long long)gridDim.x * blockDim.x;
@@ -305,10 +314,26 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(
         d[k] = dz;
         o[k] = EVAL ? ca[k] * dz : ca[k] * dz + cb[k] * v[k] + cc[k];
       }
-      st16(reinterpret_cast<uint4*>(dy) + i, pack8(o));
+      const uint4 pk = pack8(o);
+      st16(reinterpret_cast<uint4*>(dy) + i, pk);
       if (DZM) st16(reinterpret_cast<uint4*>(dzm_out) + i, pack8(d));
+      if (Q8) {
+        float r[8], c[8];
+        unpack8(pk, r);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          qm = fmaxf(qm, fabsf(r[k]));
+          c[k] = __builtin_amdgcn_fmed3f(r[k] * qs, -57344.f, 57344.f);
+        }
+        int w0 = __builtin_amdgcn_cvt_pk_bf8_f32(c[0], c[1], 0, false);
+        w0 = __builtin_amdgcn_cvt_pk_bf8_f32(c[2], c[3], w0, true);
+        int w1 = __builtin_amdgcn_cvt_pk_bf8_f32(c[4], c[5], 0, false);
+        w1 = __builtin_amdgcn_cvt_pk_bf8_f32(c[6], c[7], w1, true);
+        reinterpret_cast<uint2*>(q_out)[i] = make_uint2((uint32_t)w0, (uint32_t)w1);
+      }
     }
   }
+  if (Q8) block_amax_update(qamax, qm);
 }
 
 // BN-backward coefficients for consumers that apply  dy = a*dzm + b*y + c  on the
@@ -533,10 +558,21 @@ int bn_bwd_reduce_launch(const bf16_t* dout, const uint8_t* mask, const bf16_t* 
 int bn_bwd_elemt_launch(const bf16_t* dout, const uint8_t* mask, const bf16_t* y, const float* params,
                         const float* gamma, const float* red, const float* count, float count_h,
                         bf16_t* dy, bf16_t* dzm, long long M, int C, bool relu, bool eval_mode,
-                        hipStream_t st) {
+                        hipStream_t st, uint8_t* q8, const float* qscale, float* qamax) {
   if (C % 8 || (C >> 3) > 256 || ((C >> 3) & ((C >> 3) - 1))) return 1;
   const long long nchunk = M * (C / 8);
   const int g = ew_grid(nchunk, C / 8);
+  if (q8) {
+    // the fp8 wgrad's e5m2 dY copy: training mode, no dzm output
+    if (!qscale || !qamax || eval_mode || dzm) return 2;
+    if (relu)
+      hipLaunchKernelGGL((bn_bwd_elemt_kernel<true, false, false, true>), dim3(g), dim3(256), 0, st, dout, mask,
+                         y, params, gamma, red, count, count_h, dy, dzm, nchunk, C, q8, qscale, qamax);
+    else
+      hipLaunchKernelGGL((bn_bwd_elemt_kernel<false, false, false, true>), dim3(g), dim3(256), 0, st, dout, mask,
+                         y, params, gamma, red, count, count_h, dy, dzm, nchunk, C, q8, qscale, qamax);
+    return 0;
+  }
 #define EL(RL, DZ, EV)                                                                            \
   hipLaunchKernelGGL((bn_bwd_elemt_kernel<RL, DZ, EV>), dim3(g), dim3(256), 0, st, dout, mask, y, \
                      params, gamma, red, count, count_h, dy, dzm, nchunk, C)

@@ -437,6 +437,195 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_wgrad_dma_kernel(WgradAr
 }
 
 // ---------------------------------------------------------------------------
+// FP8 wgrad (BASELINE config 5): dY as OCP e5m2 (bf8) x X as e4m3 on the block-scaled
+// v_mfma_scale_f32_16x16x128_f8f6f4 (A format bf8, B format fp8, unit block scales):
+// 128 reduction rows (m) per MFMA, twice the bf16 MFMA rate per clock, and half the
+// operand bytes of the bf16 kernel.  Both operands arrive m-major ([m][channels],
+// 1 B per element), are copied to LDS by LDS-DMA in natural row order (128-row
+// stages, 2-deep ring, one barrier per stage), and each MFMA fragment -- 32
+// consecutive m of ONE column per lane -- is read with four ds_read_b64_tr_b8
+// (per 16-lane group: an 8-row x 16-column byte block delivered column-major, lane j
+// receiving column j of the 8 rows).  The 16-B chunk of a 128-B LDS row is XOR-
+// swizzled with row bits 0..2 and 5 (on the DMA SOURCE address, as the bf16 DMA
+// kernel), so the 8 rows x 2 lane-groups of a 32-lane half hit 16 distinct 4-bank
+// slots.  Epilogue: acc / (s_dy * s_x) into the split workspace (or += dW).
+struct WgradF8Args {
+  const uint8_t* dy;  // e5m2 [M][K]
+  const uint8_t* x;   // e4m3 NHWC [N,H,W,C]
+  const float* sdy;   // device scalars the operands were quantised with
+  const float* sx;
+  float* dw;
+  float* ws;
+  int N, H, W, C, log2C, P, Q, K, R, S, stride, pad, M, Kg;
+  int chunks_per_split;  // 128-row chunks per block
+};
+
+__device__ __forceinline__ int swz8(int row) { return (row & 7) ^ ((row >> 5) & 1); }
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_fp8_kernel(WgradF8Args a) {
+  constexpr int BRF = 128;  // reduction rows per stage = one MFMA K
+  constexpr int MI = BM / 32, NI = BN / 32;
+  constexpr int CA = BM / 16, CB = BN / 16;  // 16-B chunks per row
+  constexpr int RA = 256 / CA, RB = 256 / CB;  // rows per block-wide DMA round
+  constexpr int PA = BRF / RA, PB = BRF / RB;
+  constexpr int A_BYTES = BRF * BM, B_BYTES = BRF * BN, STAGE = A_BYTES + B_BYTES;
+  constexpr int LPT = PA + PB;
+  static_assert(RA % 64 == 0 || RA == 32, "DMA rows per round");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tilesM = (a.K + BM - 1) / BM, tilesN = (a.Kg + BN - 1) / BN;
+  const int tiles = tilesM * tilesN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = L / tiles, t = L % tiles;
+  const int k0 = (t / tilesN) * BM, g0 = (t % tilesN) * BN;
+  const int mbeg = split * a.chunks_per_split * BRF;
+  if (mbeg >= a.M) return;
+  const int mend = min(mbeg + a.chunks_per_split * BRF, a.M);
+  const int nchunks = (mend - mbeg + BRF - 1) / BRF;
+
+  // DMA map: thread -> (row tid / C? + R? i, physical chunk tid % C?); the logical chunk
+  // (source column) is the physical one XOR swz8(row), fixed per (thread, instruction)
+  const int a_row0 = tid / CA, a_pc = tid % CA;
+  const int b_row0 = tid / CB, b_pc = tid % CB;
+  int a_col[PA], b_tap_r[PB], b_tap_s[PB], b_c[PB];
+  bool a_colok[PA], b_colok[PB];
+#pragma unroll
+  for (int i = 0; i < PA; ++i) {
+    const int row = a_row0 + RA * i;
+    a_col[i] = ((a_pc ^ swz8(row)) & (CA - 1)) * 16;
+    a_colok[i] = k0 + a_col[i] < a.K;
+  }
+#pragma unroll
+  for (int i = 0; i < PB; ++i) {
+    const int row = b_row0 + RB * i;
+    const int g = g0 + ((b_pc ^ swz8(row)) & (CB - 1)) * 16;
+    b_colok[i] = g < a.Kg;
+    const int tap = b_colok[i] ? (g >> a.log2C) : 0;
+    b_tap_r[i] = tap / a.S;
+    b_tap_s[i] = tap - b_tap_r[i] * a.S;
+    b_c[i] = g & (a.C - 1);
+  }
+  // per-instruction row coordinates (n, p, q) of m = mbeg + row, advanced by BRF per stage
+  int bn_[PB], bp_[PB], bq_[PB];
+  const int pq = a.P * a.Q;
+#pragma unroll
+  for (int i = 0; i < PB; ++i) {
+    const int m = mbeg + b_row0 + RB * i;
+    const int n = m / pq, rem = m - n * pq;
+    bn_[i] = n;
+    bp_[i] = rem / a.Q;
+    bq_[i] = rem - bp_[i] * a.Q;
+  }
+  const int dq = BRF % a.Q, dp = (BRF / a.Q) % a.P, dn = BRF / pq;
+  const int wid_s = __builtin_amdgcn_readfirstlane(wid);
+
+  auto load = [&](int ch, int buf) {
+    const int mb = mbeg + ch * BRF;
+    uint8_t* As = smem + buf * STAGE;
+    uint8_t* Bs = As + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < PA; ++i) {
+      const int m = mb + a_row0 + RA * i;
+      const void* src = (a_colok[i] && m < mend) ? (const void*)(a.dy + (size_t)m * a.K + k0 + a_col[i])
+                                                 : (const void*)g_wzero16;
+      uint8_t* dst = As + (RA * i) * BM + wid_s * 1024;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+      const int m = mb + b_row0 + RB * i;
+      const int ih = bp_[i] * a.stride - a.pad + b_tap_r[i];
+      const int iw = bq_[i] * a.stride - a.pad + b_tap_s[i];
+      const bool ok = b_colok[i] && m < mend && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      const size_t pix = ((size_t)bn_[i] * a.H + ih) * a.W + iw;
+      const void* src = ok ? (const void*)(a.x + (pix << a.log2C) + b_c[i]) : (const void*)g_wzero16;
+      uint8_t* dst = Bs + (RB * i) * BN + wid_s * 1024;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      int q = bq_[i] + dq, c1 = q >= a.Q;
+      q -= c1 ? a.Q : 0;
+      int p = bp_[i] + dp + c1, c2 = p >= a.P;
+      p -= c2 ? a.P : 0;
+      bq_[i] = q;
+      bp_[i] = p;
+      bn_[i] += dn + c2;
+    }
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read: lane j of 16-lane group g4 supplies row 32 g4 + 8 t + (j >> 1), byte
+  // half (j & 1) of the column block's 16-B chunk, and receives column j of those 8 rows
+  const int g4 = lane >> 4, jl = lane & 15;
+  typedef __attribute__((ext_vector_type(2))) int v2i;
+  auto frag = [&](const uint8_t* base, int rowb, int col) {
+    // col: first column of the 16-column block (a multiple of 16); rowb: row bytes
+    i32x8 v;
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      const int row = 32 * g4 + 8 * tt + (jl >> 1);
+      const int off = row * rowb + ((((col >> 4) ^ swz8(row)) & (rowb / 16 - 1)) << 4) + (jl & 1) * 8;
+      const v2i r = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)(base + off));
+      v[2 * tt] = r[0];
+      v[2 * tt + 1] = r[1];
+    }
+    return v;
+  };
+  auto compute = [&](int buf) {
+    const uint8_t* As = smem + buf * STAGE;
+    const uint8_t* Bs = As + A_BYTES;
+    i32x8 af[MI], bfg[NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) af[i] = frag(As, BM, wm * (BM / 2) + i * 16);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) bfg[j] = frag(Bs, BN, wn * (BN / 2) + j * 16);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfg[j], acc[i][j], 1, 0, 0, 127, 0,
+                                                                      127);
+  };
+
+  load(0, 0);
+  for (int ch = 0; ch < nchunks; ++ch) {
+    wg_wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (ch + 1 < nchunks) load(ch + 1, (ch + 1) & 1);
+    compute(ch & 1);
+  }
+  (void)LPT;
+
+  const float ds = 1.f / (a.sdy[0] * a.sx[0]);
+  float* dst = a.ws ? a.ws + (size_t)split * a.K * a.Kg : a.dw;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = k0 + wm * (BM / 2) + i * 16 + g4 * 4 + e;
+        const int gg = g0 + wn * (BN / 2) + j * 16 + jl;
+        if (k < a.K && gg < a.Kg) {
+          float* p = dst + (size_t)k * a.Kg + gg;
+          if (a.ws)
+            *p = acc[i][j][e] * ds;
+          else
+            *p += acc[i][j][e] * ds;
+        }
+      }
+}
+
+// ---------------------------------------------------------------------------
 // HALO wgrad: stride-1 convolutions with K == 64 output channels whose im2col is
 // mostly redundancy -- the ImageNet stem as a 4x4 conv over the space-to-depth
 // image (16 taps x 16 channels: every input pixel appears in 16 im2col columns)
@@ -879,6 +1068,72 @@ static void wgrad_reduce_launch(const WgradArgs& a, int splits, hipStream_t st) 
   long long b = (n4 + 255) / 256;
   if (b > 4096) b = 4096;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)b, groups), dim3(256), 0, st, a.ws, a.dw, splits, n4);
+}
+
+// FP8 wgrad split plan: 128-row chunks, the bf16 kernels' block targets, workspace <= 96 MiB
+static void plan_fp8(const WgradF8Args& a, int BM, int BN, int* splits_out, int* cps_out) {
+  const int tiles = ((a.K + BM - 1) / BM) * ((a.Kg + BN - 1) / BN);
+  const int chunks = (a.M + 127) / 128;
+  int splits = (wgrad_target_blocks(a.R) + tiles - 1) / tiles;
+  const int max_splits = (chunks + 1) / 2;
+  if (splits > max_splits) splits = max_splits;
+  const long long per = (long long)a.K * a.Kg * 4;
+  while (splits > 1 && per * splits > (96ll << 20)) --splits;
+  if (splits < 1) splits = 1;
+  const int cps = (chunks + splits - 1) / splits;
+  *cps_out = cps;
+  *splits_out = (chunks + cps - 1) / cps;
+}
+
+static void fill_f8(WgradF8Args& a, int N, int H, int W, int C, int P, int Q, int K, int R, int S, int stride,
+                    int pad) {
+  a.N = N; a.H = H; a.W = W; a.C = C; a.log2C = ilog2w(C);
+  a.P = P; a.Q = Q; a.K = K; a.R = R; a.S = S; a.stride = stride; a.pad = pad;
+  a.M = (int)((long long)N * P * Q);
+  a.Kg = R * S * C;
+}
+
+int conv_wgrad_fp8_splits(int N, int H, int W, int C, int P, int Q, int K, int R, int S, int stride, int pad) {
+  WgradF8Args a;
+  fill_f8(a, N, H, W, C, P, Q, K, R, S, stride, pad);
+  int splits, cps;
+  plan_fp8(a, K == 64 ? 64 : 128, 128, &splits, &cps);
+  return splits;
+}
+
+int conv_wgrad_fp8_launch(const uint8_t* dyq, const uint8_t* xq, const float* sdy, const float* sx, float* dw,
+                          float* ws, int N, int H, int W, int C, int P, int Q, int K, int R, int S, int stride,
+                          int pad, hipStream_t st) {
+  if (C % 16 != 0 || (C & (C - 1)) != 0) return 1;  // a 16-B chunk = 16 channels of one tap
+  if (K % 64 != 0) return 2;
+  if ((long long)N * P * Q >= (1ll << 31)) return 4;
+  WgradF8Args a;
+  fill_f8(a, N, H, W, C, P, Q, K, R, S, stride, pad);
+  a.dy = dyq;
+  a.x = xq;
+  a.sdy = sdy;
+  a.sx = sx;
+  a.dw = dw;
+  const int BM = K == 64 ? 64 : 128;
+  int splits, cps;
+  plan_fp8(a, BM, 128, &splits, &cps);
+  if (splits > 1 && !ws) return 5;
+  a.ws = splits > 1 ? ws : nullptr;
+  a.chunks_per_split = cps;
+  const int tiles = ((a.K + BM - 1) / BM) * ((a.Kg + 127) / 128);
+  if (BM == 64)
+    hipLaunchKernelGGL((conv_wgrad_fp8_kernel<64, 128>), dim3(tiles * splits), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_wgrad_fp8_kernel<128, 128>), dim3(tiles * splits), dim3(256), 0, st, a);
+  if (splits > 1) {
+    WgradArgs r;
+    r.K = a.K;
+    r.Kg = a.Kg;
+    r.ws = ws;
+    r.dw = dw;
+    wgrad_reduce_launch(r, splits, st);
+  }
+  return 0;
 }
 
 static int wgrad_tune(const WgradArgs& a0, float* ws, hipStream_t st) {

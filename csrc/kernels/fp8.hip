@@ -27,8 +27,19 @@ __device__ __forceinline__ float fp8_to_f32(uint32_t byte) {
   return __builtin_amdgcn_cvt_f32_fp8((int)byte, 0);
 }
 
+// OCP e5m2 (bf8, the gradient format of the fp8 wgrad): max normal 57344; the
+// convert does not saturate either
+__device__ __forceinline__ uint32_t pack4_bf8(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_bf8_f32(__builtin_amdgcn_fmed3f(a, -57344.f, 57344.f),
+                                          __builtin_amdgcn_fmed3f(b, -57344.f, 57344.f), 0, false);
+  w = __builtin_amdgcn_cvt_pk_bf8_f32(__builtin_amdgcn_fmed3f(c, -57344.f, 57344.f),
+                                      __builtin_amdgcn_fmed3f(d, -57344.f, 57344.f), w, true);
+  return (uint32_t)w;
+}
 
-// bf16 [n] (n % 16 == 0) -> e4m3 [n]; amax_in += max |x|
+
+// bf16 [n] (n % 16 == 0) -> e4m3 (BF8: e5m2) [n]; amax_in += max |x|
+template <bool BF8>
 __global__ __launch_bounds__(256) void quant_bf16_fp8_kernel(const bf16_t* __restrict__ x,
                                                             uint8_t* __restrict__ q,
                                                             const float* __restrict__ scale,
@@ -47,7 +58,8 @@ __global__ __launch_bounds__(256) void quant_bf16_fp8_kernel(const bf16_t* __res
     for (int k = 0; k < 4; ++k) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) m = fmaxf(m, fabsf(f[4 * k + e]));
-      w[k] = pack4_fp8(f[4 * k] * s, f[4 * k + 1] * s, f[4 * k + 2] * s, f[4 * k + 3] * s);
+      w[k] = BF8 ? pack4_bf8(f[4 * k] * s, f[4 * k + 1] * s, f[4 * k + 2] * s, f[4 * k + 3] * s)
+                 : pack4_fp8(f[4 * k] * s, f[4 * k + 1] * s, f[4 * k + 2] * s, f[4 * k + 3] * s);
     }
     reinterpret_cast<uint4*>(q)[i] = make_uint4(w[0], w[1], w[2], w[3]);
   }
@@ -128,13 +140,14 @@ int fp8_update_scales_launch(float* amax, float* scale, int n, float fmax, hipSt
   return 0;
 }
 
-// e4m3 -> fp32 (tests / debugging)
+// e4m3 (BF8: e5m2) -> fp32 (tests / debugging)
+template <bool BF8>
 __global__ void dequant_fp8_kernel(const uint8_t* __restrict__ q, float* __restrict__ out,
                                    const float* __restrict__ inv_scale, long long n) {
   const float s = inv_scale ? inv_scale[0] : 1.f;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x)
-    out[i] = fp8_to_f32(q[i]) * s;
+    out[i] = (BF8 ? __builtin_amdgcn_cvt_f32_bf8((int)q[i], 0) : fp8_to_f32(q[i])) * s;
 }
 
 // One 16x16x128 scaled-MFMA tile: C[16][16] = A[16][128] * B[128][16], A row-major
@@ -165,10 +178,14 @@ static int blocks_for(long long n, int per) {
 }
 
 int quant_bf16_fp8_launch(const bf16_t* x, uint8_t* q, const float* scale, float* amax, long long n,
-                          hipStream_t st) {
+                          hipStream_t st, bool bf8) {
   if (n % 16) return 1;
-  hipLaunchKernelGGL(quant_bf16_fp8_kernel, dim3(blocks_for(n / 16, 256)), dim3(256), 0, st, x, q, scale,
-                     amax, n / 16);
+  if (bf8)
+    hipLaunchKernelGGL(quant_bf16_fp8_kernel<true>, dim3(blocks_for(n / 16, 256)), dim3(256), 0, st, x, q, scale,
+                       amax, n / 16);
+  else
+    hipLaunchKernelGGL(quant_bf16_fp8_kernel<false>, dim3(blocks_for(n / 16, 256)), dim3(256), 0, st, x, q, scale,
+                       amax, n / 16);
   return 0;
 }
 
@@ -179,8 +196,12 @@ int quant_weight_fp8_launch(const float* w, uint8_t* q, const float* scale, floa
   return 0;
 }
 
-int dequant_fp8_launch(const uint8_t* q, float* out, const float* inv_scale, long long n, hipStream_t st) {
-  hipLaunchKernelGGL(dequant_fp8_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, st, q, out, inv_scale, n);
+int dequant_fp8_launch(const uint8_t* q, float* out, const float* inv_scale, long long n, hipStream_t st,
+                       bool bf8) {
+  if (bf8)
+    hipLaunchKernelGGL(dequant_fp8_kernel<true>, dim3(blocks_for(n, 256)), dim3(256), 0, st, q, out, inv_scale, n);
+  else
+    hipLaunchKernelGGL(dequant_fp8_kernel<false>, dim3(blocks_for(n, 256)), dim3(256), 0, st, q, out, inv_scale, n);
   return 0;
 }
 

@@ -71,6 +71,11 @@ int conv_wgrad_splits(int N, int H, int W, int C, int P, int Q, int K, int R, in
 int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, float* ws, int N, int H, int W,
                       int C, int P, int Q, int K, int R, int S, int stride, int pad, hipStream_t st,
                       const TxArgs* tx = nullptr);
+// FP8 weight gradient: e5m2 dY x e4m3 X on the scaled 16x16x128 MFMA (kernels/conv_wgrad.hip)
+int conv_wgrad_fp8_splits(int N, int H, int W, int C, int P, int Q, int K, int R, int S, int stride, int pad);
+int conv_wgrad_fp8_launch(const uint8_t* dyq, const uint8_t* xq, const float* sdy, const float* sx, float* dw,
+                          float* ws, int N, int H, int W, int C, int P, int Q, int K, int R, int S, int stride,
+                          int pad, hipStream_t st);
 
 // shift (nullable): the statistics shift K the sums were taken about; overwritten with
 // the batch mean (the next step's shift)
@@ -95,7 +100,8 @@ int bn_bwd_coef_launch(const float* params, const float* gamma, const float* red
 int bn_bwd_elemt_launch(const bf16_t* dout, const uint8_t* mask, const bf16_t* y, const float* params,
                         const float* gamma, const float* red, const float* count, float count_h,
                         bf16_t* dy, bf16_t* dzm, long long M, int C, bool relu, bool eval_mode,
-                        hipStream_t st);
+                        hipStream_t st, uint8_t* q8 = nullptr, const float* qscale = nullptr,
+                        float* qamax = nullptr);
 
 // fused stem tail (kernels/stem.hip): BN + ReLU + 3x3/s2 max-pool, and its backward
 // space-to-depth stem (7x7/s2 over 3 channels as 4x4/s1 over 16)
@@ -141,7 +147,7 @@ int cifar_augment_launch(const uint8_t* data, const long long* idx, void* out, b
 
 // FP8 e4m3 (kernels/fp8.hip)
 int quant_bf16_fp8_launch(const bf16_t* x, uint8_t* q, const float* scale, float* amax, long long n,
-                          hipStream_t st);
+                          hipStream_t st, bool bf8 = false);
 // all fp8 weight images of a model in one launch (per-conv scale / amax sites)
 struct Fp8WeightDesc {
   const float* w;      // fp32 [K][R][S][C]
@@ -155,7 +161,8 @@ void quant_weight_fp8_grouped_launch(const Fp8WeightDesc* d_descs, const int* d_
 int quant_weight_fp8_launch(const float* w, uint8_t* q, const float* scale, float* amax, int K, int RS,
                             int C, int Cp, hipStream_t st);
 int fp8_update_scales_launch(float* amax, float* scale, int n, float fmax, hipStream_t st);
-int dequant_fp8_launch(const uint8_t* q, float* out, const float* inv_scale, long long n, hipStream_t st);
+int dequant_fp8_launch(const uint8_t* q, float* out, const float* inv_scale, long long n, hipStream_t st,
+                       bool bf8 = false);
 int fp8_mfma_probe_launch(const uint8_t* A, const uint8_t* Bt, float* C, hipStream_t st);
 // y(bf16) = conv(xq, wq) / (sx * sw) with e4m3 NHWC input / KRSC weight; optional BN stats slots
 int conv_fp8_fwd_launch(const uint8_t* x, const uint8_t* w, bf16_t* out, float* stats, const float* sx,

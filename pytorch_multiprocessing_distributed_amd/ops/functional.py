@@ -185,6 +185,9 @@ def _fp8_for(P):
 #     e4m3 K-tile (PMD_FP8_MIN_KG, default 128; 0 = every block conv).
 FP8_CONVS = os.environ.get("PMD_FP8_CONVS", "spatial")
 FP8_MIN_KG = int(os.environ.get("PMD_FP8_MIN_KG", "128"))
+# fp8 weight gradients (e5m2 dY x e4m3 X) for every conv whose forward ran in fp8; the
+# bf16 copy of a stage activation is then not written at all (PMD_FP8_WGRAD=0: bf16 wgrads)
+FP8_WGRAD = os.environ.get("PMD_FP8_WGRAD", "1") != "0"
 
 
 def fp8_eligible(conv_m, cin) -> bool:
@@ -262,7 +265,19 @@ def _claim(p):
     p._pmd_claim = True
 
 
-def _wgrad(P, dy, x, wpack, stride, pad, w):
+def _conv_wgrad_any(P, dy, x, xq, wk_shape, stride, pad, out=None):
+    """bf16 weight gradient, or the fp8 one (e5m2 dY x e4m3 X) when the conv input's
+    e4m3 copy ``xq = (q, scale)`` was saved and dY carries its e5m2 copy."""
+    dq = getattr(dy, "_pmd_q8", None)
+    if xq is not None and dq is not None:
+        return P.conv_wgrad_fp8(dq[0], dq[1], xq[0], xq[1], wk_shape, stride, pad, out=out)
+    if x.dtype == torch.uint8:
+        raise RuntimeError("fp8-only activation (no bf16 copy) but dY has no e5m2 copy: "
+                           "the fp8 weight gradient must run for this conv")
+    return P.conv_wgrad(dy, x, wk_shape, stride, pad, out=out)
+
+
+def _wgrad(P, dy, x, wpack, stride, pad, w, xq=None):
     """Weight gradient: accumulated into the arena (returns None) or returned."""
     if not w.requires_grad:
         return None
@@ -271,10 +286,10 @@ def _wgrad(P, dy, x, wpack, stride, pad, w):
     cx = wpack[0].shape[-1]
     tgt = _grad_target(w)
     if tgt is not None and cx == w.shape[1]:
-        P.conv_wgrad(dy, x, tuple(wpack[0].shape), stride, pad, out=tgt.permute(0, 2, 3, 1))
+        _conv_wgrad_any(P, dy, x, xq, tuple(wpack[0].shape), stride, pad, out=tgt.permute(0, 2, 3, 1))
         _ready(w)
         return None
-    dwk = P.conv_wgrad(dy, x, tuple(wpack[0].shape), stride, pad)   # fp32 [K,R,S,Cx]
+    dwk = _conv_wgrad_any(P, dy, x, xq, tuple(wpack[0].shape), stride, pad)   # fp32 [K,R,S,Cx]
     if cx != w.shape[1]:
         dwk = dwk[..., : w.shape[1]].contiguous()
     return dwk.permute(0, 3, 1, 2)                                   # [K,C,R,S] channels_last
@@ -328,9 +343,9 @@ class _WgradSide:
             self.side = _wgrad_stream(dev)
             self.main = torch.cuda.current_stream(dev)
 
-    def wgrad(self, P, dy, x, wpack, stride, pad, w):
+    def wgrad(self, P, dy, x, wpack, stride, pad, w, xq=None):
         if not self.on or _grad_target(w) is None:
-            return _wgrad(P, dy, x, wpack, stride, pad, w)
+            return _wgrad(P, dy, x, wpack, stride, pad, w, xq)
         # dy may be a LazyDy: its record_stream covers dzm, y and the coefficients
         _claim(w)
         self.side.wait_stream(self.main)
@@ -339,9 +354,14 @@ class _WgradSide:
             # a LazyDy (BN backward applied by the main-stream dgrad) is materialised
             # HERE, on the side stream: the elementwise pass leaves the critical path
             dyw = dy.materialize() if is_lazy(dy) else dy
-            P.conv_wgrad(dyw, x, tuple(wpack[0].shape), stride, pad, out=tgt.permute(0, 2, 3, 1))
+            _conv_wgrad_any(P, dyw, x, xq, tuple(wpack[0].shape), stride, pad, out=tgt.permute(0, 2, 3, 1))
         dy.record_stream(self.side)
         x.record_stream(self.side)
+        dq = getattr(dy, "_pmd_q8", None)
+        if dq is not None:
+            dq[0].record_stream(self.side)
+        if xq is not None:
+            xq[0].record_stream(self.side)
         self.ready.append(w)
         return None
 
@@ -542,22 +562,26 @@ def _tx_ok(P, conv_m, pre, training):
             and tuple(conv_m.weight.shape[2:]) == (1, 1))
 
 
-def _elemt(P, dout, mask, y, p, gamma, red, count, relu, want_dzm=False, lazy=False):
-    if lazy and not want_dzm:
+def _elemt(P, dout, mask, y, p, gamma, red, count, relu, want_dzm=False, lazy=False, q8=None):
+    if lazy and not want_dzm and q8 is None:
         return LazyDy(dout, y, P.bn_bwd_coef(p, gamma, red, count),
                       (P, mask, p, gamma, red, count, relu)), None
+    if q8 is not None and not want_dzm:
+        # + the e5m2 copy of dY for the fp8 weight gradient (dy._pmd_q8)
+        return P.bn_bwd_elemt(dout, mask, y, p, gamma, red, count, relu, q8=q8)
     return P.bn_bwd_elemt(dout, mask, y, p, gamma, red, count, relu, want_dzm=want_dzm)
 
 
 def _bn_backward(P, dout, mask, relu, training, sync, count, y1, p1, bn1, y2=None, p2=None,
-                 bn2=None, want_dzm=False, pre=None, elemt_fn=None, lazy=(False, False)):
+                 bn2=None, want_dzm=False, pre=None, elemt_fn=None, lazy=(False, False), q8=(None, None)):
     """BN(+second BN)(+ReLU) backward. Returns (dy1, dy2, dzm, grads) with
     grads = [d_g1, d_b1, d_g2, d_b2] for params that were NOT written directly.
     ``pre``: the reduce results already produced by the dgrad that computed
     ``dout`` (fused epilogue), in the order (bn1[, bn2]).  ``elemt_fn(red, count)``
     replaces the elementwise pass of BN 1 (fused stem: it re-derives dz itself;
     red/count are None in eval mode).  ``lazy[i]``: return dY of BN i as a
-    :class:`LazyDy` (its consumer is a 1x1 conv that applies it on load)."""
+    :class:`LazyDy` (its consumer is a 1x1 conv that applies it on load).  ``q8[i]``:
+    (scale, amax) of an e5m2 copy of dY of BN i for an fp8 weight gradient."""
     if pre is not None:
         r1 = pre[0]
         r2 = pre[1] if y2 is not None else None
@@ -596,11 +620,11 @@ def _bn_backward(P, dout, mask, relu, training, sync, count, y1, p1, bn1, y2=Non
             dy1, dzm = elemt_fn(red[:2 * c1].view(2, c1), count), None
         else:
             dy1, dzm = _elemt(P, dout, mask, y1, p1, bn1.weight, red[:2 * c1].view(2, c1), count,
-                              relu, want_dzm=want_dzm, lazy=lazy[0])
+                              relu, want_dzm=want_dzm, lazy=lazy[0], q8=q8[0])
         dy2 = None
         if y2 is not None:
             dy2, _ = _elemt(P, dout, mask, y2, p2, bn2.weight, red[2 * c1:].view(2, -1), count,
-                            relu, lazy=lazy[1])
+                            relu, lazy=lazy[1], q8=q8[1])
         return dy1, dy2, dzm, [None, None, None, None]
     red = P.stats_collapse(r1, r2, None, acc1, acc2)     # local sums; gamma/beta grads += local
     grads = [None, None, None, None]
@@ -622,11 +646,11 @@ def _bn_backward(P, dout, mask, relu, training, sync, count, y1, p1, bn1, y2=Non
             dy1, dzm = elemt_fn(red[:2 * c1].view(2, c1), count), None
         else:
             dy1, dzm = _elemt(P, dout, mask, y1, p1, bn1.weight, red[:2 * c1].view(2, c1),
-                              count, relu, want_dzm=want_dzm, lazy=lazy[0])
+                              count, relu, want_dzm=want_dzm, lazy=lazy[0], q8=q8[0])
         dy2 = None
         if y2 is not None:
             dy2, _ = _elemt(P, dout, mask, y2, p2, bn2.weight, red[2 * c1:].view(2, -1), count,
-                            relu, lazy=lazy[1])
+                            relu, lazy=lazy[1], q8=q8[1])
     elif elemt_fn is not None:
         dy1, dy2, dzm = elemt_fn(None, None), None, None
     else:
@@ -908,27 +932,39 @@ class _ResidualBlockFn(torch.autograd.Function):
                 sx, ax = f8.site(("in", id(stages[0][0])))
                 hq = (P.quant_bf16_fp8(x, sx, ax), sx)
         xq = hq
+        # fp8 weight gradients: a conv whose forward read an e4m3 input keeps that input
+        # (+ its scale) for an e5m2 x e4m3 wgrad, and a stage activation consumed only by
+        # such a conv is written in e4m3 alone (no bf16 copy: h is then the uint8 tensor,
+        # used for its shape)
+        f8w = f8 is not None and training and FP8_WGRAD and torch.is_grad_enabled()
+
+        def used_q(conv_m, hq_, h_):
+            return hq_ if (hq_ is not None and fp8_eligible(conv_m, h_.shape[-1])) else None
         h = x
-        recs = []
+        recs, qins = [], []
         nxt_convs = [c for c, _ in stages[1:]] + [final[0]]
         for si, (conv_m, bn) in enumerate(stages):
             wp = _conv_weight(P, conv_m, x.dtype, h.shape[-1], True)
-            y, st = _conv_fwd_any(P, f8, h, hq if (hq is not None and fp8_eligible(conv_m, h.shape[-1])) else None,
-                                  wp, conv_m, _stats_req(bn, training))
+            hq_in = used_q(conv_m, hq, h)
+            y, st = _conv_fwd_any(P, f8, h, hq_in, wp, conv_m, _stats_req(bn, training))
             p, _, count = _bn_forward_params(P, y, st, bn, training, sync)
             if f8 is not None and fp8_eligible(nxt_convs[si], y.shape[-1]):
                 site = f8.site(("a", id(bn)))
-                z, zmask, zq = P.bn_apply(y, p, relu=True, fp8=site)
+                z, zmask, zq = P.bn_apply(y, p, relu=True, fp8=site, fp8_only=f8w)
                 hq = (zq, site[0])
+                if z is None:
+                    z = zq
             else:
                 z, zmask = P.bn_apply(y, p, relu=True)
                 hq = None
             recs.append((h, wp, y, p, zmask, count))
+            qins.append(hq_in if f8w else None)
             h = z
         fconv, fbn = final
         wpf = _conv_weight(P, fconv, x.dtype, h.shape[-1], True)
-        yf, stf = _conv_fwd_any(P, f8, h, hq if (hq is not None and fp8_eligible(fconv, h.shape[-1])) else None,
-                                wpf, fconv, _stats_req(fbn, training))
+        hq_f = used_q(fconv, hq, h)
+        yf, stf = _conv_fwd_any(P, f8, h, hq_f, wpf, fconv, _stats_req(fbn, training))
+        qins.append(hq_f if f8w else None)
         # e4m3 copy of the block output only if its consumer -- the next block's first
         # conv, which has this block's first-conv kernel shape -- runs in fp8
         osite = (f8.site(("a", id(fbn))) if f8 is not None and fp8_eligible(stages[0][0], yf.shape[-1])
@@ -936,8 +972,9 @@ class _ResidualBlockFn(torch.autograd.Function):
         if shortcut is not None:
             sconv, sbn = shortcut
             wps = _conv_weight(P, sconv, x.dtype, x.shape[-1], x.requires_grad)
-            ys, sts = _conv_fwd_any(P, f8, x, xq if (xq is not None and fp8_eligible(sconv, x.shape[-1])) else None,
-                                    wps, sconv, _stats_req(sbn, training))
+            xq_s = used_q(sconv, xq, x)
+            ys, sts = _conv_fwd_any(P, f8, x, xq_s, wps, sconv, _stats_req(sbn, training))
+            qins.append(xq_s if f8w else None)
             pf, ps, countf = _bn_forward_params(P, yf, stf, fbn, training, sync, ys, sts, sbn)
             r = P.bn_apply(yf, pf, None, ys, ps, relu=True, **({"fp8": osite} if osite else {}))
         else:
@@ -949,6 +986,11 @@ class _ResidualBlockFn(torch.autograd.Function):
             out._pmd_q8 = (r[2], osite[0])      # the next block's fp8 conv input
         ctx.cfg = (cfg, sync, [r[5] for r in recs], countf, len(wpf),
                    0 if wps is None else len(wps), [len(r[1]) for r in recs])
+        # e4m3 conv inputs for the fp8 wgrads: (q, scale) per stage conv, final conv,
+        # projection conv; the scales are views of the Fp8Scaling buffer, which the next
+        # update() rewrites only after this backward (stream order)
+        ctx.qins = qins if any(q is not None for q in qins) else None
+        ctx.f8 = f8 if f8w else None
         # cross-block fusion: the NEXT block's first dgrad computes d(out) and can
         # reduce this block's final BN(s) in its epilogue.  The site carries what
         # it needs; the input's site (previous block) is remembered likewise.
@@ -1002,6 +1044,13 @@ class _ResidualBlockFn(torch.autograd.Function):
             if g is not None:
                 grads[id(p)] = g
 
+        qins = ctx.qins or [None] * (nst + 2)
+
+        def gsite(i, bn_):
+            # e5m2 scale/amax site of the dY that feeds conv i's fp8 weight gradient
+            if ctx.f8 is None or i >= len(qins) or qins[i] is None:
+                return None
+            return ctx.f8.grads.site(("dy", id(bn_)))
         # reduce of the final BN(s), if the next block's dgrad already produced it
         pre = ctx.out_site.take(dout, P) if ctx.out_site is not None else None
         # --- final BN (+ projection BN) and the residual ReLU
@@ -1011,7 +1060,8 @@ class _ResidualBlockFn(torch.autograd.Function):
             wps = tuple(sv[i + 2:i + 2 + nws])
             dyf, dys, _, g = _bn_backward(P, dout, omask, True, training, sync, countf,
                                           yf, pf, fbn, ys, ps, sbn, pre=pre,
-                                          lazy=(_tx_ok(P, fconv, pre, training), False))
+                                          lazy=(_tx_ok(P, fconv, pre, training), False),
+                                          q8=(gsite(nst, fbn), gsite(nst + 1, sbn)))
             put(sbn.weight, g[2])
             put(sbn.bias, g[3])
             dres = None
@@ -1020,7 +1070,8 @@ class _ResidualBlockFn(torch.autograd.Function):
             # stage's dgrad epilogue adds dout gated by the mask bits
             dyf, _, _, g = _bn_backward(P, dout, omask, True, training, sync, countf,
                                         yf, pf, fbn, pre=pre,
-                                        lazy=(_tx_ok(P, fconv, pre, training), False))
+                                        lazy=(_tx_ok(P, fconv, pre, training), False),
+                                        q8=(gsite(nst, fbn), None))
             dres = (dout, omask)
         put(fbn.weight, g[0])
         put(fbn.bias, g[1])
@@ -1036,7 +1087,8 @@ class _ResidualBlockFn(torch.autograd.Function):
         chk("dyf", dyf)
         side = _WgradSide(dout)
         # --- final conv (its wgrad forks to the side stream first: it overlaps the dgrad)
-        put(fconv.weight, side.wgrad(P, dyf, hlast, wpf, fconv.stride, fconv.padding, fconv.weight))
+        put(fconv.weight, side.wgrad(P, dyf, hlast, wpf, fconv.stride, fconv.padding, fconv.weight,
+                                     qins[nst]))
         dh, pre_k = dgrad_fused(dyf, wpf, tuple(hlast.shape), fconv.stride, fconv.padding, recs[-1])
         chk("dh(final)", dh)
         dx = None
@@ -1046,12 +1098,12 @@ class _ResidualBlockFn(torch.autograd.Function):
             conv_m, bn = stages[k]
             hin, wp, y, p, zmask = recs[k]
             dy, _, _, g = _bn_backward(P, dh, zmask, True, training, sync, counts[k], y, p, bn,
-                                       pre=pre_k)
+                                       pre=pre_k, q8=(gsite(k, bn), None))
             put(bn.weight, g[0])
             put(bn.bias, g[1])
             chk(f"dy(stage {k})", dy)
             put(conv_m.weight, side.wgrad(P, dy, hin, wp, conv_m.stride, conv_m.padding,
-                                          conv_m.weight))
+                                          conv_m.weight, qins[k]))
             if k > 0:
                 dh, pre_k = dgrad_fused(dy, wp, tuple(hin.shape), conv_m.stride, conv_m.padding,
                                         recs[k - 1])
@@ -1072,7 +1124,8 @@ class _ResidualBlockFn(torch.autograd.Function):
                     dx = P.conv_dgrad(dy, wp, tuple(x.shape), conv_m.stride, conv_m.padding, addend,
                                       addend_mask=amask)
         if shortcut is not None:
-            put(sconv.weight, side.wgrad(P, dys, x, wps, sconv.stride, sconv.padding, sconv.weight))
+            put(sconv.weight, side.wgrad(P, dys, x, wps, sconv.stride, sconv.padding, sconv.weight,
+                                         qins[nst + 1]))
         side.join()
         return (None, dx, *[grads.get(id(p)) for p in _block_params(stages, final, shortcut)])
 

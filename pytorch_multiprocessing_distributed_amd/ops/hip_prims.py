@@ -99,6 +99,11 @@ def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None, bnred=None, addend_
     return dx, bufs
 
 
+def conv_wgrad_fp8(dyq, sdy, xq, sx, wk_shape, stride, pad, out=None):
+    """dW of e5m2 dY (scale sdy) x e4m3 X (scale sx), ADDED to ``out`` ([K,R,S,C])."""
+    return _C.conv_wgrad_fp8(dyq, xq, sdy, sx, int(wk_shape[1]), int(wk_shape[2]), int(stride), int(pad), out)
+
+
 def conv_wgrad(dy, x, wk_shape, stride, pad, out=None):
     """fp32 [K,R,S,C]; with ``out`` the gradient is accumulated into it.  ``dy`` may
     be a :class:`.lazy.LazyDy` (BN backward applied on load)."""
@@ -140,12 +145,13 @@ def stats_collapse(a, b=None, count=None, acc_a=None, acc_b=None):
     return out
 
 
-def bn_apply(y1, p1, res=None, y2=None, p2=None, relu=True, fp8=None):
+def bn_apply(y1, p1, res=None, y2=None, p2=None, relu=True, fp8=None, fp8_only=False):
     """-> (out, mask): mask is the ReLU bitmask (uint8 per 8-channel chunk) the
     backward reads instead of re-reading ``out`` (1/16 of the bytes).
-    ``fp8=(scale, amax)`` -> (out, mask, q): q is an e4m3 copy of out * scale."""
+    ``fp8=(scale, amax)`` -> (out, mask, q): q is an e4m3 copy of out * scale;
+    ``fp8_only``: q is the only activation written (out is None)."""
     if fp8 is not None:
-        r = _C.bn_apply(y1, p1, res, y2, p2, True, True, fp8[0], fp8[1])
+        r = _C.bn_apply(y1, p1, res, y2, p2, True, True, fp8[0], fp8[1], bool(fp8_only))
         return r[0], r[1], r[2]
     r = _C.bn_apply(y1, p1, res, y2, p2, bool(relu), True, None, None)
     return (r[0], r[1]) if relu else (r[0], None)
@@ -156,13 +162,19 @@ def bn_bwd_reduce(dout, mask, y, p, relu):
     return _C.bn_bwd_reduce(dout, mask, y, p, bool(relu), buf)
 
 
-def bn_bwd_elemt(dout, mask, y, p, gamma, red, count, relu, want_dzm=False):
+def bn_bwd_elemt(dout, mask, y, p, gamma, red, count, relu, want_dzm=False, q8=None):
+    """-> (dy, dzm).  ``q8=(scale, amax)``: dy also gets an e5m2 copy (dy * scale) for the
+    fp8 weight gradient, attached as ``dy._pmd_q8 = (dyq, scale)``."""
+    qs, qa = (q8[0], q8[1]) if q8 is not None else (None, None)
     if torch.is_tensor(count):
         r = _C.bn_bwd_elemt(dout, mask, y, p, gamma.detach(), red, count, 0.0, bool(relu),
-                            bool(want_dzm), False)
+                            bool(want_dzm), False, qs, qa)
     else:
         r = _C.bn_bwd_elemt(dout, mask, y, p, gamma.detach(), red, None, float(count), bool(relu),
-                            bool(want_dzm), False)
+                            bool(want_dzm), False, qs, qa)
+    if q8 is not None:
+        r[0]._pmd_q8 = (r[1], q8[0])
+        return r[0], None
     return (r[0], r[1]) if want_dzm else (r[0], None)
 
 

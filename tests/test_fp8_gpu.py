@@ -97,6 +97,54 @@ def test_conv_fp8_fwd(shape):
     assert rel < 0.1, rel
 
 
+def test_quant_bf16_bf8_e5m2_matches_torch():
+    """The e5m2 (bf8) gradient quantiser: bytes equal torch's float8_e5m2 cast of the
+    scaled value, out-of-range values saturate to +-57344, dequant round-trips."""
+    C = _C()
+    x = (torch.randn(4096, device=DEV) * 30).to(torch.bfloat16)
+    scale = torch.tensor([4.0], device=DEV)
+    amax = torch.zeros(64, device=DEV)
+    q = C.quant_bf16_fp8(x, scale, amax, bf8=True)
+    want = (x.float() * 4.0).to(torch.float8_e5m2).view(torch.uint8)
+    assert torch.equal(q, want)
+    assert amax.max().item() == x.float().abs().max().item()
+    back = C.dequant_fp8(q, torch.tensor([0.25], device=DEV), bf8=True)
+    torch.testing.assert_close(back, x.float(), rtol=0.13, atol=1e-3)
+    big = torch.tensor([1e5, -1e5, 57344.0, 6e4] * 4, device=DEV).to(torch.bfloat16)
+    vals = C.dequant_fp8(C.quant_bf16_fp8(big, torch.tensor([1.0], device=DEV), None, bf8=True), None, bf8=True)
+    assert torch.equal(vals, torch.tensor([57344.0, -57344.0, 57344.0, 57344.0] * 4, device=DEV))
+
+
+@pytest.mark.parametrize("shape", [(64, 56, 64, 3, 1), (128, 28, 128, 3, 1), (256, 14, 256, 3, 1),
+                                   (512, 7, 512, 3, 1), (128, 56, 128, 3, 2), (256, 14, 1024, 1, 1),
+                                   (64, 56, 256, 1, 1), (1024, 14, 512, 1, 2)],
+                         ids=lambda s: "C%d_H%d_K%d_R%d_s%d" % s)
+def test_conv_wgrad_fp8(shape):
+    """e5m2 dY x e4m3 X weight gradient on the scaled 16x16x128 MFMA (transposed
+    ds_read_b64_tr_b8 fragments, split-K + ordered reduce) == the fp32 weight gradient
+    of the same dequantised operands; accumulates into ``out``."""
+    C = _C()
+    torch.manual_seed(1)
+    Cin, H, K, R, st = shape
+    pad = R // 2
+    N = 2 if H >= 56 else (4 if H >= 28 else 16)
+    x = torch.randn(N, H, H, Cin, device=DEV).relu().to(torch.bfloat16)
+    P = (H + 2 * pad - R) // st + 1
+    dy = (torch.randn(N, P, P, K, device=DEV) * 1e-3).to(torch.bfloat16)
+    sx = torch.tensor([448.0 / x.float().abs().max().item()], device=DEV)
+    sdy = torch.tensor([57344.0 / 4 / dy.float().abs().max().item()], device=DEV)
+    xq = C.quant_bf16_fp8(x, sx, None)
+    dyq = C.quant_bf16_fp8(dy, sdy, None, bf8=True)
+    base = torch.randn(K, R, R, Cin, device=DEV)
+    dw = C.conv_wgrad_fp8(dyq, xq, sdy, sx, R, R, st, pad, base.clone())
+    xd = C.dequant_fp8(xq, 1.0 / sx).permute(0, 3, 1, 2)
+    dyd = C.dequant_fp8(dyq, 1.0 / sdy, bf8=True).permute(0, 3, 1, 2)
+    ref = torch.nn.grad.conv2d_weight(xd.double(), (K, Cin, R, R), dyd.double(), stride=st,
+                                      padding=pad).permute(0, 2, 3, 1).float()
+    err = ((dw - base) - ref).abs().max() / ref.abs().max()
+    assert err < 1e-4, err
+
+
 def test_resnet50_fp8_trains():
     """Config 5 path: ResNet-50 with fp8 block-conv forwards (e4m3, delayed
     scaling) converges on a fixed batch like the bf16 model, and its first-step
