@@ -187,6 +187,9 @@ def bench_rank(rank, world, a):
         loss = step(a.warmup + i)
         if comm is not None:
             comm.raise_if_failed()          # host-mapped xGMI error word, no device sync
+    # host time to ENQUEUE the timed steps (nothing in the loop waits on the device): when
+    # it approaches ms_per_step the step is launch-/host-bound, not device-bound
+    host_dt = time.perf_counter() - t0
     torch.cuda.synchronize()
     if comm is not None:
         comm.barrier()
@@ -237,6 +240,7 @@ def bench_rank(rank, world, a):
             "final_loss": round(final_loss, 4),
             "tune_source": tune_source,
             "kernel_choice_hash": choice_hash,
+            "host_enqueue_ms_per_step": round(1000.0 * host_dt / a.steps, 3),
         }
         if stock is not None:
             rec["stock_pytorch_rocm_ips_measured"] = round(stock, 1)

@@ -44,6 +44,7 @@ class Fp8Scaling:
         self.capacity = capacity
         self.margin = float(margin)
         self.sites: dict = {}
+        self._views: dict = {}
         self.steps = 0
         # e5m2 sites of the backward (dY of the fp8 weight gradients); margin 2: a
         # gradient may grow between steps, saturating costs more than one bit of range
@@ -53,6 +54,9 @@ class Fp8Scaling:
     def site(self, key, init_from: torch.Tensor | None = None):
         """(scale [1], amax [64 slots]) views for ``key``; a new weight site takes
         its first scale from the tensor's current amax (device op, no sync)."""
+        v = self._views.get(key)
+        if v is not None:                   # hot path: no tensor slicing per call
+            return v
         idx = self.sites.get(key)
         if idx is None:
             idx = len(self.sites)
@@ -62,7 +66,8 @@ class Fp8Scaling:
             if init_from is not None:
                 a = init_from.detach().abs().max().float().clamp_min(1e-12)
                 self.scale[idx:idx + 1].copy_((self.fmax / self.margin) / a)
-        return self.scale[idx:idx + 1], self.amax[idx]
+        v = self._views[key] = (self.scale[idx:idx + 1], self.amax[idx])
+        return v
 
     @torch.no_grad()
     def update(self):

@@ -177,17 +177,21 @@ def _fp8_for(P):
 
 # Which convs run their forward in fp8 (the BN-apply feeding a bf16 conv skips its
 # e4m3 copy).  The fp8 gain of a conv has to pay for that copy (1 B per input element):
-#   PMD_FP8_CONVS=spatial (default): the R x S > 1 convs (3x3), which run 1.2-1.4x
+#   PMD_FP8_CONVS=spatial (default with PMD_FP8_WGRAD=0): the R x S > 1 convs (3x3), which run 1.2-1.4x
 #     faster in fp8 (790-1,144 vs 600-856 TFLOP/s) and read a 64-512-channel input;
 #     the 1x1 convs save less than their e4m3 input copy costs (conv_bench per-layer
 #     table in profiles/fp8_ring_depth_r02_rejected.txt);
-#   PMD_FP8_CONVS=all: every block conv whose reduction Kg = R*S*Cin fills one 128-deep
+#   PMD_FP8_CONVS=all (default): every block conv whose reduction Kg = R*S*Cin fills one 128-deep
 #     e4m3 K-tile (PMD_FP8_MIN_KG, default 128; 0 = every block conv).
-FP8_CONVS = os.environ.get("PMD_FP8_CONVS", "spatial")
-FP8_MIN_KG = int(os.environ.get("PMD_FP8_MIN_KG", "128"))
 # fp8 weight gradients (e5m2 dY x e4m3 X) for every conv whose forward ran in fp8; the
 # bf16 copy of a stage activation is then not written at all (PMD_FP8_WGRAD=0: bf16 wgrads)
 FP8_WGRAD = os.environ.get("PMD_FP8_WGRAD", "1") != "0"
+# With fp8 weight gradients the e4m3 input copy also halves the wgrad's activation bytes and
+# runs it at the fp8 MFMA rate, so every eligible block conv pays ("all": 13,217 / 13,193 vs
+# "spatial" 12,961 / 13,007 vs bf16 12,578 / 12,609 img/s, one lease, round 3); without them
+# only the 3x3 convs do (round 2: profiles/fp8_policy_ab_r02.txt).
+FP8_CONVS = os.environ.get("PMD_FP8_CONVS", "all" if FP8_WGRAD else "spatial")
+FP8_MIN_KG = int(os.environ.get("PMD_FP8_MIN_KG", "128"))
 
 
 def fp8_eligible(conv_m, cin) -> bool:
@@ -936,7 +940,8 @@ class _ResidualBlockFn(torch.autograd.Function):
         # (+ its scale) for an e5m2 x e4m3 wgrad, and a stage activation consumed only by
         # such a conv is written in e4m3 alone (no bf16 copy: h is then the uint8 tensor,
         # used for its shape)
-        f8w = f8 is not None and training and FP8_WGRAD and torch.is_grad_enabled()
+        # (grad mode is off inside Function.forward: ask the node whether a backward follows)
+        f8w = f8 is not None and training and FP8_WGRAD and any(ctx.needs_input_grad)
 
         def used_q(conv_m, hq_, h_):
             return hq_ if (hq_ is not None and fp8_eligible(conv_m, h_.shape[-1])) else None
