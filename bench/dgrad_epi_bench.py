@@ -63,6 +63,8 @@ def main():
     ap.add_argument("--tx", action="store_true",
                     help="also time the BN-backward-on-load (TX) variant: dY given as (dzm, y, coef), "
                          "against bn_bwd_elemt + the plain fused dgrad, and the TX wgrad vs the wgrad")
+    ap.add_argument("--fp8", action="store_true",
+                    help="also time the fp8 dgrad (e5m2 dY x e4m3 transposed weights) with the same epilogue")
     ap.add_argument("--impl", type=int, default=5,
                     help="conv_set_impl staging (0 = register staging, 1 = LDS-DMA BK=64, 5 = per shape)")
     a = ap.parse_args()
@@ -107,6 +109,21 @@ def main():
             HP.conv_dgrad(dy, wp, xshape, 1, 0)
         t = timeit(run, a.iters)
         tp = timeit(plain, a.iters)
+        f8s = ""
+        if a.fp8:
+            sdy = torch.tensor([1.0], device=dev)
+            sw = torch.tensor([64.0], device=dev)
+            dyq = _C.quant_bf16_fp8(dy, sdy, None, bf8=True)
+            _, wtq = _C.quant_weight_fp8_t(w, C, sw, None)
+
+            def run8():
+                if nsets:
+                    _, rr = HP.conv_dgrad_fp8(dyq, sdy, wtq, sw, xshape, 1, 0, addend, bnred=(mk, sets),
+                                              addend_mask=am)
+                    HP._release(*rr)
+                else:
+                    HP.conv_dgrad_fp8(dyq, sdy, wtq, sw, xshape, 1, 0, addend, addend_mask=am)
+            f8s = f" | fp8 {timeit(run8, a.iters) * 1e3:7.1f}"
         if a.tx:
             from pytorch_multiprocessing_distributed_amd.ops.lazy import LazyDy
             yk = torch.randn(N, H, H, K, device=dev, generator=g).to(torch.bfloat16)
@@ -151,7 +168,7 @@ def main():
               + nsets * M * C * 2 + (M * C // 8 if nsets else 0)) / 1e9
         gbp = (M * K * 2 + M * C * 2) / 1e9
         print(f"{name:>12} {M:>8} {C:>5} {K:>4} {nsets:>4} | {t * 1e3:7.1f} {gb:6.3f} {gb / t:5.2f} "
-              f"| {tp * 1e3:7.1f} {gbp / tp:5.2f}", flush=True)
+              f"| {tp * 1e3:7.1f} {gbp / tp:5.2f}{f8s}", flush=True)
         tot_us += cnt * t * 1e3
         tot_ideal += cnt * gb / 6.0 * 1e3   # at ~6 TB/s achievable HBM
         del dy, addend, sets, am, mk

@@ -1,8 +1,8 @@
-"""FP8 vs bf16 weight gradient per ResNet-50 layer (batch 256): the e5m2 x e4m3
-scaled-MFMA kernel (conv_wgrad_fp8) against the bf16 kernel the tuner picks
-(conv_wgrad), median us and TFLOP/s, split reduce included in both.
+"""FP8 vs bf16 weight (or, --dgrad, data) gradient per ResNet-50 layer (batch 256):
+the e5m2 x e4m3 scaled-MFMA kernel (conv_wgrad_fp8 / conv_dgrad_fp8) against the bf16
+kernel the tuner picks, median us and TFLOP/s, split reduce included for the wgrads.
 
-    python bench/wgrad_fp8_bench.py [--iters 20] [--only 3x3|1x1]
+    python bench/wgrad_fp8_bench.py [--iters 20] [--only 3x3|1x1] [--dgrad]
 """
 import argparse
 import os
@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--only", default="")
+    ap.add_argument("--dgrad", action="store_true", help="time the data gradients instead")
     a = ap.parse_args()
     from pytorch_multiprocessing_distributed_amd.ops import tuning
     tuning.load_default()
@@ -59,6 +60,17 @@ def main():
         dw = torch.zeros(K, R, R, Cin, device="cuda")
         b = timeit(lambda: C.conv_wgrad(dy, x, R, R, st, pad, dw), a.iters)
         f = timeit(lambda: C.conv_wgrad_fp8(dyq, xq, sdy, sx, R, R, st, pad, dw), a.iters)
+        if a.dgrad:
+            # plain data gradients (no epilogue): the tuned bf16 kernel vs the fp8 one
+            from pytorch_multiprocessing_distributed_amd.ops import hip_prims as HP
+            w = (torch.randn(K, Cin, R, R, device="cuda") / (Cin * R * R) ** 0.5).contiguous(
+                memory_format=torch.channels_last)
+            wp = HP.conv_weight(w, torch.bfloat16, Cin, True)
+            sw = torch.tensor([64.0], device="cuda")
+            _, wtq = C.quant_weight_fp8_t(w, Cin, sw, None)
+            xs = (a.batch, H, H, Cin)
+            b = timeit(lambda: HP.conv_dgrad(dy, wp, xs, st, pad), a.iters)
+            f = timeit(lambda: HP.conv_dgrad_fp8(dyq, sdy, wtq, sw, xs, st, pad), a.iters)
         fl = 2.0 * a.batch * P * P * K * R * R * Cin
         tb += b
         tf += f

@@ -322,6 +322,67 @@ Tensor conv_dgrad(Tensor dy, Tensor wkt, int64_t H, int64_t W, int64_t stride, i
   return dx;
 }
 
+// FP8 dgrad: dx[N,H,W,Cp] (bf16) from e5m2 dyq[N,P,Q,K] (scale sdy) and the e4m3 transposed
+// weight image wtq[Cp,R,S,K] (scale sw); addend / fused BN reduce as conv_dgrad
+Tensor conv_dgrad_fp8(Tensor dyq, Tensor wtq, Tensor sdy, Tensor sw, int64_t H, int64_t W, int64_t stride,
+                      int64_t pad, c10::optional<Tensor> addend, c10::optional<Tensor> bn_mask,
+                      c10::optional<Tensor> bn_y0, c10::optional<Tensor> bn_p0, c10::optional<Tensor> bn_red0,
+                      c10::optional<Tensor> bn_y1, c10::optional<Tensor> bn_p1, c10::optional<Tensor> bn_red1,
+                      c10::optional<Tensor> addend_mask) {
+  CHECK_DEV(dyq); CHECK_CONT(dyq); CHECK_DEV(wtq); CHECK_CONT(wtq);
+  TORCH_CHECK(dyq.scalar_type() == torch::kUInt8 && wtq.scalar_type() == torch::kUInt8,
+              "conv_dgrad_fp8: e5m2 dY / e4m3 weight image as uint8");
+  CHECK_F32(sdy); CHECK_F32(sw);
+  const int N = dyq.size(0), P = dyq.size(1), Q = dyq.size(2), K = dyq.size(3);
+  const int Cp = wtq.size(0), R = wtq.size(1), S = wtq.size(2);
+  TORCH_CHECK(wtq.size(3) == K, "dgrad weight/K mismatch");
+  TORCH_CHECK((H + 2 * pad - R) / stride + 1 == P && (W + 2 * pad - S) / stride + 1 == Q,
+              "dgrad spatial mismatch");
+  c10::DeviceGuard g(dyq.device());
+  Tensor dx = torch::empty({N, H, W, Cp}, dyq.options().dtype(torch::kBFloat16));
+  const pmd::bf16_t* add = nullptr;
+  if (addend && addend->defined()) {
+    CHECK_BF16(*addend); CHECK_CONT(*addend);
+    TORCH_CHECK(addend->sizes() == dx.sizes(), "addend shape");
+    add = bfp(*addend);
+  }
+  const uint8_t* amask = nullptr;
+  if (addend_mask && addend_mask->defined()) {
+    TORCH_CHECK(add, "addend_mask needs an addend");
+    TORCH_CHECK(addend_mask->scalar_type() == torch::kUInt8 && addend_mask->is_contiguous() &&
+                addend_mask->numel() == dx.numel() / 8, "addend_mask must be uint8 [M, C/8]");
+    amask = addend_mask->data_ptr<uint8_t>();
+  }
+  pmd::BnReduceArgs bnr{};
+  const bool fused = bn_red0 && bn_red0->defined();
+  if (fused) {
+    auto chk_set = [&](const c10::optional<Tensor>& y, const c10::optional<Tensor>& p,
+                       const c10::optional<Tensor>& r, int t) {
+      TORCH_CHECK(y && y->defined() && p && p->defined() && r && r->defined(), "bn reduce set incomplete");
+      CHECK_BF16(*y); CHECK_CONT(*y); CHECK_F32(*p); CHECK_F32(*r); CHECK_CONT(*r); CHECK_CONT(*p);
+      TORCH_CHECK(y->sizes() == dx.sizes(), "bn reduce: y must match dx");
+      TORCH_CHECK(p->numel() == 4 * Cp, "bn reduce: params must be [4, C]");
+      TORCH_CHECK(r->numel() == pmd_slots() * 2 * Cp, "bn reduce: red must be [slots, 2, C]");
+      bnr.y[t] = bfp(*y);
+      bnr.p[t] = p->data_ptr<float>();
+      bnr.red[t] = r->data_ptr<float>();
+    };
+    chk_set(bn_y0, bn_p0, bn_red0, 0);
+    if (bn_red1 && bn_red1->defined()) chk_set(bn_y1, bn_p1, bn_red1, 1);
+    if (bn_mask && bn_mask->defined()) {
+      TORCH_CHECK(bn_mask->scalar_type() == torch::kUInt8 && bn_mask->is_contiguous() &&
+                  bn_mask->numel() == dx.numel() / 8, "bn reduce: mask must be uint8 [M, C/8]");
+      bnr.mask = bn_mask->data_ptr<uint8_t>();
+    }
+  }
+  const int rc = pmd::conv_dgrad_fp8_launch(dyq.data_ptr<uint8_t>(), wtq.data_ptr<uint8_t>(), sdy.data_ptr<float>(),
+                                            sw.data_ptr<float>(), bfp_mut(dx), N, P, Q, K, (int)H, (int)W, Cp, R, S,
+                                            (int)stride, (int)pad, add, amask, fused ? &bnr : nullptr,
+                                            cur_stream());
+  CHECK_RC(rc, "conv_dgrad_fp8");
+  return dx;
+}
+
 // out: optional [K,R,S,C] fp32 accumulation target (e.g. a grad-arena view); dW is ADDED to it
 Tensor conv_wgrad(Tensor dy, Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad,
                   c10::optional<Tensor> out, c10::optional<Tensor> tx_y, c10::optional<Tensor> tx_coef) {
@@ -585,12 +646,14 @@ std::vector<Tensor> bn_bwd_elemt(Tensor dout, c10::optional<Tensor> mask, Tensor
                                  Tensor gamma, c10::optional<Tensor> red,
                                  c10::optional<Tensor> count, double count_h, bool relu,
                                  bool want_dzm, bool eval_mode, c10::optional<Tensor> q8_scale,
-                                 c10::optional<Tensor> q8_amax) {
+                                 c10::optional<Tensor> q8_amax, bool q8_only) {
   CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONT(dout);
   const int C = dout.size(-1);
   const long long M = dout.numel() / C;
   c10::DeviceGuard g(dout.device());
-  Tensor dy = torch::empty_like(dout);
+  TORCH_CHECK(!q8_only || (q8_scale && q8_scale->defined()), "q8_only needs the e5m2 output");
+  // q8_only: only the e5m2 copy is written (returned dy is None)
+  Tensor dy = q8_only ? Tensor() : torch::empty_like(dout);
   Tensor dzm;
   if (want_dzm) dzm = torch::empty_like(dout);
   Tensor rr, cc, gm = gamma.contiguous();
@@ -613,7 +676,7 @@ std::vector<Tensor> bn_bwd_elemt(Tensor dout, c10::optional<Tensor> mask, Tensor
   const int rc = pmd::bn_bwd_elemt_launch(
       bfp(dout), mask_ptr(mask, M * (C / 8), relu), eval_mode ? nullptr : bfp(y), params.data_ptr<float>(), gm.data_ptr<float>(),
       eval_mode ? nullptr : rr.data_ptr<float>(),
-      (eval_mode || !cc.defined()) ? nullptr : cc.data_ptr<float>(), (float)count_h, bfp_mut(dy), want_dzm ? bfp_mut(dzm) : nullptr, M, C, relu, eval_mode, cur_stream(),
+      (eval_mode || !cc.defined()) ? nullptr : cc.data_ptr<float>(), (float)count_h, q8_only ? nullptr : bfp_mut(dy), want_dzm ? bfp_mut(dzm) : nullptr, M, C, relu, eval_mode, cur_stream(),
       q8 ? q.data_ptr<uint8_t>() : nullptr, q8 ? q8_scale->data_ptr<float>() : nullptr,
       q8 ? q8_amax->data_ptr<float>() : nullptr);
   CHECK_RC(rc, "bn_bwd_elemt");
@@ -805,7 +868,13 @@ Tensor quant_bf16_fp8(Tensor x, Tensor scale, c10::optional<Tensor> amax, bool b
   return q;
 }
 
+std::vector<Tensor> quant_weight_fp8_t(Tensor w, int64_t cp, Tensor scale, c10::optional<Tensor> amax);
 Tensor quant_weight_fp8(Tensor w, int64_t cp, Tensor scale, c10::optional<Tensor> amax) {
+  return quant_weight_fp8_t(w, cp, scale, amax)[0];
+}
+
+// -> [q [K,R,S,cp], qt [cp,R,S,K]]: the forward image and the fp8 dgrad's transposed image
+std::vector<Tensor> quant_weight_fp8_t(Tensor w, int64_t cp, Tensor scale, c10::optional<Tensor> amax) {
   CHECK_DEV(w); CHECK_F32(w); CHECK_F32(scale);
   TORCH_CHECK(w.dim() == 4, "weight must be [K,C,R,S]");
   const int K = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
@@ -813,12 +882,14 @@ Tensor quant_weight_fp8(Tensor w, int64_t cp, Tensor scale, c10::optional<Tensor
   c10::DeviceGuard g(w.device());
   Tensor wphys = w.permute({0, 2, 3, 1}).contiguous();
   Tensor q = torch::empty({K, R, S, cp}, w.options().dtype(torch::kUInt8));
+  Tensor qt = torch::empty({cp, R, S, K}, w.options().dtype(torch::kUInt8));
   float* am = (amax && amax->defined()) ? amax->data_ptr<float>() : nullptr;
   TORCH_CHECK(!am || (amax->numel() >= 64 && amax->is_contiguous()), "amax must be [64] slots");
   CHECK_RC(pmd::quant_weight_fp8_launch(wphys.data_ptr<float>(), q.data_ptr<uint8_t>(),
-                                        scale.data_ptr<float>(), am, K, R * S, C, (int)cp, cur_stream()),
+                                        scale.data_ptr<float>(), am, K, R * S, C, (int)cp, cur_stream(),
+                                        qt.data_ptr<uint8_t>()),
            "quant_weight_fp8");
-  return q;
+  return {q, qt};
 }
 
 // Fp8Scaling.update(): amax [capacity, kAmaxSlots] fp32, scale [capacity] fp32, first n sites
@@ -1008,7 +1079,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd_elemt", &bn_bwd_elemt, py::arg("dout"), py::arg("mask"), py::arg("y"), py::arg("params"),
         py::arg("gamma"), py::arg("red"), py::arg("count"), py::arg("count_h"), py::arg("relu"),
         py::arg("want_dzm"), py::arg("eval_mode"), py::arg("q8_scale") = py::none(),
-        py::arg("q8_amax") = py::none());
+        py::arg("q8_amax") = py::none(), py::arg("q8_only") = false);
   m.def("bn_bwd_coef", &bn_bwd_coef);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
@@ -1028,6 +1099,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cifar_augment", &cifar_augment);
   m.def("quant_bf16_fp8", &quant_bf16_fp8, py::arg("x"), py::arg("scale"), py::arg("amax") = py::none(),
         py::arg("bf8") = false);
+  m.def("quant_weight_fp8_t", &quant_weight_fp8_t);
+  m.def("conv_dgrad_fp8", &conv_dgrad_fp8, py::arg("dyq"), py::arg("wtq"), py::arg("sdy"), py::arg("sw"),
+        py::arg("H"), py::arg("W"), py::arg("stride"), py::arg("pad"), py::arg("addend") = py::none(),
+        py::arg("bn_mask") = py::none(), py::arg("bn_y0") = py::none(), py::arg("bn_p0") = py::none(),
+        py::arg("bn_red0") = py::none(), py::arg("bn_y1") = py::none(), py::arg("bn_p1") = py::none(),
+        py::arg("bn_red1") = py::none(), py::arg("addend_mask") = py::none());
   m.def("conv_wgrad_fp8", &conv_wgrad_fp8, py::arg("dyq"), py::arg("xq"), py::arg("sdy"), py::arg("sx"),
         py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("out") = py::none());
   m.def("quant_weight_fp8", &quant_weight_fp8);

@@ -315,7 +315,9 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(
         o[k] = EVAL ? ca[k] * dz : ca[k] * dz + cb[k] * v[k] + cc[k];
       }
       const uint4 pk = pack8(o);
-      st16(reinterpret_cast<uint4*>(dy) + i, pk);
+      // Q8 with dy == nullptr: the e5m2 copy is the only dY (every consumer -- the fp8
+      // wgrad and the fp8 dgrad -- reads it)
+      if (!Q8 || dy) st16(reinterpret_cast<uint4*>(dy) + i, pk);
       if (DZM) st16(reinterpret_cast<uint4*>(dzm_out) + i, pack8(d));
       if (Q8) {
         float r[8], c[8];

@@ -32,6 +32,7 @@
 #include <map>
 #include <vector>
 #include <mutex>
+#include <type_traits>
 
 namespace pmd {
 
@@ -67,7 +68,12 @@ struct ConvArgs {
   const bf16_t* tx_y;
   const float* tx_coef;
   int tx_cp;
+  // F8 (fp8 dgrad, BASELINE config 5): src is e5m2 dY and wt an e4m3 [Nout][Kg] image
+  // (byte pointers behind the bf16_t* fields); acc is scaled by 1 / (f8_sa * f8_sb)
+  const float* f8_sa;
+  const float* f8_sb;
 };
+typedef __attribute__((ext_vector_type(8))) int i32x8_c;
 
 constexpr int LDA_REG = 64 + 8;  // padded LDS row of the register-staged path (elements)
 
@@ -149,11 +155,19 @@ __device__ __forceinline__ int swz(int row) {
 // 1x1 only: a zero-filled (padded) A chunk would become c[k], not 0; a 1x1 dgrad has
 // no padded taps, and K-tile tails read zero coefficients.
 template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA, bool MF32 = false,
-          int WM = 2, int WN = 2, bool P8 = false, bool HALO = false, int NB = 2, bool TX = false>
+          int WM = 2, int WN = 2, bool P8 = false, bool HALO = false, int NB = 2, bool TX = false,
+          bool F8 = false, int NST1 = 0>
 __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) void conv_igemm_kernel(ConvArgs a) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   static_assert(!TX || (DGRAD && DMA && !MF32 && !P8 && !HALO), "TX: DMA dgrad, 16x16 MFMA, plain pipeline");
   static_assert(DMA || (BK == 64 && NST == 2 && NW == 4), "register staging: BK=64, 2 stages, 4 waves");
+  // F8: fp8 operands (1 B per element) in the same 128-B LDS rows (BK = 64 bf16 slots =
+  // 128 fp8 reduction elements per K-tile), one v_mfma_scale_f32_16x16x128_f8f6f4 per
+  // fragment pair and K-tile; NST1: a single LDS stage (load, wait, compute) for the
+  // one- or two-K-tile reductions of the epilogue-bound dgrads (occupancy of the bf16 BK=32
+  // tiles: 4 blocks per CU)
+  static_assert(!F8 || (DMA && BK == 64 && !MF32 && !P8 && !HALO && !TX), "F8: LDS-DMA, 128-B rows, plain pipeline");
+  static_assert(!NST1 || (F8 && NST == 2), "NST1: fp8 only");
   static_assert(!MF32 || (DMA && BK == 64), "32x32 MFMA path: LDS-DMA, BK=64");
   static_assert(!P8 || (DMA && BK == 64 && NST == 2 && !MF32), "P8: LDS-DMA, BK=64, 2 buffers, 16x16 MFMA");
   static_assert(!HALO || (DMA && BK == 64 && (NST == 2 || NST == 3) && !MF32 && !P8),
@@ -165,6 +179,11 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
   // per-channel sums need 4x fewer cross-lane steps)
   constexpr bool SWAPC = PMD_CONV_SWAPC && !STATS && !MF32;
   constexpr int CH = BK / 8;                      // 16-B chunks per LDS row
+  constexpr int CE = F8 ? 16 : 8;                 // reduction elements per 16-B chunk
+  constexpr int BKE = F8 ? 2 * BK : BK;           // reduction elements per K-tile
+  using ET = typename std::conditional<F8, uint8_t, bf16_t>::type;
+  const ET* const srcE = reinterpret_cast<const ET*>(a.src);
+  const ET* const wtE = reinterpret_cast<const ET*>(a.wt);
   constexpr int RPI = DMA ? 64 / CH : 32;         // rows per load instruction (wave / block)
   constexpr int PA = DMA ? BM / (NW * RPI) : BM / 32;  // A load instructions per thread per tile
   constexpr int PB = DMA ? BN / (NW * RPI) : BN / 32;
@@ -197,7 +216,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
   constexpr int HALO_PIX = 348;
   constexpr int HALO_CHUNKS = ((HALO_PIX * 8 + NT - 1) / NT) * NT;
   constexpr int HALO_BYTES = HALO ? HALO_CHUNKS * 16 : 0;
-  constexpr int SMEM_MAIN = HALO ? HALO_BYTES + NST * B_ELEMS * 2 : NST * STAGE * 2;
+  constexpr int SMEM_MAIN = HALO ? HALO_BYTES + NST * B_ELEMS * 2 : (NST1 ? 1 : NST) * STAGE * 2;
   constexpr int SMEM_EPI = BM * LDC * 2;
   constexpr int PSTR = 17;                          // fused BN-reduce partials [NT][17] (odd stride)
   constexpr int SMEM_PART = DGRAD ? NT * PSTR * 4 : 0;
@@ -282,13 +301,13 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
       a_w[i] = ow * a.stride - a.pad;
     }
   }
-  const bf16_t* b_row[PB];
+  const ET* b_row[PB];
   bool b_ok[PB];
 #pragma unroll
   for (int i = 0; i < PB; ++i) {
     const int nn = n0 + b_row_of(i);
     b_ok[i] = nn < a.Nout;
-    b_row[i] = a.wt + (size_t)(b_ok[i] ? nn : 0) * a.Kg;
+    b_row[i] = wtE + (size_t)(b_ok[i] ? nn : 0) * a.Kg;
   }
   // Uniform-tap fast path (LDS-DMA, Cs % BK == 0 -- every layer but the stem):
   // a K-tile then lies inside ONE filter tap, so the tap (r, s) and its pixel
@@ -296,7 +315,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
   //   ih = u_h + dr, iw = u_w + ds, pix = u_p + dr*W + ds   (dr, ds scalars)
   // with (dr, ds) = (r, s) fwd, (-r, -s) stride-1 dgrad, (-tr, -ts) stride-2
   // dgrad (the phase fixes r = r0 + 2 tr, so (h + pad - r) / 2 = u_h - tr).
-  const bool uni = DMA && a.Cs >= BK;
+  const bool uni = DMA && a.Cs >= BKE;
   int u_h[PA], u_w[PA], u_p[PA];
 #pragma unroll
   for (int i = 0; i < PA; ++i) {
@@ -316,7 +335,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
   const int wid_s = __builtin_amdgcn_readfirstlane(wid);
 
   uint4 ra[DMA ? 1 : PA], rb[DMA ? 1 : PB];
-  const int nk = (Kgp + BK - 1) / BK;
+  const int nk = (Kgp + BKE - 1) / BKE;
 
   // Tap state of the NEXT K-tile the uniform loader issues.  K-tiles are issued
   // strictly in order (prologue 0..NST-2, then kt+NST-1), and with Cs >= BK a
@@ -325,13 +344,13 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
   int u_cb = 0, u_tr = 0, u_ts = 0, u_kt = 0;
   // per-row source pointers at tap (0,0) channel 0 (+ this lane's chunk); a tile
   // then only adds the wave-uniform offset (dr*W + ds)*Cs + cb
-  const bf16_t* a_ptr[PA];
+  const ET* a_ptr[PA];
   const bf16_t* y_ptr[TX ? PA : 1];
 #pragma unroll
   for (int i = 0; i < PA; ++i) {
-    const int ci = MF32 ? lane_c32[i & 1] : achunk(i) * 8;
+    const int ci = MF32 ? lane_c32[i & 1] : achunk(i) * CE;
     // signed: u_p is -1.. at padded borders (never dereferenced there: `ok` masks it)
-    a_ptr[i] = a.src + ((long long)u_p[i] << a.log2Cs) + ci;
+    a_ptr[i] = srcE + ((long long)u_p[i] << a.log2Cs) + ci;
     if constexpr (TX) y_ptr[i] = a.tx_y + ((long long)u_p[i] << a.log2Cs) + ci;
   }
   auto load_tile_uni = [&](int kt, int dbuf) {
@@ -367,7 +386,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
     }
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
-      const int boff = tapo + (MF32 ? lane_c32[i & 1] : bchunk(i) * 8);
+      const int boff = tapo + (MF32 ? lane_c32[i & 1] : bchunk(i) * CE);
       const void* src = (b_ok[i] && kok) ? (const void*)(b_row[i] + boff) : (const void*)g_zero16;
       bf16_t* dst = lds + dbuf * STAGE + A_ELEMS + (wid_s * (BN / NW) + RPI * i) * LDR;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
@@ -375,7 +394,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
     }
     // advance to the next K-tile: channel block, then tap column, then tap row
     ++u_kt;
-    u_cb += BK;
+    u_cb += BKE;
     if (u_cb == a.Cs) {
       u_cb = 0;
       if (++u_ts == ns) {
@@ -388,7 +407,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
   auto load_tile = [&](int kt, int dbuf) {
 #pragma unroll
     for (int i = 0; i < PA; ++i) {
-      const int k0 = kt * BK + achunk(i) * 8;
+      const int k0 = kt * BKE + achunk(i) * CE;
       const bool kok = k0 < Kgp;
       const int tap = k0 >> a.log2Cs;
       const int c = k0 & (a.Cs - 1);
@@ -409,7 +428,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
       ok = ok && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
       if constexpr (DMA) {
         const void* src = g_zero16;
-        if (ok) src = a.src + (((size_t)(a_base[i] + ih * a.W + iw)) << a.log2Cs) + c;
+        if (ok) src = srcE + (((size_t)(a_base[i] + ih * a.W + iw)) << a.log2Cs) + c;
         bf16_t* dst = lds + dbuf * STAGE + (wid * (BM / NW) + RPI * i) * LDR;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
@@ -431,7 +450,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
     }
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
-      const int k0 = kt * BK + bchunk(i) * 8;
+      const int k0 = kt * BKE + bchunk(i) * CE;
       const bool kok = k0 < Kgp;
       const int tap = k0 >> a.log2Cs;
       const int tr = tap / ns;
@@ -492,6 +511,58 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
     (void)kt;
     const bf16_t* As = lds + buf * STAGE;
     const bf16_t* Bs = lds + buf * STAGE + A_ELEMS;
+    if constexpr (F8) {
+      // lane l holds row l & 15, reduction bytes 32 (l >> 4) .. +31 = logical chunks q0, q0+1
+      const int q0 = 2 * (lane >> 4);
+      auto frag8 = [&](const bf16_t* base, int r) {
+        const uint4 lo = *reinterpret_cast<const uint4*>(base + r * LDR + ((q0 ^ swz<BK>(r)) << 3));
+        const uint4 hi = *reinterpret_cast<const uint4*>(base + r * LDR + (((q0 + 1) ^ swz<BK>(r)) << 3));
+        i32x8_c v;
+        v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+        v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+        return v;
+      };
+      // the B fragments stay in registers, the A fragments stream one at a time: a 32-B
+      // fragment is 8 VGPRs, and holding all MI + NI of them (64) would cost the fused-
+      // epilogue dgrads a wave per SIMD (154 VGPRs -> 3 waves; the epilogue needs 4)
+      // formats: the gathered operand is e5m2 (bf8) in dgrad (dY), e4m3 in fwd; weights e4m3
+      constexpr int FA = DGRAD ? 1 : 0;
+      if constexpr (NST1) {
+        // single-stage (short-reduction, epilogue-bound) variant: ONE A and ONE B fragment
+        // live at a time (the A fragments are re-read NI times from LDS -- 1-4 K-tiles per
+        // block, negligible) so the kernel stays at 4 waves per SIMD like the bf16 one
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const i32x8_c bf = frag8(Bs, wn * (BN / WN) + j * 16 + frow);
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            const i32x8_c af = frag8(As, wm * (BM / WM) + i * 16 + frow);
+            acc[i][j] = SWAPC ? __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bf, af, acc[i][j], 0, FA, 0, 127,
+                                                                                0, 127)
+                              : __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bf, acc[i][j], FA, 0, 0, 127,
+                                                                                0, 127);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+        return;
+      }
+      i32x8_c bfg[NI];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) bfg[j] = frag8(Bs, wn * (BN / WN) + j * 16 + frow);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const i32x8_c af = frag8(As, wm * (BM / WM) + i * 16 + frow);
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = SWAPC ? __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfg[j], af, acc[i][j], 0, FA, 0,
+                                                                              127, 0, 127)
+                            : __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bfg[j], acc[i][j], FA, 0, 0,
+                                                                              127, 0, 127);
+        // keep the scheduler from hoisting the next A fragment's reads above these MFMAs
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      return;
+    }
     if constexpr (MF32) {
       const int r32 = lane & 31;
 #pragma unroll
@@ -563,6 +634,17 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
   if constexpr (DMA) {
     // the loader choice is hoisted out of the K loop: one loop instance per loader
     auto pipeline = [&](auto&& load) {
+    if constexpr (NST1) {
+      // one LDS stage: load, wait, publish, compute, retire the reads before the next load
+      for (int kt = 0; kt < nk; ++kt) {
+        if (kt) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        load(kt, 0);
+        wait_vmcnt<0>();
+        asm volatile("s_barrier" ::: "memory");
+        compute(0, kt);
+      }
+      return;
+    }
     // prologue: tiles 0 .. NST-2 in flight
 #pragma unroll
     for (int t = 0; t < NST - 1; ++t)
@@ -776,6 +858,15 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
       else pipeline(load_tile);
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr (F8) {
+      const float dsc = 1.f / (a.f8_sa[0] * a.f8_sb[0]);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][e] *= dsc;
+    }
   } else {
     if (nk > 0) {
       load_tile(0, 0);
@@ -1606,6 +1697,8 @@ static int conv_igemm_launch_b(const bf16_t* src, const bf16_t* wt, bf16_t* out,
   a.tx_y = nullptr;
   a.tx_coef = nullptr;
   a.tx_cp = 0;
+  a.f8_sa = nullptr;
+  a.f8_sb = nullptr;
   if (tx && tx->y) {
     // BN backward on load: 1x1 dgrads only (see the TX note), coefficients cover every K-tile
     if (!dgrad || R != 1 || S != 1 || pad != 0 || batch != 1 || !tx->coef || tx->cp < (Cs + 31) / 32 * 32)
@@ -1623,6 +1716,70 @@ static int conv_igemm_launch_b(const bf16_t* src, const bf16_t* wt, bf16_t* out,
   } else {
     if (stats) launch_sel<false, true>(a, st);
     else launch_sel<false, false>(a, st);
+  }
+  return 0;
+}
+
+// ---- FP8 dgrad (config 5): e5m2 dY x e4m3 [Cp][R][S][K] weight image, the bf16 kernel's
+// dgrad epilogue (addend + mask, fused BN-backward reduce), fixed tile policy (no tuner):
+// 128x64 for 64-channel outputs, 128x128 otherwise, a single LDS stage when the whole
+// reduction is <= 4 K-tiles (the epilogue-bound short-reduction dgrads keep 4 blocks / CU)
+template <int BM, int BN, bool ONE>
+static void launch_f8(const ConvArgs& a, hipStream_t st) {
+  const bool ph2 = a.stride == 2;
+  const int Mgrid = ph2 ? a.N * ((a.OH + 1) >> 1) * ((a.OW + 1) >> 1) : a.M;
+  const int tiles = ((Mgrid + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
+  const dim3 grid(tiles, ph2 ? 4 : 1, 1), block(256);
+  const int nb = a.bn_red[0] ? (a.bn_red[1] ? 2 : 1) : 0;
+#define F8K(NBV) \
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 64, 2, true, false, true, false, 2, 2, false, false, NBV, false, true, \
+                                        ONE ? 1 : 0>), grid, block, 0, st, a)
+  if (nb == 2) F8K(2);
+  else if (nb == 1) F8K(1);
+  else F8K(0);
+#undef F8K
+}
+
+int conv_dgrad_fp8_launch(const uint8_t* dyq, const uint8_t* wtq, const float* sdy, const float* sw, bf16_t* out,
+                          int N, int H, int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
+                          const bf16_t* addend, const uint8_t* addend_mask, const BnReduceArgs* bnr,
+                          hipStream_t st) {
+  // dgrad view: gathered operand dY [N, H, W, Cs] (H x W = the conv's output grid), output [N, OH, OW, Nout]
+  if (Cs % 16 != 0 || (Cs & (Cs - 1)) != 0) return 1;  // a 16-B chunk = 16 channels of one tap
+  if (Nout % 8 != 0) return 2;
+  if (stride != 1 && stride != 2) return 3;
+  ConvArgs a{};
+  a.batch = 1;
+  a.src = reinterpret_cast<const bf16_t*>(dyq);
+  a.wt = reinterpret_cast<const bf16_t*>(wtq);
+  a.out = out;
+  a.addend = addend;
+  a.addend_mask = addend ? addend_mask : nullptr;
+  if (bnr) {
+    if (!bnr->y[0] || !bnr->p[0] || !bnr->red[0]) return 5;
+    a.bn_mask = bnr->mask;
+    for (int t = 0; t < 2; ++t) {
+      a.bn_y[t] = bnr->y[t];
+      a.bn_p[t] = bnr->p[t];
+      a.bn_red[t] = bnr->red[t];
+    }
+  }
+  a.N = N; a.H = H; a.W = W; a.Cs = Cs; a.log2Cs = ilog2(Cs);
+  a.OH = OH; a.OW = OW; a.Nout = Nout; a.R = R; a.S = S;
+  a.stride = stride; a.log2stride = ilog2(stride); a.pad = pad;
+  const long long M = (long long)N * OH * OW;
+  if (M >= (1ll << 31) || (long long)N * H * W >= (1ll << 31)) return 4;
+  a.M = (int)M;
+  a.Kg = R * S * Cs;
+  a.f8_sa = sdy;
+  a.f8_sb = sw;
+  const bool one = a.Kg <= 512;  // <= 4 K-tiles: the short-reduction, epilogue-bound dgrads
+  if (a.Nout <= 64) {
+    if (one) launch_f8<128, 64, true>(a, st);
+    else launch_f8<128, 64, false>(a, st);
+  } else {
+    if (one) launch_f8<128, 128, true>(a, st);
+    else launch_f8<128, 128, false>(a, st);
   }
   return 0;
 }

@@ -66,10 +66,11 @@ __global__ __launch_bounds__(256) void quant_bf16_fp8_kernel(const bf16_t* __res
   if (amax) block_amax_update(amax, m);
 }
 
-// fp32 master [K][RS][C] (channels_last physical) -> e4m3 [K][RS][Cp] (zero padded)
+// fp32 master [K][RS][C] (channels_last physical) -> e4m3 [K][RS][Cp] (zero padded), and
+// optionally the transposed image qt [Cp][RS][K] (the fp8 dgrad's B^T, same scale)
 __global__ void quant_weight_fp8_kernel(const float* __restrict__ w, uint8_t* __restrict__ q,
                                         const float* __restrict__ scale, float* __restrict__ amax,
-                                        int K, int RS, int C, int Cp) {
+                                        int K, int RS, int C, int Cp, uint8_t* __restrict__ qt) {
   const float s = scale[0];
   float m = 0.f;
   const int total = K * RS * Cp;
@@ -78,7 +79,12 @@ __global__ void quant_weight_fp8_kernel(const float* __restrict__ w, uint8_t* __
     const int krs = i / Cp;
     const float v = c < C ? w[(size_t)krs * C + c] : 0.f;
     m = fmaxf(m, fabsf(v));
-    q[i] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(v * s), 0.f, 0, false) & 0xff);
+    const uint8_t b = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(v * s), 0.f, 0, false) & 0xff);
+    q[i] = b;
+    if (qt) {
+      const int k = krs / RS, rs = krs - k * RS;
+      qt[((size_t)c * RS + rs) * K + k] = b;
+    }
   }
   if (amax) block_amax_update(amax, m);
 }
@@ -106,7 +112,12 @@ __global__ void quant_weight_fp8_grouped_kernel(const Fp8WeightDesc* __restrict_
     const int krs = i / d.Cp;
     const float v = c < d.C ? d.w[(size_t)krs * d.C + c] : 0.f;
     m = fmaxf(m, fabsf(v));
-    d.q[i] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(v * s), 0.f, 0, false) & 0xff);
+    const uint8_t b = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(v * s), 0.f, 0, false) & 0xff);
+    d.q[i] = b;
+    if (d.qt) {
+      const int k = krs / d.RS, rs = krs - k * d.RS;
+      d.qt[((size_t)c * d.RS + rs) * d.K + k] = b;
+    }
   }
   // block_amax_update picks slot blockIdx % kAmaxSlots of the weight's own site
   block_amax_update(d.amax, m);
@@ -190,9 +201,9 @@ int quant_bf16_fp8_launch(const bf16_t* x, uint8_t* q, const float* scale, float
 }
 
 int quant_weight_fp8_launch(const float* w, uint8_t* q, const float* scale, float* amax, int K, int RS,
-                            int C, int Cp, hipStream_t st) {
+                            int C, int Cp, hipStream_t st, uint8_t* qt) {
   hipLaunchKernelGGL(quant_weight_fp8_kernel, dim3(blocks_for((long long)K * RS * Cp, 256 * 16)), dim3(256), 0,
-                     st, w, q, scale, amax, K, RS, C, Cp);
+                     st, w, q, scale, amax, K, RS, C, Cp, qt);
   return 0;
 }
 

@@ -72,6 +72,12 @@ int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, float* ws, i
                       int C, int P, int Q, int K, int R, int S, int stride, int pad, hipStream_t st,
                       const TxArgs* tx = nullptr);
 // FP8 weight gradient: e5m2 dY x e4m3 X on the scaled 16x16x128 MFMA (kernels/conv_wgrad.hip)
+// FP8 data gradient: e5m2 dY [N,P,Q,K] x e4m3 wkt image [Cp][R][S][K] -> bf16 dX [N,H,W,Cp] with the
+// bf16 dgrad's epilogue (addend (+mask), fused BN-backward reduce) (kernels/conv_igemm.hip)
+int conv_dgrad_fp8_launch(const uint8_t* dyq, const uint8_t* wtq, const float* sdy, const float* sw, bf16_t* out,
+                          int N, int H, int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
+                          const bf16_t* addend, const uint8_t* addend_mask, const BnReduceArgs* bnr,
+                          hipStream_t st);
 int conv_wgrad_fp8_splits(int N, int H, int W, int C, int P, int Q, int K, int R, int S, int stride, int pad);
 int conv_wgrad_fp8_launch(const uint8_t* dyq, const uint8_t* xq, const float* sdy, const float* sx, float* dw,
                           float* ws, int N, int H, int W, int C, int P, int Q, int K, int R, int S, int stride,
@@ -152,6 +158,7 @@ int quant_bf16_fp8_launch(const bf16_t* x, uint8_t* q, const float* scale, float
 struct Fp8WeightDesc {
   const float* w;      // fp32 [K][R][S][C]
   uint8_t* q;          // e4m3 [K][R][S][Cp]
+  uint8_t* qt;         // optional e4m3 [Cp][R][S][K]: the fp8 dgrad's B^T image (nullptr: none)
   const float* scale;  // [1]
   float* amax;         // [kAmaxSlots]
   int K, RS, C, Cp;
@@ -159,7 +166,7 @@ struct Fp8WeightDesc {
 void quant_weight_fp8_grouped_launch(const Fp8WeightDesc* d_descs, const int* d_block_start, int n,
                                      int total_blocks, hipStream_t st);
 int quant_weight_fp8_launch(const float* w, uint8_t* q, const float* scale, float* amax, int K, int RS,
-                            int C, int Cp, hipStream_t st);
+                            int C, int Cp, hipStream_t st, uint8_t* qt = nullptr);
 int fp8_update_scales_launch(float* amax, float* scale, int n, float fmax, hipStream_t st);
 int dequant_fp8_launch(const uint8_t* q, float* out, const float* inv_scale, long long n, hipStream_t st,
                        bool bf8 = false);

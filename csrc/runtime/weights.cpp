@@ -106,9 +106,11 @@ class WeightImages {
 // quant_weight_fp8 launch per conv (52 x ~11 us for ResNet-50).
 class Fp8WeightImages {
  public:
+  // want_t[i]: also keep the transposed e4m3 image [Cp][R][S][K] (fp8 dgrad B^T)
   Fp8WeightImages(std::vector<at::Tensor> weights, std::vector<int64_t> cps, std::vector<at::Tensor> scales,
-                  std::vector<at::Tensor> amaxes)
+                  std::vector<at::Tensor> amaxes, std::vector<bool> want_t)
       : weights_(std::move(weights)), scales_(std::move(scales)), amaxes_(std::move(amaxes)) {
+    TORCH_CHECK(want_t.empty() || want_t.size() == weights_.size(), "fp8 weight images: want_t size");
     TORCH_CHECK(!weights_.empty() && weights_.size() == cps.size() && cps.size() == scales_.size() &&
                     scales_.size() == amaxes_.size(),
                 "fp8 weight images: mismatched entry lists");
@@ -129,9 +131,13 @@ class Fp8WeightImages {
       TORCH_CHECK(cp >= C && cp % 8 == 0, "fp8 weight images: padded channels");
       at::Tensor q = at::empty({K, R, S, cp}, w.options().dtype(at::kByte));
       q_.push_back(q);
+      at::Tensor qt;
+      if (!want_t.empty() && want_t[i]) qt = at::empty({cp, R, S, K}, w.options().dtype(at::kByte));
+      qt_.push_back(qt);
       Fp8WeightDesc d;
       d.w = w.data_ptr<float>();
       d.q = q.data_ptr<uint8_t>();
+      d.qt = qt.defined() ? qt.data_ptr<uint8_t>() : nullptr;
       d.scale = scales_[i].data_ptr<float>();
       d.amax = amaxes_[i].data_ptr<float>();
       d.K = K;
@@ -174,8 +180,14 @@ class Fp8WeightImages {
     return q_[i];
   }
 
+  // transposed image (undefined -> None when not requested)
+  at::Tensor get_t(int64_t i) const {
+    TORCH_CHECK(i >= 0 && i < n_, "fp8 weight images: index");
+    return qt_[i];
+  }
+
  private:
-  std::vector<at::Tensor> weights_, scales_, amaxes_, q_;
+  std::vector<at::Tensor> weights_, scales_, amaxes_, q_, qt_;
   std::vector<const float*> ptrs_;
   at::Tensor d_descs_, d_starts_;
   int n_ = 0, total_blocks_ = 0;
@@ -191,9 +203,12 @@ void register_weights(pybind11::module& m) {
       .def_property_readonly("refreshed", &WeightImages::refreshed);
   py::class_<Fp8WeightImages>(m, "Fp8WeightImages")
       .def(py::init<std::vector<at::Tensor>, std::vector<int64_t>, std::vector<at::Tensor>,
-                    std::vector<at::Tensor>>())
+                    std::vector<at::Tensor>, std::vector<bool>>(),
+           py::arg("weights"), py::arg("cps"), py::arg("scales"), py::arg("amaxes"),
+           py::arg("want_t") = std::vector<bool>())
       .def("refresh", &Fp8WeightImages::refresh)
-      .def("get", &Fp8WeightImages::get);
+      .def("get", &Fp8WeightImages::get)
+      .def("get_t", &Fp8WeightImages::get_t);
 }
 
 }  // namespace pmd

@@ -118,8 +118,10 @@ class Fp8WeightSet:
         self.f8 = f8
         self.index = {id(m): i for i, (m, _) in enumerate(entries)}
         sites = [f8.site(("w", id(m)), init_from=m.weight) for m, _ in entries]
+        # + the transposed [Cp][R][S][K] images of the fp8 dgrads (same scale sites)
         self._c = C.Fp8WeightImages([m.weight for m, _ in entries], [cp for _, cp in entries],
-                                    [sc for sc, _ in sites], [am for _, am in sites])
+                                    [sc for sc, _ in sites], [am for _, am in sites],
+                                    [FP8_DGRAD] * len(entries))
 
     def refresh(self):
         self._c.refresh()
@@ -127,6 +129,11 @@ class Fp8WeightSet:
     def lookup(self, conv_m, cin):
         i = self.index.get(id(conv_m))
         return None if i is None else self._c.get(i)
+
+    def lookup_t(self, conv_m):
+        """The fp8 dgrad's e4m3 [Cp][R][S][K] image (None: not kept for this conv)."""
+        i = self.index.get(id(conv_m))
+        return None if i is None else self._c.get_t(i)
 
 
 def _weight_images(P, w, dtype, cin, want_t):
@@ -191,6 +198,9 @@ FP8_WGRAD = os.environ.get("PMD_FP8_WGRAD", "1") != "0"
 # "spatial" 12,961 / 13,007 vs bf16 12,578 / 12,609 img/s, one lease, round 3); without them
 # only the 3x3 convs do (round 2: profiles/fp8_policy_ab_r02.txt).
 FP8_CONVS = os.environ.get("PMD_FP8_CONVS", "all" if FP8_WGRAD else "spatial")
+# fp8 data gradients (e5m2 dY x e4m3 transposed weight image, the bf16 dgrad's fused
+# epilogue) for the same convs (PMD_FP8_DGRAD=0: bf16 dgrads); needs the fp8 wgrads' dY copy
+FP8_DGRAD = FP8_WGRAD and os.environ.get("PMD_FP8_DGRAD", "1") != "0"
 FP8_MIN_KG = int(os.environ.get("PMD_FP8_MIN_KG", "128"))
 
 
@@ -571,8 +581,10 @@ def _elemt(P, dout, mask, y, p, gamma, red, count, relu, want_dzm=False, lazy=Fa
         return LazyDy(dout, y, P.bn_bwd_coef(p, gamma, red, count),
                       (P, mask, p, gamma, red, count, relu)), None
     if q8 is not None and not want_dzm:
-        # + the e5m2 copy of dY for the fp8 weight gradient (dy._pmd_q8)
-        return P.bn_bwd_elemt(dout, mask, y, p, gamma, red, count, relu, q8=q8)
+        # + the e5m2 copy of dY for the fp8 weight / data gradients (dy._pmd_q8); q8[2]: it
+        # is the only copy (both consumers of this dY run in fp8)
+        return P.bn_bwd_elemt(dout, mask, y, p, gamma, red, count, relu, q8=q8[:2],
+                              q8_only=len(q8) > 2 and q8[2])
     return P.bn_bwd_elemt(dout, mask, y, p, gamma, red, count, relu, want_dzm=want_dzm)
 
 
@@ -996,6 +1008,9 @@ class _ResidualBlockFn(torch.autograd.Function):
         # update() rewrites only after this backward (stream order)
         ctx.qins = qins if any(q is not None for q in qins) else None
         ctx.f8 = f8 if f8w else None
+        wi = _state["wimg"]
+        ctx.f8img = (wi.fp8 if (f8w and FP8_DGRAD and wi is not None and wi.fp8 is not None
+                                and wi.fp8.f8 is f8) else None)
         # cross-block fusion: the NEXT block's first dgrad computes d(out) and can
         # reduce this block's final BN(s) in its epilogue.  The site carries what
         # it needs; the input's site (previous block) is remembered likewise.
@@ -1051,11 +1066,16 @@ class _ResidualBlockFn(torch.autograd.Function):
 
         qins = ctx.qins or [None] * (nst + 2)
 
+        convs = [c for c, _ in stages] + [final[0]] + ([shortcut[0]] if shortcut is not None else [])
+
         def gsite(i, bn_):
-            # e5m2 scale/amax site of the dY that feeds conv i's fp8 weight gradient
+            # e5m2 scale/amax site of the dY that feeds conv i's fp8 weight gradient, and
+            # whether that copy is the only one (conv i's dgrad runs in fp8 as well)
             if ctx.f8 is None or i >= len(qins) or qins[i] is None:
                 return None
-            return ctx.f8.grads.site(("dy", id(bn_)))
+            sc, am = ctx.f8.grads.site(("dy", id(bn_)))
+            only = ctx.f8img is not None and ctx.f8img.lookup_t(convs[i]) is not None
+            return sc, am, only
         # reduce of the final BN(s), if the next block's dgrad already produced it
         pre = ctx.out_site.take(dout, P) if ctx.out_site is not None else None
         # --- final BN (+ projection BN) and the residual ReLU
@@ -1082,19 +1102,34 @@ class _ResidualBlockFn(torch.autograd.Function):
         put(fbn.bias, g[1])
         fuse = _state["fuse_bnred"] and training
 
-        def dgrad_fused(dy_, wp_, shape, stride, pad, rec, addend=None):
+        f8img = ctx.f8img
+
+        def dgrad(dy_, wp_, conv_m_, shape, addend=None, bnred=None, addend_mask=None):
+            # fp8 data gradient when dY carries its e5m2 copy and the conv keeps an e4m3
+            # transposed weight image; else the bf16 kernel (same epilogue options)
+            dq = getattr(dy_, "_pmd_q8", None)
+            if dq is not None and f8img is not None:
+                wtq = f8img.lookup_t(conv_m_)
+                if wtq is not None:
+                    sw = ctx.f8.site(("w", id(conv_m_)))[0]
+                    return P.conv_dgrad_fp8(dq[0], dq[1], wtq, sw, shape, conv_m_.stride, conv_m_.padding,
+                                            addend, bnred=bnred, addend_mask=addend_mask)
+            return P.conv_dgrad(dy_, wp_, shape, conv_m_.stride, conv_m_.padding, addend, bnred=bnred,
+                                addend_mask=addend_mask)
+
+        def dgrad_fused(dy_, wp_, conv_m_, shape, rec, addend=None):
             # dgrad whose output feeds stage rec's BN+ReLU backward: fuse its reduce
             if not fuse:
-                return P.conv_dgrad(dy_, wp_, shape, stride, pad, addend), None
+                return dgrad(dy_, wp_, conv_m_, shape, addend), None
             _hin, _wp, y_, p_, z_ = rec
-            dx_, red_ = P.conv_dgrad(dy_, wp_, shape, stride, pad, addend, bnred=(z_, [(y_, p_)]))
+            dx_, red_ = dgrad(dy_, wp_, conv_m_, shape, addend, bnred=(z_, [(y_, p_)]))
             return dx_, _Pre(red_, _after_dgrad_event(dx_, sync if training else None))
         chk("dyf", dyf)
         side = _WgradSide(dout)
         # --- final conv (its wgrad forks to the side stream first: it overlaps the dgrad)
         put(fconv.weight, side.wgrad(P, dyf, hlast, wpf, fconv.stride, fconv.padding, fconv.weight,
                                      qins[nst]))
-        dh, pre_k = dgrad_fused(dyf, wpf, tuple(hlast.shape), fconv.stride, fconv.padding, recs[-1])
+        dh, pre_k = dgrad_fused(dyf, wpf, fconv, tuple(hlast.shape), recs[-1])
         chk("dh(final)", dh)
         dx = None
         # --- conv->BN->ReLU stages in reverse; the block-input gradient of the
@@ -1110,24 +1145,21 @@ class _ResidualBlockFn(torch.autograd.Function):
             put(conv_m.weight, side.wgrad(P, dy, hin, wp, conv_m.stride, conv_m.padding,
                                           conv_m.weight, qins[k]))
             if k > 0:
-                dh, pre_k = dgrad_fused(dy, wp, tuple(hin.shape), conv_m.stride, conv_m.padding,
-                                        recs[k - 1])
+                dh, pre_k = dgrad_fused(dy, wp, conv_m, tuple(hin.shape), recs[k - 1])
             elif ctx.needs_input_grad[1]:
                 if shortcut is not None:
-                    addend = P.conv_dgrad(dys, wps, tuple(x.shape), sconv.stride, sconv.padding)
+                    addend = dgrad(dys, wps, sconv, tuple(x.shape))
                     amask = None
                 else:
                     addend, amask = dres
                 site = ctx.in_site
                 if site is not None:
                     # d(x) is the previous block's d(out): reduce ITS final BN(s) here
-                    dx, site_red = P.conv_dgrad(dy, wp, tuple(x.shape), conv_m.stride,
-                                                conv_m.padding, addend, bnred=(site.mask, site.sets),
-                                                addend_mask=amask)
+                    dx, site_red = dgrad(dy, wp, conv_m, tuple(x.shape), addend,
+                                         bnred=(site.mask, site.sets), addend_mask=amask)
                     site.put(dx, _Pre(site_red, _after_dgrad_event(dx, sync if training else None)))
                 else:
-                    dx = P.conv_dgrad(dy, wp, tuple(x.shape), conv_m.stride, conv_m.padding, addend,
-                                      addend_mask=amask)
+                    dx = dgrad(dy, wp, conv_m, tuple(x.shape), addend, addend_mask=amask)
         if shortcut is not None:
             put(sconv.weight, side.wgrad(P, dys, x, wps, sconv.stride, sconv.padding, sconv.weight,
                                          qins[nst + 1]))

@@ -99,6 +99,21 @@ def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None, bnred=None, addend_
     return dx, bufs
 
 
+def conv_dgrad_fp8(dyq, sdy, wtq, sw, x_shape, stride, pad, addend=None, bnred=None, addend_mask=None):
+    """dX (bf16) of e5m2 dY (scale sdy) x the e4m3 transposed weight image ``wtq``
+    [Cp,R,S,K] (scale sw), with :func:`conv_dgrad`'s epilogue options."""
+    if bnred is None:
+        return _C.conv_dgrad_fp8(dyq, wtq, sdy, sw, int(x_shape[1]), int(x_shape[2]), int(stride), int(pad),
+                                 addend, addend_mask=addend_mask)
+    mask, sets = bnred
+    bufs = [_acquire(y.shape[-1], y.device) for y, _ in sets]
+    (y0, p0), (y1, p1) = sets[0], (sets[1] if len(sets) > 1 else (None, None))
+    dx = _C.conv_dgrad_fp8(dyq, wtq, sdy, sw, int(x_shape[1]), int(x_shape[2]), int(stride), int(pad),
+                           addend, mask, y0, p0, bufs[0], y1, p1, bufs[1] if len(bufs) > 1 else None,
+                           addend_mask)
+    return dx, bufs
+
+
 def conv_wgrad_fp8(dyq, sdy, xq, sx, wk_shape, stride, pad, out=None):
     """dW of e5m2 dY (scale sdy) x e4m3 X (scale sx), ADDED to ``out`` ([K,R,S,C])."""
     return _C.conv_wgrad_fp8(dyq, xq, sdy, sx, int(wk_shape[1]), int(wk_shape[2]), int(stride), int(pad), out)
@@ -162,19 +177,21 @@ def bn_bwd_reduce(dout, mask, y, p, relu):
     return _C.bn_bwd_reduce(dout, mask, y, p, bool(relu), buf)
 
 
-def bn_bwd_elemt(dout, mask, y, p, gamma, red, count, relu, want_dzm=False, q8=None):
+def bn_bwd_elemt(dout, mask, y, p, gamma, red, count, relu, want_dzm=False, q8=None, q8_only=False):
     """-> (dy, dzm).  ``q8=(scale, amax)``: dy also gets an e5m2 copy (dy * scale) for the
-    fp8 weight gradient, attached as ``dy._pmd_q8 = (dyq, scale)``."""
+    fp8 weight / data gradients, attached as ``dy._pmd_q8 = (dyq, scale)``; with
+    ``q8_only`` the e5m2 copy is the only one written and is itself returned as dy."""
     qs, qa = (q8[0], q8[1]) if q8 is not None else (None, None)
     if torch.is_tensor(count):
         r = _C.bn_bwd_elemt(dout, mask, y, p, gamma.detach(), red, count, 0.0, bool(relu),
-                            bool(want_dzm), False, qs, qa)
+                            bool(want_dzm), False, qs, qa, bool(q8_only))
     else:
         r = _C.bn_bwd_elemt(dout, mask, y, p, gamma.detach(), red, None, float(count), bool(relu),
-                            bool(want_dzm), False, qs, qa)
+                            bool(want_dzm), False, qs, qa, bool(q8_only))
     if q8 is not None:
-        r[0]._pmd_q8 = (r[1], q8[0])
-        return r[0], None
+        d = r[1] if q8_only else r[0]
+        d._pmd_q8 = (r[1], q8[0])
+        return d, None
     return (r[0], r[1]) if want_dzm else (r[0], None)
 
 

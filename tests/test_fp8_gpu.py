@@ -145,6 +145,52 @@ def test_conv_wgrad_fp8(shape):
     assert err < 1e-4, err
 
 
+@pytest.mark.parametrize("shape", [(64, 56, 64, 3, 1), (64, 56, 256, 1, 1), (256, 56, 64, 1, 1),
+                                   (128, 28, 128, 3, 1), (128, 56, 128, 3, 2), (256, 14, 256, 3, 1),
+                                   (1024, 14, 256, 1, 1), (256, 14, 1024, 1, 1), (512, 28, 1024, 1, 2),
+                                   (512, 7, 512, 3, 1)],
+                         ids=lambda s: "C%d_H%d_K%d_R%d_s%d" % s)
+def test_conv_dgrad_fp8(shape):
+    """e5m2 dY x e4m3 transposed weight image on the scaled MFMA inside the implicit-GEMM
+    dgrad kernel == the fp32 data gradient of the same dequantised operands; with an
+    addend and the fused BN-backward reduce, == the unfused bf16 epilogue ops."""
+    from pytorch_multiprocessing_distributed_amd.ops import hip_prims as HP
+    C = _C()
+    torch.manual_seed(2)
+    Cin, H, K, R, st = shape
+    pad = R // 2
+    N = 2 if H >= 56 else (4 if H >= 28 else 8)
+    P = (H + 2 * pad - R) // st + 1
+    dy = torch.randn(N, P, P, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(K, Cin, R, R, device=DEV) / (Cin * R * R) ** 0.5).contiguous(
+        memory_format=torch.channels_last)
+    sw = torch.tensor([448.0 / w.abs().max().item()], device=DEV)
+    sdy = torch.tensor([57344.0 / 4 / dy.float().abs().max().item()], device=DEV)
+    wq, wtq = C.quant_weight_fp8_t(w, Cin, sw, None)
+    dyq = C.quant_bf16_fp8(dy, sdy, None, bf8=True)
+    # the transposed image is the forward image with K and C swapped
+    assert torch.equal(wtq, wq.permute(3, 1, 2, 0))
+    dx = HP.conv_dgrad_fp8(dyq, sdy, wtq, sw, (N, H, H, Cin), st, pad)
+    wd = C.dequant_fp8(wq, 1.0 / sw).permute(0, 3, 1, 2).double()
+    dyd = C.dequant_fp8(dyq, 1.0 / sdy, bf8=True).permute(0, 3, 1, 2).double()
+    ref = torch.nn.grad.conv2d_input((N, Cin, H, H), wd, dyd, stride=st, padding=pad).permute(0, 2, 3, 1)
+    err = (dx.double() - ref).abs().max() / ref.abs().max()
+    assert err < 1e-2, err
+    # fused epilogue: addend + BN-backward reduce over one BN input
+    add = torch.randn(N, H, H, Cin, device=DEV).to(torch.bfloat16)
+    yb = torch.randn(N, H, H, Cin, device=DEV).to(torch.bfloat16)
+    p = torch.stack([torch.randn(Cin, device=DEV) * 0.1, torch.rand(Cin, device=DEV) + 0.5,
+                     torch.rand(Cin, device=DEV), torch.randn(Cin, device=DEV)]).contiguous()
+    _, mask = HP.bn_apply(yb, p, relu=True)
+    dx_f, reds = HP.conv_dgrad_fp8(dyq, sdy, wtq, sw, (N, H, H, Cin), st, pad, add, bnred=(mask, [(yb, p)]))
+    bits = (mask.view(-1, 1).int() >> torch.arange(8, device=DEV).view(1, 8)) & 1
+    want = ((dx.float() + add.float()) * bits.view(dx.shape).float())
+    torch.testing.assert_close(dx_f.float(), want, rtol=2e-2, atol=2e-2 * want.abs().max().item())
+    got = HP.stats_collapse(reds[0]).view(2, Cin)
+    exp = HP.stats_collapse(HP.bn_bwd_reduce(dx_f, mask, yb, p, True)).view(2, Cin)
+    torch.testing.assert_close(got, exp, rtol=1e-3, atol=1e-3 * exp.abs().max().item())
+
+
 def test_resnet50_fp8_trains():
     """Config 5 path: ResNet-50 with fp8 block-conv forwards (e4m3, delayed
     scaling) converges on a fixed batch like the bf16 model, and its first-step
