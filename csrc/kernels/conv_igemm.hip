@@ -182,8 +182,6 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
   constexpr int CE = F8 ? 16 : 8;                 // reduction elements per 16-B chunk
   constexpr int BKE = F8 ? 2 * BK : BK;           // reduction elements per K-tile
   using ET = typename std::conditional<F8, uint8_t, bf16_t>::type;
-  const ET* const srcE = reinterpret_cast<const ET*>(a.src);
-  const ET* const wtE = reinterpret_cast<const ET*>(a.wt);
   constexpr int RPI = DMA ? 64 / CH : 32;         // rows per load instruction (wave / block)
   constexpr int PA = DMA ? BM / (NW * RPI) : BM / 32;  // A load instructions per thread per tile
   constexpr int PB = DMA ? BN / (NW * RPI) : BN / 32;
@@ -231,6 +229,9 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
     a.wt += blockIdx.z * a.bs_wt;
     a.out += blockIdx.z * a.bs_out;
   }
+  // operand base pointers in elements of the operand type (F8: bytes behind the bf16_t* fields)
+  const ET* const srcE = reinterpret_cast<const ET*>(a.src);
+  const ET* const wtE = reinterpret_cast<const ET*>(a.wt);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;

@@ -188,8 +188,8 @@ def _fp8_for(P):
 #     faster in fp8 (790-1,144 vs 600-856 TFLOP/s) and read a 64-512-channel input;
 #     the 1x1 convs save less than their e4m3 input copy costs (conv_bench per-layer
 #     table in profiles/fp8_ring_depth_r02_rejected.txt);
-#   PMD_FP8_CONVS=all (default): every block conv whose reduction Kg = R*S*Cin fills one 128-deep
-#     e4m3 K-tile (PMD_FP8_MIN_KG, default 128; 0 = every block conv).
+#   PMD_FP8_CONVS=all (default): every block conv whose reduction Kg = R*S*Cin >= PMD_FP8_MIN_KG
+#     (default 0 = every block conv with the fp8 gradients, else 128 = a full e4m3 K-tile).
 # fp8 weight gradients (e5m2 dY x e4m3 X) for every conv whose forward ran in fp8; the
 # bf16 copy of a stage activation is then not written at all (PMD_FP8_WGRAD=0: bf16 wgrads)
 FP8_WGRAD = os.environ.get("PMD_FP8_WGRAD", "1") != "0"
@@ -201,7 +201,11 @@ FP8_CONVS = os.environ.get("PMD_FP8_CONVS", "all" if FP8_WGRAD else "spatial")
 # fp8 data gradients (e5m2 dY x e4m3 transposed weight image, the bf16 dgrad's fused
 # epilogue) for the same convs (PMD_FP8_DGRAD=0: bf16 dgrads); needs the fp8 wgrads' dY copy
 FP8_DGRAD = FP8_WGRAD and os.environ.get("PMD_FP8_DGRAD", "1") != "0"
-FP8_MIN_KG = int(os.environ.get("PMD_FP8_MIN_KG", "128"))
+# Minimum forward reduction R*S*Cin of an fp8 conv.  A 64-deep reduction half-fills the
+# 128-deep e4m3 K-tile, but with fp8 data AND weight gradients the l1 convs still pay
+# through their e5m2-only dY and e4m3-only activations: 0 = every block conv (13,976 /
+# 13,998 vs 13,791 / 13,784 img/s at 128, same lease); 128 without the fp8 gradients.
+FP8_MIN_KG = int(os.environ.get("PMD_FP8_MIN_KG", "0" if FP8_DGRAD else "128"))
 
 
 def fp8_eligible(conv_m, cin) -> bool:
