@@ -21,8 +21,9 @@
 // it trades 2.25x fewer multiplies for 16/(2x2)=4x larger transformed operands;
 // with bf16 MFMA at ~2.5 PFLOP/s against ~8 TB/s HBM the implicit GEMM is already
 // near the bandwidth roofline for these layers, so the transformed-tensor
-// traffic costs more than the MFMA work saved.  The autotuner-free selector is
-// PMD_CONV_ALGO=winograd (ops/hip_prims.py); bench/winograd_bench.py measures it.
+// traffic costs more than the MFMA work saved.  Not on the training path (round 3):
+// an explicit API (ops/winograd.py::conv_fwd / conv_dgrad); bench/winograd_bench.py
+// measures it against the implicit GEMM.
 #include "common.h"
 
 namespace pmd {
