@@ -113,8 +113,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
     for (int u = 0; u < U; ++u) {
       const long long i = i0 + u * step;
       if (i < nchunk) {
-        yv[u] = reinterpret_cast<const uint4*>(y1)[i];
-        if (MODE >= 1) rv[u] = reinterpret_cast<const uint4*>(r)[i];
+        yv[u] = ld16s(reinterpret_cast<const uint4*>(y1) + i);
+        if (MODE >= 1) rv[u] = ld16s(reinterpret_cast<const uint4*>(r) + i);
       }
     }
 #pragma unroll
@@ -295,9 +295,9 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(
     for (int u = 0; u < U; ++u) {
       const long long i = i0 + u * step;
       if (i < nchunk) {
-        dv[u] = reinterpret_cast<const uint4*>(dout)[i];
+        dv[u] = ld16s(reinterpret_cast<const uint4*>(dout) + i);
         mv[u] = RELU ? mask[i] : 0xffu;
-        if (!EVAL) yv[u] = reinterpret_cast<const uint4*>(y)[i];
+        if (!EVAL) yv[u] = ld16s(reinterpret_cast<const uint4*>(y) + i);
       }
     }
 #pragma unroll

@@ -50,6 +50,66 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
 __device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
 
 // 8 bf16 <-> uint4 helpers
+// 16-B load of a once-read activation stream (BN passes, dgrad epilogue operands).
+// Non-temporal by default (PMD_LD_NT=1): the streamed lines are marked for early
+// eviction, so they do not push the concurrently running kernels' re-read operands
+// (conv weight images, im2col tiles, wgrad operand rows) out of the XCD's L2.  Full-step
+// A/B, two interleaved rounds on one lease: 13,147 / 13,133 vs 12,761 / 12,781 img/s
+// with plain loads (+2.9%, profiles/ab_r03_nt_loads.txt).
+#ifndef PMD_LD_NT
+#define PMD_LD_NT 1
+#endif
+__device__ __forceinline__ uint4 ld16s(const void* p) {
+  if constexpr (PMD_LD_NT) {
+    typedef unsigned int u32x4_ld __attribute__((ext_vector_type(4)));
+    const u32x4_ld w = __builtin_nontemporal_load(reinterpret_cast<const u32x4_ld*>(p));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  } else {
+    return *reinterpret_cast<const uint4*>(p);
+  }
+}
+// LDS-DMA 16-B copy global -> LDS (global_load_lds_dwordx4).  nt (wave-uniform): the
+// operand rows no other block of the grid reads (a 1x1 conv's activation rows when one
+// column tile covers every output channel, a wgrad operand read by a single tile row /
+// column) are loaded non-temporal (cache policy aux = 2).  PMD_DMA_NT=0 disables it.
+#ifndef PMD_DMA_NT
+#define PMD_DMA_NT 0
+#endif
+__device__ __forceinline__ void glds16(const void* src, void* dst, bool nt) {
+  if (PMD_DMA_NT && nt)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)dst, 16, 0, 2);
+  else
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+}
+// 16-B register load, non-temporal when `nt` (wave-uniform; same rule as glds16)
+__device__ __forceinline__ uint4 ld16c(const void* p, bool nt) {
+  if (PMD_DMA_NT && nt) {
+    typedef unsigned int u32x4_ld2 __attribute__((ext_vector_type(4)));
+    const u32x4_ld2 w = __builtin_nontemporal_load(reinterpret_cast<const u32x4_ld2*>(p));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  return *reinterpret_cast<const uint4*>(p);
+}
+// same for a once-read fp32 stream (split-K partials)
+#ifndef PMD_LD_NT2
+#define PMD_LD_NT2 0
+#endif
+__device__ __forceinline__ float4 ld16f(const void* p) {
+  if constexpr (PMD_LD_NT2) {
+    typedef float f32x4_ld __attribute__((ext_vector_type(4)));
+    const f32x4_ld w = __builtin_nontemporal_load(reinterpret_cast<const f32x4_ld*>(p));
+    return make_float4(w[0], w[1], w[2], w[3]);
+  } else {
+    return *reinterpret_cast<const float4*>(p);
+  }
+}
+__device__ __forceinline__ uint4 ld16s2(const void* p) {
+  if constexpr (PMD_LD_NT2) return ld16s(p);
+  return *reinterpret_cast<const uint4*>(p);
+}
+
 __device__ __forceinline__ void unpack8(const uint4& v, float (&f)[8]) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll

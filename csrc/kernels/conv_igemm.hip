@@ -109,6 +109,9 @@ __device__ __forceinline__ void wait_vmcnt() {
 #ifndef PMD_CONV_SWAPC
 #define PMD_CONV_SWAPC 1
 #endif
+#ifndef PMD_CONV_ST_NT
+#define PMD_CONV_ST_NT 0  // 1: non-temporal epilogue output stores (A/B knob)
+#endif
 #ifndef PMD_CONV_MINB4
 #define PMD_CONV_MINB4 2  // __launch_bounds__ min blocks per CU of the 4-wave tiles (VGPR cap A/B knob)
 #endif
@@ -257,6 +260,9 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
     Kgp = nr * ns * a.Cs;
   }
   const int tilesN = (a.Nout + BN - 1) / BN;
+  // the A rows of a 1x1 conv are read by this block alone when one column tile covers
+  // every output channel (no L2 reuse to protect: non-temporal DMA, glds16)
+  const bool a_once = tilesN == 1 && a.R == 1 && a.S == 1;
   const int Mgrid = (DGRAD && a.stride == 2) ? a.N * ((a.OH + 1) >> 1) * ((a.OW + 1) >> 1) : a.M;
   const int hw_out = a.OH * a.OW;
   const int halo_T = HALO ? (hw_out + BM - 1) / BM : 1;  // HALO: M tiles never straddle images
@@ -377,8 +383,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
                       (unsigned)(u_w[i] + ds) < (unsigned)a.W;
       const void* src = ok ? (const void*)(a_ptr[i] + aoff) : (const void*)g_zero16;
       bf16_t* dst = lds + dbuf * STAGE + (wid_s * (BM / NW) + RPI * i) * LDR;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      glds16(src, dst, a_once);
       if constexpr (TX) {
         const void* sy = ok ? (const void*)(y_ptr[i] + aoff) : (const void*)g_zero16;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)sy,
@@ -431,8 +436,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
         const void* src = g_zero16;
         if (ok) src = srcE + (((size_t)(a_base[i] + ih * a.W + iw)) << a.log2Cs) + c;
         bf16_t* dst = lds + dbuf * STAGE + (wid * (BM / NW) + RPI * i) * LDR;
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+        glds16(src, dst, a_once);
         if constexpr (TX) {
           const void* sy = g_zero16;
           if (ok) sy = a.tx_y + (((size_t)(a_base[i] + ih * a.W + iw)) << a.log2Cs) + c;
@@ -1079,14 +1083,14 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
         if (sw) v[g] = make_uint4(v[g].z, v[g].w, v[g].x, v[g].y);
       }
       if (has_add && ok[g]) {
-        ad[g] = *reinterpret_cast<const uint4*>(a.addend + off[g]);
+        ad[g] = ld16s(a.addend + off[g]);
         am[g] = has_amask ? a.addend_mask[off[g] >> 3] : 0xffu;
       }
       if (nbn && ok[g]) {
         mb[g] = a.bn_mask ? a.bn_mask[off[g] >> 3] : 0xffu;
 #pragma unroll
         for (int t = 0; t < NBA; ++t)
-          if (t < nbn) yy[t][g] = *reinterpret_cast<const uint4*>(a.bn_y[t] + off[g]);
+          if (t < nbn) yy[t][g] = ld16s(a.bn_y[t] + off[g]);
       }
     }
 #pragma unroll
@@ -1113,7 +1117,13 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
         o.z &= ((mk & 16u) ? 0x0000ffffu : 0u) | ((mk & 32u) ? 0xffff0000u : 0u);
         o.w &= ((mk & 64u) ? 0x0000ffffu : 0u) | ((mk & 128u) ? 0xffff0000u : 0u);
       }
-      *reinterpret_cast<uint4*>(a.out + off[g]) = o;
+      if constexpr (PMD_CONV_ST_NT) {
+        typedef unsigned int u32x4_st __attribute__((ext_vector_type(4)));
+        const u32x4_st w = {o.x, o.y, o.z, o.w};
+        __builtin_nontemporal_store(w, reinterpret_cast<u32x4_st*>(a.out + off[g]));
+      } else {
+        *reinterpret_cast<uint4*>(a.out + off[g]) = o;
+      }
       if (nbn) {
         float d[8];
         unpack8(o, d);

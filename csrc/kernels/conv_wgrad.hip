@@ -113,6 +113,8 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
     bq_[i] = rem - bp_[i] * a.Q;
   }
   const int dq = BR % a.Q, dp = (BR / a.Q) % a.P, dn = BR / pq;
+  // operands read by a single tile column / row: non-temporal (see glds16)
+  const bool dy_once = tilesN == 1, x_once = tilesM == 1 && a.R == 1 && a.S == 1;
   // TX: this thread's 8 dY channels are fixed for the whole kernel
   float ta[8], tb[8], tc[8];
   if constexpr (TX) {
@@ -133,7 +135,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
       const int m = mb + a_row + RA * i;
       uint4 v = make_uint4(0, 0, 0, 0);
       if (a_colok && m < mend) {
-        v = *reinterpret_cast<const uint4*>(a.dy + (size_t)m * a.K + k0 + a_col);
+        v = ld16c(a.dy + (size_t)m * a.K + k0 + a_col, dy_once);
         if constexpr (TX) {
           const uint4 yv = *reinterpret_cast<const uint4*>(a.tx_y + (size_t)m * a.K + k0 + a_col);
           float d[8], yy[8], o[8];
@@ -154,7 +156,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
       uint4 v = make_uint4(0, 0, 0, 0);
       if (b_colok && m < mend && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W) {
         const size_t pix = ((size_t)bn_[i] * a.H + ih) * a.W + iw;
-        v = *reinterpret_cast<const uint4*>(a.x + (pix << a.log2C) + cch);
+        v = ld16c(a.x + (pix << a.log2C) + cch, x_once);
       }
       rb[i] = v;
       // advance this row by BR (single-carry; dq < Q, dp < P)
@@ -319,6 +321,9 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_wgrad_dma_kernel(WgradAr
   }
   const int dq = BRD % a.Q, dp = (BRD / a.Q) % a.P, dn = BRD / pq;
   const int wid_s = __builtin_amdgcn_readfirstlane(wid);
+  // an operand read by a single tile column (dY) / row (X) of this split: non-temporal
+  // (X of a 3x3 wgrad is re-gathered for every tap: kept cacheable)
+  const bool dy_once = tilesN == 1, x_once = tilesM == 1 && a.R == 1 && a.S == 1;
 
   auto load = [&](int ch, int buf) {
     const int mb = mbeg + ch * BRD;
@@ -330,8 +335,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_wgrad_dma_kernel(WgradAr
       const void* src = (a_colok && m < mend) ? (const void*)(a.dy + (size_t)m * a.K + k0 + a_col)
                                              : (const void*)g_wzero16;
       char* dst = As + (RA * i) * (BM * 2) + wid_s * 1024;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      glds16(src, dst, dy_once);
     }
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
@@ -342,8 +346,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_wgrad_dma_kernel(WgradAr
       const size_t pix = ((size_t)bn_[i] * a.H + ih) * a.W + iw;
       const void* src = ok ? (const void*)(a.x + (pix << a.log2C) + cch) : (const void*)g_wzero16;
       char* dst = Bs + (RB * i) * (BN * 2) + wid_s * 1024;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      glds16(src, dst, x_once);
       int q = bq_[i] + dq, c1 = q >= a.Q;
       q -= c1 ? a.Q : 0;
       int p = bp_[i] + dp + c1, c2 = p >= a.P;
@@ -851,7 +854,7 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restr
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 4
     for (int s = s0; s < s1; ++s) {
-      const float4 v = reinterpret_cast<const float4*>(ws)[(long long)s * n4 + i];
+      const float4 v = ld16f(reinterpret_cast<const float4*>(ws) + ((long long)s * n4 + i));
       acc.x += v.x;
       acc.y += v.y;
       acc.z += v.z;
