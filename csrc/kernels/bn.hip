@@ -21,21 +21,8 @@
 #ifndef PMD_EW_U
 #define PMD_EW_U 1
 #endif
-#ifndef PMD_EW_NT
-#define PMD_EW_NT 0  // 1: non-temporal output stores in the elementwise passes (A/B knob)
-#endif
 
 namespace pmd {
-
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void st16(void* p, const uint4& v) {
-  if constexpr (PMD_EW_NT) {
-    const u32x4_t w = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(p));
-  } else {
-    *reinterpret_cast<uint4*>(p) = v;
-  }
-}
 
 __device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
   const float4 a = *reinterpret_cast<const float4*>(p);
@@ -113,8 +100,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
     for (int u = 0; u < U; ++u) {
       const long long i = i0 + u * step;
       if (i < nchunk) {
-        yv[u] = ld16s(reinterpret_cast<const uint4*>(y1) + i);
-        if (MODE >= 1) rv[u] = ld16s(reinterpret_cast<const uint4*>(r) + i);
+        yv[u] = ld16n<NT_BNA_Y>(reinterpret_cast<const uint4*>(y1) + i);
+        if (MODE >= 1) rv[u] = ld16n<NT_BNA_R>(reinterpret_cast<const uint4*>(r) + i);
       }
     }
 #pragma unroll
@@ -139,7 +126,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
       const uint4 pk = pack8(v);
       // Q8 with out == nullptr: the e4m3 copy is the ONLY activation (its consumers --
       // the fp8 conv and the fp8 wgrad -- never read a bf16 one)
-      if (!Q8 || out) st16(reinterpret_cast<uint4*>(out) + i, pk);
+      if (!Q8 || out) st16n<NT_EW_ST>(reinterpret_cast<uint4*>(out) + i, pk);
       if (RELU && mask_out) mask_out[i] = (uint8_t)bits;
       if (Q8) {
         float o[8];
@@ -295,9 +282,9 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(
     for (int u = 0; u < U; ++u) {
       const long long i = i0 + u * step;
       if (i < nchunk) {
-        dv[u] = ld16s(reinterpret_cast<const uint4*>(dout) + i);
+        dv[u] = ld16n<NT_BNB_D>(reinterpret_cast<const uint4*>(dout) + i);
         mv[u] = RELU ? mask[i] : 0xffu;
-        if (!EVAL) yv[u] = ld16s(reinterpret_cast<const uint4*>(y) + i);
+        if (!EVAL) yv[u] = ld16n<NT_BNB_Y>(reinterpret_cast<const uint4*>(y) + i);
       }
     }
 #pragma unroll
@@ -317,8 +304,8 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(
       const uint4 pk = pack8(o);
       // Q8 with dy == nullptr: the e5m2 copy is the only dY (every consumer -- the fp8
       // wgrad and the fp8 dgrad -- reads it)
-      if (!Q8 || dy) st16(reinterpret_cast<uint4*>(dy) + i, pk);
-      if (DZM) st16(reinterpret_cast<uint4*>(dzm_out) + i, pack8(d));
+      if (!Q8 || dy) st16n<NT_EW_ST>(reinterpret_cast<uint4*>(dy) + i, pk);
+      if (DZM) st16n<NT_EW_ST>(reinterpret_cast<uint4*>(dzm_out) + i, pack8(d));
       if (Q8) {
         float r[8], c[8];
         unpack8(pk, r);

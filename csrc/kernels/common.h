@@ -50,28 +50,70 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
 __device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
 
 // 8 bf16 <-> uint4 helpers
-// 16-B load of a once-read activation stream (BN passes, dgrad epilogue operands).
-// Non-temporal by default (PMD_LD_NT=1): the streamed lines are marked for early
-// eviction, so they do not push the concurrently running kernels' re-read operands
-// (conv weight images, im2col tiles, wgrad operand rows) out of the XCD's L2.  Full-step
-// A/B, two interleaved rounds on one lease: 13,147 / 13,133 vs 12,761 / 12,781 img/s
-// with plain loads (+2.9%, profiles/ab_r03_nt_loads.txt).
-#ifndef PMD_LD_NT
-#define PMD_LD_NT 1
+// ---- cache policy of the streamed activation traffic (gfx950 "nt" = early eviction).
+// Memory-bound passes next to the kernels of the OTHER stream: every line a streaming
+// pass leaves in the XCD's L2 pushes out a re-read operand of the concurrent kernel
+// (conv weight images, im2col tiles, wgrad operand rows).  Each stream below is
+// non-temporal iff its bit is set in PMD_NT_MASK (compile time; A/B builds via
+// PMD_EXTRA_CFLAGS=-DPMD_NT_MASK=...).  Full-step A/B on one lease
+// (profiles/ab_r03_nt_loads.txt): BN-pass + dgrad-epilogue loads +2.9%, conv epilogue
+// stores a further +1.2%, split-K partial / stem loads +0.2%; elementwise stores neutral.
+enum NtStream {
+  NT_BNA_Y = 1,      // bn_apply: BN input y
+  NT_BNA_R = 2,      // bn_apply: residual / second BN input
+  NT_BNB_D = 4,      // bn_bwd_elemt: dz
+  NT_BNB_Y = 8,      // bn_bwd_elemt: BN input y
+  NT_EPI_A = 16,     // dgrad epilogue: addend (identity-path gradient)
+  NT_EPI_Y = 32,     // dgrad epilogue: BN inputs of the fused BN-backward reduce
+  NT_CONV_ST = 64,   // conv / fp8-conv epilogue output stores
+  NT_EW_ST = 128,    // elementwise BN outputs (bn_apply out, bn_bwd_elemt dy / dzm)
+  NT_WS_LD = 256,    // wgrad_reduce: split-K partials
+  NT_STEM = 512,     // stem pool passes: stem conv output
+  NT_WS_ST = 1024,   // wgrad split-K partial stores
+};
+#ifndef PMD_NT_MASK
+#define PMD_NT_MASK (NT_BNA_Y | NT_BNA_R | NT_BNB_D | NT_BNB_Y | NT_EPI_A | NT_EPI_Y | NT_CONV_ST | NT_WS_LD | NT_STEM)
 #endif
-__device__ __forceinline__ uint4 ld16s(const void* p) {
-  if constexpr (PMD_LD_NT) {
-    typedef unsigned int u32x4_ld __attribute__((ext_vector_type(4)));
-    const u32x4_ld w = __builtin_nontemporal_load(reinterpret_cast<const u32x4_ld*>(p));
+typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
+typedef float f32x4_nt __attribute__((ext_vector_type(4)));
+template <int S>
+__device__ __forceinline__ uint4 ld16n(const void* p) {
+  if constexpr ((PMD_NT_MASK & S) != 0) {
+    const u32x4_nt w = __builtin_nontemporal_load(reinterpret_cast<const u32x4_nt*>(p));
     return make_uint4(w[0], w[1], w[2], w[3]);
   } else {
     return *reinterpret_cast<const uint4*>(p);
   }
 }
+template <int S>
+__device__ __forceinline__ float4 ld16fn(const void* p) {
+  if constexpr ((PMD_NT_MASK & S) != 0) {
+    const f32x4_nt w = __builtin_nontemporal_load(reinterpret_cast<const f32x4_nt*>(p));
+    return make_float4(w[0], w[1], w[2], w[3]);
+  } else {
+    return *reinterpret_cast<const float4*>(p);
+  }
+}
+template <int S>
+__device__ __forceinline__ void st16n(void* p, const uint4& v) {
+  if constexpr ((PMD_NT_MASK & S) != 0) {
+    const u32x4_nt w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4_nt*>(p));
+  } else {
+    *reinterpret_cast<uint4*>(p) = v;
+  }
+}
+template <int S>
+__device__ __forceinline__ void stfn(float* p, float v) {
+  if constexpr ((PMD_NT_MASK & S) != 0) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 // LDS-DMA 16-B copy global -> LDS (global_load_lds_dwordx4).  nt (wave-uniform): the
 // operand rows no other block of the grid reads (a 1x1 conv's activation rows when one
 // column tile covers every output channel, a wgrad operand read by a single tile row /
-// column) are loaded non-temporal (cache policy aux = 2).  PMD_DMA_NT=0 disables it.
+// column) can be loaded non-temporal (cache policy aux = 2) with PMD_DMA_NT=1: measured
+// -1.9% on the full step (12,920 / 12,909 vs 13,175 / 13,173 img/s) -- those rows are
+// re-read by the OTHER stream's kernel (the dgrad's dY by the wgrad), so off by default.
 #ifndef PMD_DMA_NT
 #define PMD_DMA_NT 0
 #endif
@@ -86,27 +128,9 @@ __device__ __forceinline__ void glds16(const void* src, void* dst, bool nt) {
 // 16-B register load, non-temporal when `nt` (wave-uniform; same rule as glds16)
 __device__ __forceinline__ uint4 ld16c(const void* p, bool nt) {
   if (PMD_DMA_NT && nt) {
-    typedef unsigned int u32x4_ld2 __attribute__((ext_vector_type(4)));
-    const u32x4_ld2 w = __builtin_nontemporal_load(reinterpret_cast<const u32x4_ld2*>(p));
+    const u32x4_nt w = __builtin_nontemporal_load(reinterpret_cast<const u32x4_nt*>(p));
     return make_uint4(w[0], w[1], w[2], w[3]);
   }
-  return *reinterpret_cast<const uint4*>(p);
-}
-// same for a once-read fp32 stream (split-K partials)
-#ifndef PMD_LD_NT2
-#define PMD_LD_NT2 0
-#endif
-__device__ __forceinline__ float4 ld16f(const void* p) {
-  if constexpr (PMD_LD_NT2) {
-    typedef float f32x4_ld __attribute__((ext_vector_type(4)));
-    const f32x4_ld w = __builtin_nontemporal_load(reinterpret_cast<const f32x4_ld*>(p));
-    return make_float4(w[0], w[1], w[2], w[3]);
-  } else {
-    return *reinterpret_cast<const float4*>(p);
-  }
-}
-__device__ __forceinline__ uint4 ld16s2(const void* p) {
-  if constexpr (PMD_LD_NT2) return ld16s(p);
   return *reinterpret_cast<const uint4*>(p);
 }
 

@@ -109,9 +109,6 @@ __device__ __forceinline__ void wait_vmcnt() {
 #ifndef PMD_CONV_SWAPC
 #define PMD_CONV_SWAPC 1
 #endif
-#ifndef PMD_CONV_ST_NT
-#define PMD_CONV_ST_NT 0  // 1: non-temporal epilogue output stores (A/B knob)
-#endif
 #ifndef PMD_CONV_MINB4
 #define PMD_CONV_MINB4 2  // __launch_bounds__ min blocks per CU of the 4-wave tiles (VGPR cap A/B knob)
 #endif
@@ -1083,14 +1080,14 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
         if (sw) v[g] = make_uint4(v[g].z, v[g].w, v[g].x, v[g].y);
       }
       if (has_add && ok[g]) {
-        ad[g] = ld16s(a.addend + off[g]);
+        ad[g] = ld16n<NT_EPI_A>(a.addend + off[g]);
         am[g] = has_amask ? a.addend_mask[off[g] >> 3] : 0xffu;
       }
       if (nbn && ok[g]) {
         mb[g] = a.bn_mask ? a.bn_mask[off[g] >> 3] : 0xffu;
 #pragma unroll
         for (int t = 0; t < NBA; ++t)
-          if (t < nbn) yy[t][g] = ld16s(a.bn_y[t] + off[g]);
+          if (t < nbn) yy[t][g] = ld16n<NT_EPI_Y>(a.bn_y[t] + off[g]);
       }
     }
 #pragma unroll
@@ -1117,13 +1114,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
         o.z &= ((mk & 16u) ? 0x0000ffffu : 0u) | ((mk & 32u) ? 0xffff0000u : 0u);
         o.w &= ((mk & 64u) ? 0x0000ffffu : 0u) | ((mk & 128u) ? 0xffff0000u : 0u);
       }
-      if constexpr (PMD_CONV_ST_NT) {
-        typedef unsigned int u32x4_st __attribute__((ext_vector_type(4)));
-        const u32x4_st w = {o.x, o.y, o.z, o.w};
-        __builtin_nontemporal_store(w, reinterpret_cast<u32x4_st*>(a.out + off[g]));
-      } else {
-        *reinterpret_cast<uint4*>(a.out + off[g]) = o;
-      }
+      st16n<NT_CONV_ST>(a.out + off[g], o);
       if (nbn) {
         float d[8];
         unpack8(o, d);

@@ -245,7 +245,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
         if (k < a.K && gg < a.Kg) {
           float* p = dst + (size_t)k * a.Kg + gg;
           if (a.ws)
-            *p = acc[i][j][e];
+            stfn<NT_WS_ST>(p, acc[i][j][e]);
           else
             *p += acc[i][j][e];
         }
@@ -432,7 +432,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_wgrad_dma_kernel(WgradAr
         if (k < a.K && gg < a.Kg) {
           float* p = dst + (size_t)k * a.Kg + gg;
           if (a.ws)
-            *p = acc[i][j][e];
+            stfn<NT_WS_ST>(p, acc[i][j][e]);
           else
             *p += acc[i][j][e];
         }
@@ -621,7 +621,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fp8_kernel(WgradF8Args a) {
         if (k < a.K && gg < a.Kg) {
           float* p = dst + (size_t)k * a.Kg + gg;
           if (a.ws)
-            *p = acc[i][j][e] * ds;
+            stfn<NT_WS_ST>(p, acc[i][j][e] * ds);
           else
             *p += acc[i][j][e] * ds;
         }
@@ -805,7 +805,7 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_halo_kernel(WgradArgs a, Ha
         const int gg = wid * (16 * NI) + j * 16 + (lane & 15);
         float* p = dst + (size_t)k * a.Kg + gg;
         if (a.ws)
-          *p = acc[i][j][e];
+          stfn<NT_WS_ST>(p, acc[i][j][e]);
         else
           *p += acc[i][j][e];
       }
@@ -854,7 +854,7 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restr
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 4
     for (int s = s0; s < s1; ++s) {
-      const float4 v = ld16f(reinterpret_cast<const float4*>(ws) + ((long long)s * n4 + i));
+      const float4 v = ld16fn<NT_WS_LD>(reinterpret_cast<const float4*>(ws) + ((long long)s * n4 + i));
       acc.x += v.x;
       acc.y += v.y;
       acc.z += v.z;

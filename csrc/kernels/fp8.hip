@@ -411,8 +411,7 @@ __global__ __launch_bounds__(256, 2) void conv_fp8_fwd_kernel(Fp8ConvArgs a) {
     const int row = idx / CPR, cc = idx % CPR;
     const int m = m0 + row, n = n0 + cc * 8;
     if (m < a.M && n < a.Nout)
-      *reinterpret_cast<uint4*>(a.out + (size_t)m * a.Nout + n) =
-          *reinterpret_cast<const uint4*>(Cs + row * LDC + cc * 8);
+      st16n<NT_CONV_ST>(a.out + (size_t)m * a.Nout + n, *reinterpret_cast<const uint4*>(Cs + row * LDC + cc * 8));
   }
 }
 

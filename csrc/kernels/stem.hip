@@ -54,7 +54,7 @@ __global__ __launch_bounds__(256) void stem_pool_fwd_kernel(const bf16_t* __rest
     const int ih = p * 2 - 1 + t / 3, iw = q * 2 - 1 + t % 3;
     ok[t] = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
     const int ch = min(max(ih, 0), H - 1), cw = min(max(iw, 0), W - 1);
-    raw[t] = ld16s2(yb + ((size_t)ch * W + cw) * C);
+    raw[t] = ld16n<NT_STEM>(yb + ((size_t)ch * W + cw) * C);
   }
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_reduce_kernel(
     const int jj = j - r * per_row;
     const int h = h0 + r, w = jj >> log2C8;
     float v[8], d[8];
-    unpack8(ld16s2(reinterpret_cast<const uint4*>(y) + (((size_t)n * H + h) * per_row + jj)), v);
+    unpack8(ld16n<NT_STEM>(reinterpret_cast<const uint4*>(y) + (((size_t)n * H + h) * per_row + jj)), v);
     t.dz(h, w, cc, v, sc, sh, d);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -244,7 +244,7 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_elemt_kernel(
     const int h = h0 + r, w = jj >> log2C8;
     const size_t i = ((size_t)n * H + h) * per_row + jj;
     float v[8], d[8], o[8];
-    unpack8(ld16s2(reinterpret_cast<const uint4*>(y) + i), v);
+    unpack8(ld16n<NT_STEM>(reinterpret_cast<const uint4*>(y) + i), v);
     t.dz(h, w, cc, v, sc, sh, d);
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = EVAL ? ca[k] * d[k] : ca[k] * d[k] + cb[k] * v[k] + ccf[k];
