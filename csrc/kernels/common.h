@@ -108,26 +108,28 @@ __device__ __forceinline__ void stfn(float* p, float v) {
   if constexpr ((PMD_NT_MASK & S) != 0) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
-// LDS-DMA 16-B copy global -> LDS (global_load_lds_dwordx4).  nt (wave-uniform): the
-// operand rows no other block of the grid reads (a 1x1 conv's activation rows when one
-// column tile covers every output channel, a wgrad operand read by a single tile row /
-// column) can be loaded non-temporal (cache policy aux = 2) with PMD_DMA_NT=1: measured
-// -1.9% on the full step (12,920 / 12,909 vs 13,175 / 13,173 img/s) -- those rows are
-// re-read by the OTHER stream's kernel (the dgrad's dY by the wgrad), so off by default.
+// LDS-DMA / register 16-B operand loads of the conv and wgrad mainloops, non-temporal
+// when `nt` (wave-uniform: the operand rows no other block of the grid reads) AND the
+// operand's bit is set in PMD_DMA_NT: 1 = conv A rows of a 1x1 conv whose single column
+// tile covers every output channel, 2 = wgrad dY read by one tile column, 4 = wgrad X of a
+// 1x1 conv read by one tile row.  All three (7) measured -1.9% on the full step (12,920 /
+// 12,909 vs 13,175 / 13,173 img/s): a dgrad's dY rows are re-read by the weight gradient
+// on the other stream, so evicting them early turns its L2/MALL hits into HBM reads.
 #ifndef PMD_DMA_NT
 #define PMD_DMA_NT 0
 #endif
+template <int OP>
 __device__ __forceinline__ void glds16(const void* src, void* dst, bool nt) {
-  if (PMD_DMA_NT && nt)
+  if ((PMD_DMA_NT & OP) && nt)
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                      (__attribute__((address_space(3))) void*)dst, 16, 0, 2);
   else
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                      (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
-// 16-B register load, non-temporal when `nt` (wave-uniform; same rule as glds16)
+template <int OP>
 __device__ __forceinline__ uint4 ld16c(const void* p, bool nt) {
-  if (PMD_DMA_NT && nt) {
+  if ((PMD_DMA_NT & OP) && nt) {
     const u32x4_nt w = __builtin_nontemporal_load(reinterpret_cast<const u32x4_nt*>(p));
     return make_uint4(w[0], w[1], w[2], w[3]);
   }

@@ -380,7 +380,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
                       (unsigned)(u_w[i] + ds) < (unsigned)a.W;
       const void* src = ok ? (const void*)(a_ptr[i] + aoff) : (const void*)g_zero16;
       bf16_t* dst = lds + dbuf * STAGE + (wid_s * (BM / NW) + RPI * i) * LDR;
-      glds16(src, dst, a_once);
+      glds16<1>(src, dst, a_once);
       if constexpr (TX) {
         const void* sy = ok ? (const void*)(y_ptr[i] + aoff) : (const void*)g_zero16;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)sy,
@@ -433,7 +433,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
         const void* src = g_zero16;
         if (ok) src = srcE + (((size_t)(a_base[i] + ih * a.W + iw)) << a.log2Cs) + c;
         bf16_t* dst = lds + dbuf * STAGE + (wid * (BM / NW) + RPI * i) * LDR;
-        glds16(src, dst, a_once);
+        glds16<1>(src, dst, a_once);
         if constexpr (TX) {
           const void* sy = g_zero16;
           if (ok) sy = a.tx_y + (((size_t)(a_base[i] + ih * a.W + iw)) << a.log2Cs) + c;

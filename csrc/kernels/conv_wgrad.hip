@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
       const int m = mb + a_row + RA * i;
       uint4 v = make_uint4(0, 0, 0, 0);
       if (a_colok && m < mend) {
-        v = ld16c(a.dy + (size_t)m * a.K + k0 + a_col, dy_once);
+        v = ld16c<2>(a.dy + (size_t)m * a.K + k0 + a_col, dy_once);
         if constexpr (TX) {
           const uint4 yv = *reinterpret_cast<const uint4*>(a.tx_y + (size_t)m * a.K + k0 + a_col);
           float d[8], yy[8], o[8];
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
       uint4 v = make_uint4(0, 0, 0, 0);
       if (b_colok && m < mend && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W) {
         const size_t pix = ((size_t)bn_[i] * a.H + ih) * a.W + iw;
-        v = ld16c(a.x + (pix << a.log2C) + cch, x_once);
+        v = ld16c<4>(a.x + (pix << a.log2C) + cch, x_once);
       }
       rb[i] = v;
       // advance this row by BR (single-carry; dq < Q, dp < P)
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_wgrad_dma_kernel(WgradAr
       const void* src = (a_colok && m < mend) ? (const void*)(a.dy + (size_t)m * a.K + k0 + a_col)
                                              : (const void*)g_wzero16;
       char* dst = As + (RA * i) * (BM * 2) + wid_s * 1024;
-      glds16(src, dst, dy_once);
+      glds16<2>(src, dst, dy_once);
     }
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
@@ -346,7 +346,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_wgrad_dma_kernel(WgradAr
       const size_t pix = ((size_t)bn_[i] * a.H + ih) * a.W + iw;
       const void* src = ok ? (const void*)(a.x + (pix << a.log2C) + cch) : (const void*)g_wzero16;
       char* dst = Bs + (RB * i) * (BN * 2) + wid_s * 1024;
-      glds16(src, dst, x_once);
+      glds16<4>(src, dst, x_once);
       int q = bq_[i] + dq, c1 = q >= a.Q;
       q -= c1 ? a.Q : 0;
       int p = bp_[i] + dp + c1, c2 = p >= a.P;
