@@ -841,12 +841,15 @@ static bool halo_cfg(const WgradArgs& a, HaloArgs* h, int* nich) {
 
 static int halo_splits(const HaloArgs& h) { return (h.bands + h.bpb - 1) / h.bpb; }
 
-// dW[i] += sum_s ws[s][i].  blockIdx.y = split group of <= kSplitGroup slices:
-// one group -> plain read-modify-write in fixed order (deterministic); several
-// groups (tiny outputs with hundreds of splits) -> one fp32 atomic per group.
+// dW[i] += sum_s ws[s][i], in a fixed order (bitwise reproducible).  blockIdx.y = split
+// group of <= kSplitGroup slices: with one group the block adds straight into dW; with
+// several (tiny outputs with hundreds of splits) a group stage (to_ws = 1) leaves each
+// group's sum in its first slice, and a second launch (sst = kSplitGroup) adds those
+// group sums into dW in group order.  (The round-2 version combined the groups with fp32
+// atomics, whose order -- hence the last bits of the l1 weight gradients -- varied run to run.)
 constexpr int kSplitGroup = 32;
-__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw, int splits,
-                                    long long n4) {
+__global__ void wgrad_reduce_kernel(float* __restrict__ ws, float* __restrict__ dw, int splits,
+                                    long long n4, int sst, int to_ws) {
   const int s0 = blockIdx.y * kSplitGroup;
   const int s1 = s0 + kSplitGroup < splits ? s0 + kSplitGroup : splits;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
@@ -854,25 +857,21 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restr
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 4
     for (int s = s0; s < s1; ++s) {
-      const float4 v = ld16fn<NT_WS_LD>(reinterpret_cast<const float4*>(ws) + ((long long)s * n4 + i));
+      const float4 v = ld16fn<NT_WS_LD>(reinterpret_cast<const float4*>(ws) + ((long long)s * sst * n4 + i));
       acc.x += v.x;
       acc.y += v.y;
       acc.z += v.z;
       acc.w += v.w;
     }
-    if (gridDim.y == 1) {
+    if (to_ws) {
+      reinterpret_cast<float4*>(ws)[(long long)s0 * n4 + i] = acc;  // this thread read it first
+    } else {
       float4 d = reinterpret_cast<float4*>(dw)[i];
       d.x += acc.x;
       d.y += acc.y;
       d.z += acc.z;
       d.w += acc.w;
       reinterpret_cast<float4*>(dw)[i] = d;
-    } else {
-      float* p = dw + 4 * i;
-      atomicAdd(p, acc.x);
-      atomicAdd(p + 1, acc.y);
-      atomicAdd(p + 2, acc.z);
-      atomicAdd(p + 3, acc.w);
     }
   }
 }
@@ -1070,7 +1069,13 @@ static void wgrad_reduce_launch(const WgradArgs& a, int splits, hipStream_t st) 
   const int groups = (splits + kSplitGroup - 1) / kSplitGroup;
   long long b = (n4 + 255) / 256;
   if (b > 4096) b = 4096;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)b, groups), dim3(256), 0, st, a.ws, a.dw, splits, n4);
+  if (groups == 1) {
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)b, 1), dim3(256), 0, st, a.ws, a.dw, splits, n4, 1, 0);
+  } else {
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)b, groups), dim3(256), 0, st, a.ws, a.dw, splits, n4, 1, 1);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)b, 1), dim3(256), 0, st, a.ws, a.dw, groups, n4,
+                       kSplitGroup, 0);
+  }
 }
 
 // FP8 wgrad split plan: 128-row chunks, the bf16 kernels' block targets, workspace <= 96 MiB

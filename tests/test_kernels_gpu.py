@@ -106,6 +106,24 @@ def test_wgrad_variants(shape, impl):
     _close(dw, dwr, 2e-3)
 
 
+def test_wgrad_many_splits_reproducible():
+    """A tiny weight gradient over a long reduction (ResNet-50 layer-1 1x1, K = 64:
+    two output tiles, hundreds of split-K slices -> several reduction groups) is
+    bitwise identical run to run (fixed-order two-stage group reduction, no fp32
+    atomics) and matches fp32 conv2d_weight."""
+    HP = _hp()
+    torch.manual_seed(7)
+    N, H, C, K = 64, 56, 256, 64
+    x = torch.randn(N, H, H, C, device=DEV).to(torch.bfloat16)
+    dy = torch.randn(N, H, H, K, device=DEV).to(torch.bfloat16)
+    # M = 200,704 rows over 2 output tiles: the 384-block split plan gives 192 slices
+    a = HP.conv_wgrad(dy, x, (K, 1, 1, C), 1, 0)
+    b = HP.conv_wgrad(dy, x, (K, 1, 1, C), 1, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b), "split-K weight gradient differs between two identical runs"
+    _close(a, TP.conv_wgrad(dy, x, (K, 1, 1, C), 1, 0), 2e-3)
+
+
 @pytest.mark.parametrize("N,H,C,R,pad,P", [
     (3, 112, 16, 4, 2, 112),   # the space-to-depth stem: 4x4 over 16 ch, output cropped to H
     (3, 56, 64, 3, 1, 56),     # layer1 3x3
