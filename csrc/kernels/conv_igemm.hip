@@ -109,6 +109,9 @@ __device__ __forceinline__ void wait_vmcnt() {
 #ifndef PMD_CONV_SWAPC
 #define PMD_CONV_SWAPC 1
 #endif
+#ifndef PMD_CONV_ST_PASS
+#define PMD_CONV_ST_PASS 0
+#endif
 #ifndef PMD_CONV_MINB4
 #define PMD_CONV_MINB4 2  // __launch_bounds__ min blocks per CU of the 4-wave tiles (VGPR cap A/B knob)
 #endif
@@ -1114,7 +1117,12 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
         o.z &= ((mk & 16u) ? 0x0000ffffu : 0u) | ((mk & 32u) ? 0xffff0000u : 0u);
         o.w &= ((mk & 64u) ? 0x0000ffffu : 0u) | ((mk & 128u) ? 0xffff0000u : 0u);
       }
-      st16n<NT_CONV_ST>(a.out + off[g], o);
+      // PMD_CONV_ST_PASS (A/B): 0 = both passes as PMD_NT_MASK says, 1 = forward outputs only,
+      // 2 = data-gradient outputs only
+      if constexpr (PMD_CONV_ST_PASS == 0 || (PMD_CONV_ST_PASS == 1) == !DGRAD)
+        st16n<NT_CONV_ST>(a.out + off[g], o);
+      else
+        *reinterpret_cast<uint4*>(a.out + off[g]) = o;
       if (nbn) {
         float d[8];
         unpack8(o, d);
