@@ -1025,12 +1025,14 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
   // masks, BN inputs) is issued before the group's first store (the stores may
   // alias nothing the group reads), so a thread has G x (1-3) HBM reads in
   // flight instead of one dependent load->store chain per row.  Full-step A/B
-  // (bench/ab_so.sh): G=2 +0.6% over the serial loop, G=4 -3.6% (the 4-deep
-  // register tile of activation chunks costs more than the extra latency hiding).
+  // (bench/ab_so.sh): G=2 +0.6% over the serial loop, G=4 -3.6% with default-policy
+  // loads (the 4-deep register tile of activation chunks cost more than the extra
+  // latency hiding) -- but +0.5% once the epilogue operands stream non-temporal (round 3:
+  // 13,440 / 13,435 vs 13,348 / 13,386 img/s, profiles/ab_r03_nt_loads.txt).
   constexpr int ITERS = BM * CPR / NT;
   static_assert((BM * CPR) % NT == 0, "whole epilogue iterations");
 #ifndef PMD_EPI_G
-#define PMD_EPI_G 2
+#define PMD_EPI_G 4
 #endif
   constexpr int G = ITERS < PMD_EPI_G ? ITERS : PMD_EPI_G;
   static_assert(ITERS % G == 0, "epilogue groups");
