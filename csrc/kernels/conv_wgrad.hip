@@ -900,6 +900,13 @@ static int wgrad_target_blocks(int R) {
   static const int t7 = env_int("PMD_WGRAD_BLOCKS_R7", 2048);
   return R == 1 ? t1 : (R <= 3 ? t3 : t7);
 }
+// fp8 weight gradients (128-row chunks, half the bytes per row): fewer, longer splits --
+// 256 blocks measured +0.4% on the fp8 step (14,761 / 14,787 vs 14,712 / 14,728 img/s,
+// profiles/ab_r03_nt_loads.txt) where 256 for the bf16 wgrads is -0.3%.  PMD_WGRAD_BLOCKS_F8.
+static int wgrad_target_blocks_f8(int R) {
+  static const int t = env_int("PMD_WGRAD_BLOCKS_F8", 256);
+  return R <= 3 ? t : wgrad_target_blocks(R);
+}
 
 // Variant (conv_wgrad_set_impl or PMD_WGRAD_IMPL): 0 register staging
 // (2 stages), 1 LDS-DMA 64-row stages x2 (default: autotuned per shape over
@@ -1082,7 +1089,7 @@ static void wgrad_reduce_launch(const WgradArgs& a, int splits, hipStream_t st) 
 static void plan_fp8(const WgradF8Args& a, int BM, int BN, int* splits_out, int* cps_out) {
   const int tiles = ((a.K + BM - 1) / BM) * ((a.Kg + BN - 1) / BN);
   const int chunks = (a.M + 127) / 128;
-  int splits = (wgrad_target_blocks(a.R) + tiles - 1) / tiles;
+  int splits = (wgrad_target_blocks_f8(a.R) + tiles - 1) / tiles;
   const int max_splits = (chunks + 1) / 2;
   if (splits > max_splits) splits = max_splits;
   const long long per = (long long)a.K * a.Kg * 4;
