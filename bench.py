@@ -56,17 +56,23 @@ def parse():
                     help="SyncBN statistics transport (auto: one-shot xGMI kernel when W>1)")
     ap.add_argument("--grad_compress", default="none", choices=["none", "bf16"])
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
-                    help="fp8 = BASELINE config 5: block-conv forwards on the e4m3 scaled MFMA "
-                         "(delayed per-tensor scaling), everything else bf16/fp32")
+                    help="fp8 = BASELINE config 5: every block conv's forward, data gradient and "
+                         "weight gradient on the scaled fp8 MFMA (e4m3 weights/activations, e5m2 "
+                         "gradients, delayed per-tensor scaling); stem, classifier, BN in bf16/fp32")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process-group backend for W>1 (auto: nccl = RCCL)")
     ap.add_argument("--same_device", action="store_true",
                     help="W>1 ranks all on GPU 0 (with --backend gloo: rehearses the exact "
                          "multi-rank code path -- DataParallel, native reducer, xGMI SyncBN -- "
                          "on a one-GPU box; not a throughput number)")
-    ap.add_argument("--comm", default="c10d", choices=["c10d", "rccl"],
-                    help="gradient-bucket transport: torch ProcessGroupNCCL or the native "
-                         "RCCL communicator (csrc/runtime/rccl_comm.cpp)")
+    ap.add_argument("--comm", default="auto", choices=["auto", "c10d", "rccl"],
+                    help="gradient-bucket transport: auto = the native RCCL communicator "
+                         "(csrc/runtime/rccl_comm.cpp) when it can be the only in-step communicator "
+                         "and its self-test passes, else torch ProcessGroupNCCL (c10d)")
+    ap.add_argument("--dp_rehearsal", action="store_true",
+                    help="W=1 only: run the production W>1 per-rank step on a single-rank process "
+                         "group -- DataParallel hooks, native reducer, bucket all-reduces (--comm), "
+                         "SyncBN through the one-shot xGMI kernel -- to measure its per-rank cost")
     ap.add_argument("--tune_table", default="",
                     help="kernel tuning table loaded before warmup: '' = the committed table(s) for "
                          "this device (ops/tables/, deterministic kernel choices), 'online' = "
@@ -81,6 +87,15 @@ def parse():
                     help="capture the whole training step (fwd+bwd+SGD) in a HIP graph and replay it "
                          "(single GPU); each replay is a full step on a freshly generated batch")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
 
 
 def syncbn_label(comm, sync_bn):
@@ -103,17 +118,28 @@ def bench_rank(rank, world, a):
     from pytorch_multiprocessing_distributed_amd.parallel.comm import get_comm
     from pytorch_multiprocessing_distributed_amd.parallel.dp import DataParallel
 
-    if world > 1:
+    rehearsal = a.dp_rehearsal and world == 1
+    if world > 1 or rehearsal:
         backend = "nccl" if a.backend == "auto" else a.backend
-        if a.same_device:
+        if a.same_device or rehearsal:
             os.environ["LOCAL_RANK"] = "0"
+        if rehearsal:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
         dev = launch.init_process(rank, world, backend, "cuda")
     else:
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     model = build_model(a.model, num_classes=a.classes, stem="imagenet").to(dev)
-    comm = get_comm()
+    if rehearsal:
+        # the W>1 machinery on a single-rank group: get_comm() would return None at W=1
+        from pytorch_multiprocessing_distributed_amd.parallel.comm import Comm
+        comm = Comm()
+        if a.syncbn_comm == "auto":
+            a.syncbn_comm = "xgmi"          # the production W>1 SyncBN transport
+    else:
+        comm = get_comm()
     setup_syncbn(comm, a.sync_bn, a.syncbn_comm, True)
     model = DataParallel(model, comm, bucket_mb=a.bucket_mb, first_bucket_mb=a.first_bucket_mb,
                          compress=a.grad_compress, transport=a.comm if comm is not None else "c10d",
@@ -221,6 +247,8 @@ def bench_rank(rank, world, a):
         parallelism = f"dp{world}"
         if world > 1 and a.same_device:
             parallelism += f"-same-gpu-{dist.get_backend()}"
+        if rehearsal:
+            parallelism += "-rehearsal"
         rec = {
             "metric": metric, "value": round(ips, 1), "unit": "images/sec",
             "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -230,7 +258,8 @@ def bench_rank(rank, world, a):
             "config": {"model": model_name, "global_batch": a.batch * world,
                        "seq_len": None,
                        "image_size": a.image, "per_gpu_batch": a.batch,
-                       "parallelism": parallelism, "sync_bn": a.sync_bn == "on" and world > 1,
+                       "parallelism": parallelism,
+                       "sync_bn": a.sync_bn == "on" and (world > 1 or rehearsal),
                        "bucket_mb": a.bucket_mb, "hip_graph": bool(a.graph and world == 1),
                        "syncbn_comm": syncbn_label(comm, a.sync_bn),
                        "grad_compress": a.grad_compress,
@@ -257,7 +286,7 @@ def bench_rank(rank, world, a):
             torch.cuda.synchronize()
         with open(a.profile, "w") as f:
             f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=80))
-    if world > 1:
+    if world > 1 or rehearsal:
         launch.shutdown()
 
 

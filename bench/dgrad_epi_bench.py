@@ -60,9 +60,6 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="")
     ap.add_argument("--tile", type=int, default=0, help="conv_set_tile policy (0 = autotuned)")
-    ap.add_argument("--tx", action="store_true",
-                    help="also time the BN-backward-on-load (TX) variant: dY given as (dzm, y, coef), "
-                         "against bn_bwd_elemt + the plain fused dgrad, and the TX wgrad vs the wgrad")
     ap.add_argument("--fp8", action="store_true",
                     help="also time the fp8 dgrad (e5m2 dY x e4m3 transposed weights) with the same epilogue")
     ap.add_argument("--impl", type=int, default=5,
@@ -124,46 +121,6 @@ def main():
                 else:
                     HP.conv_dgrad_fp8(dyq, sdy, wtq, sw, xshape, 1, 0, addend, addend_mask=am)
             f8s = f" | fp8 {timeit(run8, a.iters) * 1e3:7.1f}"
-        if a.tx:
-            from pytorch_multiprocessing_distributed_amd.ops.lazy import LazyDy
-            yk = torch.randn(N, H, H, K, device=dev, generator=g).to(torch.bfloat16)
-            pk = torch.stack([yk.float().mean((0, 1, 2)), torch.rsqrt(yk.float().var((0, 1, 2)) + 1e-5),
-                              torch.ones(K, device=dev), torch.zeros(K, device=dev)]).contiguous()
-            _, mkk = HP.bn_apply(yk, pk, relu=True)
-            red = torch.randn(2, K, device=dev)
-            gam = torch.ones(K, device=dev)
-            coef = HP.bn_bwd_coef(pk, gam, red, float(M))
-            lz = LazyDy(dy, yk, coef, None)
-            x = torch.randn(N, H, H, C, device=dev, generator=g).to(torch.bfloat16)
-
-            def mat():
-                d, _ = HP.bn_bwd_elemt(dy, mkk, yk, pk, gam, red, float(M), True)
-                return d
-
-            def run_mat():
-                d = mat()
-                if nsets:
-                    _, rr = HP.conv_dgrad(d, wp, xshape, 1, 0, addend, bnred=(mk, sets), addend_mask=am)
-                    HP._release(*rr)
-                else:
-                    HP.conv_dgrad(d, wp, xshape, 1, 0, addend, addend_mask=am)
-
-            def run_tx():
-                if nsets:
-                    _, rr = HP.conv_dgrad(lz, wp, xshape, 1, 0, addend, bnred=(mk, sets), addend_mask=am)
-                    HP._release(*rr)
-                else:
-                    HP.conv_dgrad(lz, wp, xshape, 1, 0, addend, addend_mask=am)
-            dw = torch.zeros(K, 1, 1, C, device=dev)
-            dmat = mat()
-            te = timeit(mat, a.iters)
-            tm = timeit(run_mat, a.iters)
-            tt = timeit(run_tx, a.iters)
-            twm = timeit(lambda: HP.conv_wgrad(dmat, x, (K, 1, 1, C), 1, 0, out=dw), a.iters)
-            twt = timeit(lambda: HP.conv_wgrad(lz, x, (K, 1, 1, C), 1, 0, out=dw), a.iters)
-            print(f"{'':>12}   TX: elemt {te * 1e3:6.1f} + dgrad = {tm * 1e3:6.1f} us | TX dgrad {tt * 1e3:6.1f} us"
-                  f" | wgrad {twm * 1e3:6.1f} vs TX wgrad {twt * 1e3:6.1f} us", flush=True)
-            del yk, lz, x, dw, dmat
         gb = (M * K * 2 + M * C * 2 + (M * C * 2 if add else 0) + (M * C // 8 if amask else 0)
               + nsets * M * C * 2 + (M * C // 8 if nsets else 0)) / 1e9
         gbp = (M * K * 2 + M * C * 2) / 1e9

@@ -256,8 +256,7 @@ Tensor conv_dgrad(Tensor dy, Tensor wkt, int64_t H, int64_t W, int64_t stride, i
                   c10::optional<Tensor> bn_y0, c10::optional<Tensor> bn_p0,
                   c10::optional<Tensor> bn_red0, c10::optional<Tensor> bn_y1,
                   c10::optional<Tensor> bn_p1, c10::optional<Tensor> bn_red1,
-                  c10::optional<Tensor> addend_mask, c10::optional<Tensor> tx_y,
-                  c10::optional<Tensor> tx_coef) {
+                  c10::optional<Tensor> addend_mask) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONT(dy);
   CHECK_DEV(wkt); CHECK_BF16(wkt); CHECK_CONT(wkt);
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), K = dy.size(3);
@@ -302,22 +301,10 @@ Tensor conv_dgrad(Tensor dy, Tensor wkt, int64_t H, int64_t W, int64_t stride, i
       bnr.mask = bn_mask->data_ptr<uint8_t>();
     }
   }
-  // TX: dy holds dzm (the masked BN-output gradient); the kernel applies the BN
-  // backward dY = a dzm + b y + c while reading it (tx_coef = bn_bwd_coef's [3][Cp])
-  pmd::TxArgs tx{};
-  const bool use_tx = tx_y && tx_y->defined();
-  if (use_tx) {
-    CHECK_BF16(*tx_y); CHECK_CONT(*tx_y);
-    TORCH_CHECK(tx_y->sizes() == dy.sizes(), "tx_y must match dy");
-    TORCH_CHECK(tx_coef && tx_coef->defined() && tx_coef->dim() == 2 && tx_coef->size(0) == 3 &&
-                tx_coef->size(1) >= K, "tx_coef must be [3, Cp >= K]");
-    CHECK_F32(*tx_coef); CHECK_CONT(*tx_coef);
-    tx = {bfp(*tx_y), tx_coef->data_ptr<float>(), (int)tx_coef->size(1)};
-  }
   // the gathered operand is dy (spatial P x Q, K channels); output spatial is H x W
   const int rc = pmd::conv_igemm_launch(bfp(dy), bfp(wkt), bfp_mut(dx), nullptr, N, P, Q, K, (int)H,
                                         (int)W, Cp, R, S, (int)stride, (int)pad, true, add, amask,
-                                        fused ? &bnr : nullptr, cur_stream(), nullptr, use_tx ? &tx : nullptr);
+                                        fused ? &bnr : nullptr, cur_stream(), nullptr);
   CHECK_RC(rc, "conv_dgrad");
   return dx;
 }
@@ -385,7 +372,7 @@ Tensor conv_dgrad_fp8(Tensor dyq, Tensor wtq, Tensor sdy, Tensor sw, int64_t H, 
 
 // out: optional [K,R,S,C] fp32 accumulation target (e.g. a grad-arena view); dW is ADDED to it
 Tensor conv_wgrad(Tensor dy, Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad,
-                  c10::optional<Tensor> out, c10::optional<Tensor> tx_y, c10::optional<Tensor> tx_coef) {
+                  c10::optional<Tensor> out) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONT(dy);
   CHECK_DEV(x); CHECK_BF16(x); CHECK_CONT(x);
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
@@ -407,20 +394,9 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int64_t R, int64_t S, int64_t stride, int
                                             (int)pad);
   Tensor ws;
   if (splits > 1) ws = torch::empty({splits, K, R * S * C}, x.options().dtype(torch::kFloat32));
-  pmd::TxArgs tx{};
-  const bool use_tx = tx_y && tx_y->defined();
-  if (use_tx) {
-    CHECK_BF16(*tx_y); CHECK_CONT(*tx_y);
-    TORCH_CHECK(tx_y->sizes() == dy.sizes(), "tx_y must match dy");
-    TORCH_CHECK(tx_coef && tx_coef->defined() && tx_coef->dim() == 2 && tx_coef->size(0) == 3 &&
-                tx_coef->size(1) >= K, "tx_coef must be [3, Cp >= K]");
-    CHECK_F32(*tx_coef); CHECK_CONT(*tx_coef);
-    tx = {bfp(*tx_y), tx_coef->data_ptr<float>(), (int)tx_coef->size(1)};
-  }
   const int rc = pmd::conv_wgrad_launch(bfp(dy), bfp(x), dw.data_ptr<float>(),
                                         splits > 1 ? ws.data_ptr<float>() : nullptr, N, H, W, C, P, Q,
-                                        K, (int)R, (int)S, (int)stride, (int)pad, cur_stream(),
-                                        use_tx ? &tx : nullptr);
+                                        K, (int)R, (int)S, (int)stride, (int)pad, cur_stream());
   CHECK_RC(rc, "conv_wgrad");
   return dw;
 }
@@ -617,28 +593,6 @@ Tensor bn_bwd_reduce(Tensor dout, c10::optional<Tensor> mask, Tensor y, Tensor p
                                            relu, cur_stream());
   CHECK_RC(rc, "bn_bwd_reduce");
   return red;
-}
-
-// [3][Cp] fp32 (a | b | c) with dy = a*dzm + b*y + c, zero past C (Cp = C rounded up to 64)
-Tensor bn_bwd_coef(Tensor params, Tensor gamma, c10::optional<Tensor> red, c10::optional<Tensor> count,
-                   double count_h, bool eval_mode) {
-  CHECK_DEV(params);
-  const int C = params.size(-1);
-  const int Cp = (C + 63) / 64 * 64;
-  c10::DeviceGuard g(params.device());
-  Tensor coef = torch::empty({3, Cp}, params.options().dtype(torch::kFloat32));
-  Tensor rr, cc, gm = gamma.contiguous(), pp = params.contiguous();
-  if (!eval_mode) {
-    TORCH_CHECK(red && red->defined(), "train backward needs sums");
-    rr = red->contiguous();
-    if (count && count->defined()) cc = count->contiguous();
-  }
-  const int rc = pmd::bn_bwd_coef_launch(pp.data_ptr<float>(), gm.data_ptr<float>(),
-                                         eval_mode ? nullptr : rr.data_ptr<float>(),
-                                         (eval_mode || !cc.defined()) ? nullptr : cc.data_ptr<float>(),
-                                         (float)count_h, coef.data_ptr<float>(), C, Cp, eval_mode, cur_stream());
-  CHECK_RC(rc, "bn_bwd_coef");
-  return coef;
 }
 
 // count: device scalar (SyncBN global count) or, if absent, count_h from the host
@@ -1062,10 +1016,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wkt"), py::arg("H"), py::arg("W"),
         py::arg("stride"), py::arg("pad"), py::arg("addend"), py::arg("bn_mask"), py::arg("bn_y0"),
         py::arg("bn_p0"), py::arg("bn_red0"), py::arg("bn_y1"), py::arg("bn_p1"), py::arg("bn_red1"),
-        py::arg("addend_mask"), py::arg("tx_y") = py::none(), py::arg("tx_coef") = py::none());
+        py::arg("addend_mask"));
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"),
-        py::arg("pad"), py::arg("out") = py::none(), py::arg("tx_y") = py::none(),
-        py::arg("tx_coef") = py::none());
+        py::arg("pad"), py::arg("out") = py::none());
   m.def("bn_finalize", &bn_finalize, py::arg("sums"), py::arg("count"), py::arg("gamma"), py::arg("beta"),
         py::arg("eps"), py::arg("rm"), py::arg("rv"), py::arg("momentum"), py::arg("nbt"),
         py::arg("eval_mode"), py::arg("shift") = py::none());
@@ -1080,7 +1033,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gamma"), py::arg("red"), py::arg("count"), py::arg("count_h"), py::arg("relu"),
         py::arg("want_dzm"), py::arg("eval_mode"), py::arg("q8_scale") = py::none(),
         py::arg("q8_amax") = py::none(), py::arg("q8_only") = false);
-  m.def("bn_bwd_coef", &bn_bwd_coef);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("stem_pool_fwd", &stem_pool_fwd);

@@ -325,41 +325,6 @@ __global__ __launch_bounds__(256) void bn_bwd_elemt_kernel(
   if (Q8) block_amax_update(qamax, qm);
 }
 
-// BN-backward coefficients for consumers that apply  dy = a*dzm + b*y + c  on the
-// fly (the 1x1-conv dgrad / wgrad operand loaders, kernels/conv_igemm.hip and
-// conv_wgrad.hip, "TX"): coef [3][Cp] = (a, b, c), the exact per-channel terms
-// bn_bwd_elemt_kernel uses, zero-padded to Cp channels so a K-tile tail reads zeros.
-__global__ void bn_bwd_coef_kernel(const float* __restrict__ params, const float* __restrict__ gamma,
-                                   const float* __restrict__ red, const float* __restrict__ count,
-                                   float count_h, float* __restrict__ coef, int C, int Cp, int eval_mode) {
-  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < Cp; c += gridDim.x * blockDim.x) {
-    float a = 0.f, b = 0.f, cc = 0.f;
-    if (c < C) {
-      if (eval_mode) {
-        a = params[2 * C + c];
-      } else {
-        const float inv_cnt = 1.f / (count ? count[0] : count_h);
-        const float mean = params[c], inv = params[C + c];
-        a = gamma[c] * inv;
-        const float mdy = red[c] * inv_cnt, mdyx = red[C + c] * inv_cnt;
-        b = -a * inv * mdyx;
-        cc = a * (mean * inv * mdyx - mdy);
-      }
-    }
-    coef[c] = a;
-    coef[Cp + c] = b;
-    coef[2 * Cp + c] = cc;
-  }
-}
-
-int bn_bwd_coef_launch(const float* params, const float* gamma, const float* red, const float* count,
-                       float count_h, float* coef, int C, int Cp, bool eval_mode, hipStream_t st) {
-  if (C <= 0 || Cp < C) return 1;
-  hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((Cp + 255) / 256), dim3(256), 0, st, params, gamma, red, count,
-                     count_h, coef, C, Cp, eval_mode ? 1 : 0);
-  return 0;
-}
-
 // out[0:2Ca] = sum_slots a[slot][2][Ca]; out[2Ca:2Ca+2Cb] = same for b; out[last] = count.
 // clear: zero the slot buffers after reading (they return to the host-side pool
 // ready for the next conv epilogue / reduce -- no memset launch).

@@ -61,13 +61,6 @@ struct ConvArgs {
   // problem z reads src + z * bs_src, wt + z * bs_wt and writes out + z * bs_out
   int batch;
   long long bs_src, bs_wt, bs_out;
-  // TX (dgrad of a 1x1 conv whose dY is a BN-backward output, see the TX note at the
-  // kernel): the gathered operand is dzm (= src), and every A element is replaced by
-  //   a[k] * dzm + b[k] * tx_y + c[k]     (coef [3][tx_cp]: a | b | c)
-  // i.e. bn_bwd_elemt is applied while the operand is read; dY is never stored.
-  const bf16_t* tx_y;
-  const float* tx_coef;
-  int tx_cp;
   // F8 (fp8 dgrad, BASELINE config 5): src is e5m2 dY and wt an e4m3 [Nout][Kg] image
   // (byte pointers behind the bf16_t* fields); acc is scaled by 1 / (f8_sa * f8_sb)
   const float* f8_sa;
@@ -150,26 +143,18 @@ __device__ __forceinline__ int swz(int row) {
 // their A fragments from that halo image at a wave-uniform pixel offset, instead of
 // gathering every input pixel 9 times from L2 (the 64/128-channel 3x3 layers are
 // bound by that L2->LDS gather traffic); only the weight tiles stream per K-tile.
-//
-// TX: the A operand of a 1x1 dgrad is the BN-backward output dy = a*dzm + b*y + c
-// (per channel k of the reduction); both dzm and y tiles are LDS-DMA'd side by side
-// and the fragment is transformed in registers right after its ds_read -- the
-// BN-backward elementwise pass (3 tensor passes) becomes one extra operand read.
-// 1x1 only: a zero-filled (padded) A chunk would become c[k], not 0; a 1x1 dgrad has
-// no padded taps, and K-tile tails read zero coefficients.
 template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA, bool MF32 = false,
-          int WM = 2, int WN = 2, bool P8 = false, bool HALO = false, int NB = 2, bool TX = false,
-          bool F8 = false, int NST1 = 0>
+          int WM = 2, int WN = 2, bool P8 = false, bool HALO = false, int NB = 2, bool F8 = false,
+          int NST1 = 0>
 __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) void conv_igemm_kernel(ConvArgs a) {
   constexpr int NW = WM * WN, NT = 64 * NW;
-  static_assert(!TX || (DGRAD && DMA && !MF32 && !P8 && !HALO), "TX: DMA dgrad, 16x16 MFMA, plain pipeline");
   static_assert(DMA || (BK == 64 && NST == 2 && NW == 4), "register staging: BK=64, 2 stages, 4 waves");
   // F8: fp8 operands (1 B per element) in the same 128-B LDS rows (BK = 64 bf16 slots =
   // 128 fp8 reduction elements per K-tile), one v_mfma_scale_f32_16x16x128_f8f6f4 per
   // fragment pair and K-tile; NST1: a single LDS stage (load, wait, compute) for the
   // one- or two-K-tile reductions of the epilogue-bound dgrads (occupancy of the bf16 BK=32
   // tiles: 4 blocks per CU)
-  static_assert(!F8 || (DMA && BK == 64 && !MF32 && !P8 && !HALO && !TX), "F8: LDS-DMA, 128-B rows, plain pipeline");
+  static_assert(!F8 || (DMA && BK == 64 && !MF32 && !P8 && !HALO), "F8: LDS-DMA, 128-B rows, plain pipeline");
   static_assert(!NST1 || (F8 && NST == 2), "NST1: fp8 only");
   static_assert(!MF32 || (DMA && BK == 64), "32x32 MFMA path: LDS-DMA, BK=64");
   static_assert(!P8 || (DMA && BK == 64 && NST == 2 && !MF32), "P8: LDS-DMA, BK=64, 2 buffers, 16x16 MFMA");
@@ -190,13 +175,13 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
   constexpr int PB = DMA ? BN / (NW * RPI) : BN / 32;
   static_assert(PA >= 1 && PB >= 1, "tile too small for this BK");
   static_assert(!DMA || ((BM / NW) % RPI == 0 && (BN / NW) % RPI == 0), "wave row slabs");
-  constexpr int LPT = PA * (TX ? 2 : 1) + PB;
+  constexpr int LPT = PA + PB;
   constexpr int MI = BM / (16 * WM);  // 16-row MFMA tiles per wave
   constexpr int NI = BN / (16 * WN);  // 16-col MFMA tiles per wave
   constexpr int LDR = DMA ? BK : BK + 8;  // LDS row length (elements)
   constexpr int A_ELEMS = BM * LDR;
   constexpr int B_ELEMS = BN * LDR;
-  constexpr int STAGE = A_ELEMS + B_ELEMS + (TX ? A_ELEMS : 0);  // TX: y tile after B
+  constexpr int STAGE = A_ELEMS + B_ELEMS;
   constexpr int LDC = BN + 8;
   // epilogue C-staging layout (SWAPC only): EPI_SW = 8-B half swap in rows with bit 3
   // set (conflict-free ds_write_b64); EPI_RM = row order of the ds_read_b128 row reads
@@ -352,13 +337,11 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
   // per-row source pointers at tap (0,0) channel 0 (+ this lane's chunk); a tile
   // then only adds the wave-uniform offset (dr*W + ds)*Cs + cb
   const ET* a_ptr[PA];
-  const bf16_t* y_ptr[TX ? PA : 1];
 #pragma unroll
   for (int i = 0; i < PA; ++i) {
     const int ci = MF32 ? lane_c32[i & 1] : achunk(i) * CE;
     // signed: u_p is -1.. at padded borders (never dereferenced there: `ok` masks it)
     a_ptr[i] = srcE + ((long long)u_p[i] << a.log2Cs) + ci;
-    if constexpr (TX) y_ptr[i] = a.tx_y + ((long long)u_p[i] << a.log2Cs) + ci;
   }
   auto load_tile_uni = [&](int kt, int dbuf) {
     (void)kt;
@@ -384,11 +367,6 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
       const void* src = ok ? (const void*)(a_ptr[i] + aoff) : (const void*)g_zero16;
       bf16_t* dst = lds + dbuf * STAGE + (wid_s * (BM / NW) + RPI * i) * LDR;
       glds16<1>(src, dst, a_once);
-      if constexpr (TX) {
-        const void* sy = ok ? (const void*)(y_ptr[i] + aoff) : (const void*)g_zero16;
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)sy,
-                                         (__attribute__((address_space(3))) void*)(dst + A_ELEMS + B_ELEMS), 16, 0, 0);
-      }
     }
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
@@ -437,13 +415,6 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
         if (ok) src = srcE + (((size_t)(a_base[i] + ih * a.W + iw)) << a.log2Cs) + c;
         bf16_t* dst = lds + dbuf * STAGE + (wid * (BM / NW) + RPI * i) * LDR;
         glds16<1>(src, dst, a_once);
-        if constexpr (TX) {
-          const void* sy = g_zero16;
-          if (ok) sy = a.tx_y + (((size_t)(a_base[i] + ih * a.W + iw)) << a.log2Cs) + c;
-          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)sy,
-                                           (__attribute__((address_space(3))) void*)(dst + A_ELEMS + B_ELEMS), 16, 0,
-                                           0);
-        }
       } else {
         uint4 v = make_uint4(0, 0, 0, 0);
         if (ok) {
@@ -598,33 +569,6 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
       const int q = ks * 4 + (lane >> 4);
 #pragma unroll
       for (int i = 0; i < MI; ++i) af[i] = frag(As, wm * (BM / WM) + i * 16 + frow, q);
-      if constexpr (TX) {
-        // this lane's 8 reduction channels of the K-step: kt*BK + 8q .. +7 (1x1: Kg = channels)
-        const int ch = kt * BK + q * 8;
-        float ca[8], cb[8], cc[8];
-        const float* cf = a.tx_coef + ch;
-        {
-          const float4 x0 = *reinterpret_cast<const float4*>(cf), x1 = *reinterpret_cast<const float4*>(cf + 4);
-          const float4 y0 = *reinterpret_cast<const float4*>(cf + a.tx_cp);
-          const float4 y1 = *reinterpret_cast<const float4*>(cf + a.tx_cp + 4);
-          const float4 z0 = *reinterpret_cast<const float4*>(cf + 2 * a.tx_cp);
-          const float4 z1 = *reinterpret_cast<const float4*>(cf + 2 * a.tx_cp + 4);
-          ca[0] = x0.x; ca[1] = x0.y; ca[2] = x0.z; ca[3] = x0.w; ca[4] = x1.x; ca[5] = x1.y; ca[6] = x1.z; ca[7] = x1.w;
-          cb[0] = y0.x; cb[1] = y0.y; cb[2] = y0.z; cb[3] = y0.w; cb[4] = y1.x; cb[5] = y1.y; cb[6] = y1.z; cb[7] = y1.w;
-          cc[0] = z0.x; cc[1] = z0.y; cc[2] = z0.z; cc[3] = z0.w; cc[4] = z1.x; cc[5] = z1.y; cc[6] = z1.z; cc[7] = z1.w;
-        }
-        const bf16_t* Ys = lds + buf * STAGE + A_ELEMS + B_ELEMS;
-#pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          const bf16x8 yv = frag(Ys, wm * (BM / WM) + i * 16 + frow, q);
-          float d[8], yy[8], o[8];
-          unpack8(__builtin_bit_cast(uint4, af[i]), d);
-          unpack8(__builtin_bit_cast(uint4, yv), yy);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = ca[e] * d[e] + cb[e] * yy[e] + cc[e];
-          af[i] = __builtin_bit_cast(bf16x8, pack8(o));
-        }
-      }
 #pragma unroll
       for (int j = 0; j < NI; ++j) bfg[j] = frag(Bs, wn * (BN / WN) + j * 16 + frow, q);
 #pragma unroll
@@ -1111,8 +1055,8 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
       }
       if (nbn) {
         // the output IS a BN site's dz; every consumer gates it with this same ReLU
-        // mask (BN backward, identity-path addend), so store dzm = dz * mask -- the
-        // form the BN-backward-on-load (TX) consumers read (bit-exact zeroing)
+        // mask (BN backward, identity-path addend), so store dzm = dz * mask (bit-exact
+        // zeroing; the fused reduce below sums exactly what is stored)
         const uint32_t mk = mb[g];
         o.x &= ((mk & 1u) ? 0x0000ffffu : 0u) | ((mk & 2u) ? 0xffff0000u : 0u);
         o.y &= ((mk & 4u) ? 0x0000ffffu : 0u) | ((mk & 8u) ? 0xffff0000u : 0u);
@@ -1310,26 +1254,6 @@ static void launch_k(const ConvArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, NST, DGRAD, STATS, DMA, MF32, WM, WN, P8, HALO, 0>), grid,
                        block, 0, st, a);
   }
-}
-
-// TX dgrad (BN backward applied on load, 1x1 only): the fixed configuration of the
-// short-reduction fused-epilogue dgrads -- 128x128 (or 128x64) tiles, LDS-DMA BK=32,
-// 2 (3) stages -- with the y tile next to dzm in each stage (no autotuning)
-template <int BM, int BN, int NST>
-static void launch_tx(const ConvArgs& a, hipStream_t st) {
-  const int Mgrid = a.stride == 2 ? a.N * ((a.OH + 1) >> 1) * ((a.OW + 1) >> 1) : a.M;
-  const int tiles = ((Mgrid + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
-  const dim3 grid(tiles, a.stride == 2 ? 4 : 1, 1), block(256);
-  const int nb = a.bn_red[0] ? (a.bn_red[1] ? 2 : 1) : 0;
-  if (nb == 2)
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 32, NST, true, false, true, false, 2, 2, false, false, 2, true>),
-                       grid, block, 0, st, a);
-  else if (nb == 1)
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 32, NST, true, false, true, false, 2, 2, false, false, 1, true>),
-                       grid, block, 0, st, a);
-  else
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 32, NST, true, false, true, false, 2, 2, false, false, 0, true>),
-                       grid, block, 0, st, a);
 }
 
 // HALO conv (see the kernel): 3x3, stride 1, pad 1, Cs % 64 == 0, 7 <= W <= 56
@@ -1657,7 +1581,7 @@ static int conv_igemm_launch_b(const bf16_t* src, const bf16_t* wt, bf16_t* out,
                                int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
                                bool dgrad, const bf16_t* addend, const uint8_t* addend_mask,
                                const BnReduceArgs* bnr, hipStream_t st, const float* shift, int batch,
-                               long long bs_src, long long bs_wt, long long bs_out, const TxArgs* tx) {
+                               long long bs_src, long long bs_wt, long long bs_out) {
   if (Cs % 8 != 0 || (Cs & (Cs - 1)) != 0) return 1;  // power-of-two channels (>= 8)
   if (Nout % 8 != 0) return 2;
   if (stride != 1 && stride != 2) return 3;
@@ -1706,22 +1630,8 @@ static int conv_igemm_launch_b(const bf16_t* src, const bf16_t* wt, bf16_t* out,
   if (M >= (1ll << 31) || (long long)N * H * W >= (1ll << 31)) return 4;
   a.M = (int)M;
   a.Kg = R * S * Cs;
-  a.tx_y = nullptr;
-  a.tx_coef = nullptr;
-  a.tx_cp = 0;
   a.f8_sa = nullptr;
   a.f8_sb = nullptr;
-  if (tx && tx->y) {
-    // BN backward on load: 1x1 dgrads only (see the TX note), coefficients cover every K-tile
-    if (!dgrad || R != 1 || S != 1 || pad != 0 || batch != 1 || !tx->coef || tx->cp < (Cs + 31) / 32 * 32)
-      return 7;
-    a.tx_y = tx->y;
-    a.tx_coef = tx->coef;
-    a.tx_cp = tx->cp;
-    if (a.Nout > 64) launch_tx<128, 128, 2>(a, st);
-    else launch_tx<128, 64, 3>(a, st);
-    return 0;
-  }
   if (dgrad) {
     if (stats) launch_sel<true, true>(a, st);
     else launch_sel<true, false>(a, st);
@@ -1744,7 +1654,7 @@ static void launch_f8(const ConvArgs& a, hipStream_t st) {
   const dim3 grid(tiles, ph2 ? 4 : 1, 1), block(256);
   const int nb = a.bn_red[0] ? (a.bn_red[1] ? 2 : 1) : 0;
 #define F8K(NBV) \
-  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 64, 2, true, false, true, false, 2, 2, false, false, NBV, false, true, \
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 64, 2, true, false, true, false, 2, 2, false, false, NBV, true, \
                                         ONE ? 1 : 0>), grid, block, 0, st, a)
   if (nb == 2) F8K(2);
   else if (nb == 1) F8K(1);
@@ -1800,9 +1710,9 @@ int conv_dgrad_fp8_launch(const uint8_t* dyq, const uint8_t* wtq, const float* s
 int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* stats, int N, int H,
                       int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
                       bool dgrad, const bf16_t* addend, const uint8_t* addend_mask,
-                      const BnReduceArgs* bnr, hipStream_t st, const float* shift, const TxArgs* tx) {
+                      const BnReduceArgs* bnr, hipStream_t st, const float* shift) {
   return conv_igemm_launch_b(src, wt, out, stats, N, H, W, Cs, OH, OW, Nout, R, S, stride, pad, dgrad, addend,
-                             addend_mask, bnr, st, shift, 1, 0, 0, 0, tx);
+                             addend_mask, bnr, st, shift, 1, 0, 0, 0);
 }
 
 // `batch` independent forward convolutions of one shape in ONE launch (grid.z), no
@@ -1811,7 +1721,7 @@ int conv_igemm_batched_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, 
                               long long bs_wt, long long bs_out, int N, int H, int W, int Cs, int OH, int OW,
                               int Nout, int R, int S, int stride, int pad, hipStream_t st) {
   return conv_igemm_launch_b(src, wt, out, nullptr, N, H, W, Cs, OH, OW, Nout, R, S, stride, pad, false, nullptr,
-                             nullptr, nullptr, st, nullptr, batch, bs_src, bs_wt, bs_out, nullptr);
+                             nullptr, nullptr, st, nullptr, batch, bs_src, bs_wt, bs_out);
 }
 
 void conv_weight_prep_launch(const float* w, bf16_t* wk, bf16_t* wkt, int K, int RS, int C, int Cp,

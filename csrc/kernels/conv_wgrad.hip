@@ -39,11 +39,6 @@ struct WgradArgs {
   int P, Q, K, R, S, stride, pad;
   int M, Kg;
   int chunks_per_split;  // 64-row chunks per block
-  // TX: dy holds dzm and the operand is a[k] dzm + b[k] tx_y + c[k] (BN backward on
-  // load, coef [3][tx_cp]); register-staged kernel only
-  const bf16_t* tx_y;
-  const float* tx_coef;
-  int tx_cp;
 };
 
 constexpr int BR = 64;  // reduction rows per stage
@@ -64,7 +59,7 @@ __device__ __forceinline__ int toff(int row, int col) {
   return row * ROWB + (((byte >> 5) ^ swz<ROWB>(row)) << 5) + (byte & 31);
 }
 
-template <int BM, int BN, bool TX = false>
+template <int BM, int BN>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
   constexpr int MI = BM / 32, NI = BN / 32;
   constexpr int A_BYTES = BR * BM * 2, B_BYTES = BR * BN * 2;
@@ -115,17 +110,6 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
   const int dq = BR % a.Q, dp = (BR / a.Q) % a.P, dn = BR / pq;
   // operands read by a single tile column / row: non-temporal (see glds16)
   const bool dy_once = tilesN == 1, x_once = tilesM == 1 && a.R == 1 && a.S == 1;
-  // TX: this thread's 8 dY channels are fixed for the whole kernel
-  float ta[8], tb[8], tc[8];
-  if constexpr (TX) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int k = a_colok ? k0 + a_col + e : 0;
-      ta[e] = a.tx_coef[k];
-      tb[e] = a.tx_coef[a.tx_cp + k];
-      tc[e] = a.tx_coef[2 * a.tx_cp + k];
-    }
-  }
 
   uint4 ra[PA], rb[PB];
   auto load = [&](int ch) {
@@ -134,18 +118,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradArgs a) {
     for (int i = 0; i < PA; ++i) {
       const int m = mb + a_row + RA * i;
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (a_colok && m < mend) {
-        v = ld16c<2>(a.dy + (size_t)m * a.K + k0 + a_col, dy_once);
-        if constexpr (TX) {
-          const uint4 yv = *reinterpret_cast<const uint4*>(a.tx_y + (size_t)m * a.K + k0 + a_col);
-          float d[8], yy[8], o[8];
-          unpack8(v, d);
-          unpack8(yv, yy);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = ta[e] * d[e] + tb[e] * yy[e] + tc[e];
-          v = pack8(o);
-        }
-      }
+      if (a_colok && m < mend) v = ld16c<2>(a.dy + (size_t)m * a.K + k0 + a_col, dy_once);
       ra[i] = v;
     }
 #pragma unroll
@@ -1041,13 +1014,8 @@ static void wgrad_run(int impl, WgradArgs a, float* ws, hipStream_t st) {
   const bool k64 = a.K == 64;
   switch (impl) {
     case 0:
-      if (a.tx_y) {
-        if (k64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128, true>), grid, dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((conv_wgrad_kernel<128, 128, true>), grid, dim3(256), 0, st, a);
-      } else {
-        if (k64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128>), grid, dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), grid, dim3(256), 0, st, a);
-      }
+      if (k64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), grid, dim3(256), 0, st, a);
       break;
     case 2:  // DMA, 32-row stages, 4-deep ring
       if (k64) hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 128, 32, 4>), grid, dim3(256), 0, st, a);
@@ -1232,8 +1200,7 @@ int conv_wgrad_splits(int N, int H, int W, int C, int P, int Q, int K, int R, in
 }
 
 int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, float* ws, int N, int H, int W,
-                      int C, int P, int Q, int K, int R, int S, int stride, int pad, hipStream_t st,
-                      const TxArgs* tx) {
+                      int C, int P, int Q, int K, int R, int S, int stride, int pad, hipStream_t st) {
   if (C % 8 != 0 || (C & (C - 1)) != 0) return 1;
   if (K % 64 != 0) return 2;
   if ((long long)N * P * Q >= (1ll << 31)) return 4;
@@ -1241,20 +1208,8 @@ int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, float* ws, i
   a.dy = dy;
   a.x = x;
   a.dw = dw;
-  a.tx_y = nullptr;
-  a.tx_coef = nullptr;
-  a.tx_cp = 0;
   fill_args(a, N, H, W, C, P, Q, K, R, S, stride, pad);
   if (!ws && conv_wgrad_splits(N, H, W, C, P, Q, K, R, S, stride, pad) > 1) return 5;
-  if (tx && tx->y) {
-    // BN backward applied on load: the register-staged variant, no autotuning
-    if (!tx->coef || tx->cp < K) return 6;
-    a.tx_y = tx->y;
-    a.tx_coef = tx->coef;
-    a.tx_cp = tx->cp;
-    wgrad_run(0, a, ws, st);
-    return 0;
-  }
   int impl = wgrad_impl();
   if (!wgrad_cfg_ok(impl, a)) impl = 1;
   if (impl == 1 && wgrad_autotune_on()) {

@@ -18,18 +18,10 @@ struct BnReduceArgs {
 };
 // stats (optional): BN statistic slots [kStatSlots][2][Nout] of (sum (y-K), sum (y-K)^2) with
 // K = shift[n] (nullable: 0) -- see bn_moments in common.h
-// BN backward applied while a 1x1 dgrad / wgrad reads its dY operand (see conv_igemm.hip
-// TX): dY = a*src + b*y + c per channel, coef [3][cp] fp32 (a | b | c)
-struct TxArgs {
-  const bf16_t* y;
-  const float* coef;
-  int cp;
-};
 int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* stats, int N, int H,
                       int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
                       bool dgrad, const bf16_t* addend, const uint8_t* addend_mask,
-                      const BnReduceArgs* bnr, hipStream_t st, const float* shift = nullptr,
-                      const TxArgs* tx = nullptr);
+                      const BnReduceArgs* bnr, hipStream_t st, const float* shift = nullptr);
 // `batch` same-shape forward convolutions in one launch (grid.z), no epilogue fusions
 int conv_igemm_batched_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, int batch, long long bs_src,
                               long long bs_wt, long long bs_out, int N, int H, int W, int Cs, int OH, int OW,
@@ -69,8 +61,7 @@ int conv_wgrad_splits(int N, int H, int W, int C, int P, int Q, int K, int R, in
                       int pad);
 // dw += dW (dw must be initialised: zeros or an accumulation target)
 int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, float* ws, int N, int H, int W,
-                      int C, int P, int Q, int K, int R, int S, int stride, int pad, hipStream_t st,
-                      const TxArgs* tx = nullptr);
+                      int C, int P, int Q, int K, int R, int S, int stride, int pad, hipStream_t st);
 // FP8 weight gradient: e5m2 dY x e4m3 X on the scaled 16x16x128 MFMA (kernels/conv_wgrad.hip)
 // FP8 data gradient: e5m2 dY [N,P,Q,K] x e4m3 wkt image [Cp][R][S][K] -> bf16 dX [N,H,W,Cp] with the
 // bf16 dgrad's epilogue (addend (+mask), fused BN-backward reduce) (kernels/conv_igemm.hip)
@@ -101,8 +92,6 @@ int bn_apply_launch(const bf16_t* y1, const float* p1, const bf16_t* r, const fl
                     const float* qscale, float* qamax, hipStream_t st);
 int bn_bwd_reduce_launch(const bf16_t* dout, const uint8_t* mask, const bf16_t* y,
                          const float* params, float* red, int M, int C, bool relu, hipStream_t st);
-int bn_bwd_coef_launch(const float* params, const float* gamma, const float* red, const float* count,
-                       float count_h, float* coef, int C, int Cp, bool eval_mode, hipStream_t st);
 int bn_bwd_elemt_launch(const bf16_t* dout, const uint8_t* mask, const bf16_t* y, const float* params,
                         const float* gamma, const float* red, const float* count, float count_h,
                         bf16_t* dy, bf16_t* dzm, long long M, int C, bool relu, bool eval_mode,

@@ -27,8 +27,10 @@ def build_parser():
     p.add_argument("--image_size", default=None, type=int, help="input size (32 cifar / 224 imagenet)")
     p.add_argument("--num_classes", default=None, type=int, help="10 cifar / 1000 imagenet")
     p.add_argument("--dtype", default="auto", choices=["auto", "bf16", "fp32", "fp8"],
-                   help="activation dtype (auto: bf16 on GPU, fp32 on CPU); fp8 = block-conv "
-                        "forwards on the e4m3 scaled MFMA with bf16 elsewhere (GPU only)")
+                   help="activation dtype (auto: bf16 on GPU, fp32 on CPU); fp8 = every block conv's "
+                        "forward, data gradient and weight gradient on the scaled fp8 MFMA (e4m3 "
+                        "weights/activations, e5m2 gradients, delayed per-tensor scaling), stem, "
+                        "classifier and BatchNorm in bf16/fp32 (GPU only)")
     p.add_argument("--backend", default="auto", choices=["auto", "nccl", "rccl", "gloo"],
                    help="auto: RCCL (torch 'nccl') with GPUs, gloo on CPU")
     p.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
@@ -71,10 +73,11 @@ def build_parser():
                    help="gradient bucket reducer implementation")
     p.add_argument("--grad_compress", default="none", choices=["none", "bf16"],
                    help="wire dtype of the gradient all-reduce")
-    p.add_argument("--comm", default="c10d", choices=["c10d", "rccl"],
-                   help="gradient-bucket transport: torch ProcessGroupNCCL (c10d, default) or the "
-                        "framework's own RCCL communicator (csrc/runtime/rccl_comm.cpp; "
-                        "experimental: needs the xGMI SyncBN transport or --sync_bn off)")
+    p.add_argument("--comm", default="auto", choices=["auto", "c10d", "rccl"],
+                   help="gradient-bucket transport: auto (default) = the framework's own RCCL "
+                        "communicator (csrc/runtime/rccl_comm.cpp) when it can be the only in-step "
+                        "communicator (SyncBN on the xGMI kernel or off) and its startup self-test "
+                        "passes, else torch ProcessGroupNCCL (c10d); the choice is printed")
     p.add_argument("--last_bucket_mb", default=2.0, type=float,
                    help="cap of the LAST gradient bucket (earliest layers: its all-reduce is "
                         "launched at the end of backward, fully exposed)")

@@ -233,7 +233,7 @@ def _run(rank, world_size, args, dev):
                          broadcast_buffers=args.broadcast_buffers,
                          reducer=getattr(args, "reducer", "native"),
                          compress=getattr(args, "grad_compress", "none"),
-                         transport=getattr(args, "comm", "c10d") if on_gpu else "c10d",
+                         transport=getattr(args, "comm", "auto") if on_gpu else "c10d",
                          last_bucket_mb=getattr(args, "last_bucket_mb", 2.0))
     if rank == 0 and comm is not None:
         print("[pmd] gradient buckets (MiB, launch order): "

@@ -40,7 +40,6 @@ import weakref
 import torch
 
 from . import torch_prims
-from .lazy import LazyDy, is_lazy
 
 _NAN_CHECK = os.environ.get("PMD_NAN_CHECK", "0") == "1"   # debug: finite-check block backward
 
@@ -299,8 +298,6 @@ def _wgrad(P, dy, x, wpack, stride, pad, w, xq=None):
     """Weight gradient: accumulated into the arena (returns None) or returned."""
     if not w.requires_grad:
         return None
-    if is_lazy(dy):
-        dy = dy.materialize()
     cx = wpack[0].shape[-1]
     tgt = _grad_target(w)
     if tgt is not None and cx == w.shape[1]:
@@ -364,15 +361,11 @@ class _WgradSide:
     def wgrad(self, P, dy, x, wpack, stride, pad, w, xq=None):
         if not self.on or _grad_target(w) is None:
             return _wgrad(P, dy, x, wpack, stride, pad, w, xq)
-        # dy may be a LazyDy: its record_stream covers dzm, y and the coefficients
         _claim(w)
         self.side.wait_stream(self.main)
         with torch.cuda.stream(self.side):
             tgt = _grad_target(w)
-            # a LazyDy (BN backward applied by the main-stream dgrad) is materialised
-            # HERE, on the side stream: the elementwise pass leaves the critical path
-            dyw = dy.materialize() if is_lazy(dy) else dy
-            _conv_wgrad_any(P, dyw, x, xq, tuple(wpack[0].shape), stride, pad, out=tgt.permute(0, 2, 3, 1))
+            _conv_wgrad_any(P, dy, x, xq, tuple(wpack[0].shape), stride, pad, out=tgt.permute(0, 2, 3, 1))
         dy.record_stream(self.side)
         x.record_stream(self.side)
         dq = getattr(dy, "_pmd_q8", None)
@@ -552,38 +545,7 @@ def _bn_forward_params(P, y, st, bn, training, sync, y2=None, st2=None, bn2=None
     return p1, p2, count
 
 
-# BN backward applied by the consumer 1x1 dgrad while it reads dY (ops/lazy.py,
-# PMD_BN_TX=1).  Built, correct (tests/test_bn_tx_gpu.py) and OFF by default: the
-# whole step measured 20.1 -> 21.1 ms with it (docs/ARCHITECTURE.md, "BN backward on load")
-_BN_TX = os.environ.get("PMD_BN_TX", "0") == "1"
-
-
-def set_bn_tx(flag: bool):
-    global _BN_TX
-    _BN_TX = bool(flag)
-
-
-def _tx_ok(P, conv_m, pre, training):
-    """Can ``conv_m`` consume this BN site's dY lazily?  1x1 conv (no padded taps),
-    gfx950 prims, training, and dZ already gated by the ReLU mask -- which the
-    fused-reduce dgrad that produced it (``pre``) guarantees.
-
-    Used for the block-final BN of a Bottleneck only (its consumer conv3 reduces
-    over 4x planes channels into planes: the largest dY for the smallest output):
-    there the TX dgrad on the main stream replaces bn_bwd_elemt + dgrad (l1: 270 vs
-    393 us, l2: 159 vs 210 us, bench/dgrad_epi_bench.py --tx), and the weight
-    gradient -- whose TX variant is 2-3x slower than the DMA wgrad -- materialises
-    dY on the side stream, off the critical path (:meth:`_WgradSide.wgrad`).  For
-    the conv1 / shortcut consumers (small reduction, epilogue-bound) the TX dgrad
-    measured slower than the elementwise pass it replaces."""
-    return (_BN_TX and training and pre is not None and getattr(P, "SUPPORTS_TX", False)
-            and tuple(conv_m.weight.shape[2:]) == (1, 1))
-
-
-def _elemt(P, dout, mask, y, p, gamma, red, count, relu, want_dzm=False, lazy=False, q8=None):
-    if lazy and not want_dzm and q8 is None:
-        return LazyDy(dout, y, P.bn_bwd_coef(p, gamma, red, count),
-                      (P, mask, p, gamma, red, count, relu)), None
+def _elemt(P, dout, mask, y, p, gamma, red, count, relu, want_dzm=False, q8=None):
     if q8 is not None and not want_dzm:
         # + the e5m2 copy of dY for the fp8 weight / data gradients (dy._pmd_q8); q8[2]: it
         # is the only copy (both consumers of this dY run in fp8)
@@ -593,14 +555,13 @@ def _elemt(P, dout, mask, y, p, gamma, red, count, relu, want_dzm=False, lazy=Fa
 
 
 def _bn_backward(P, dout, mask, relu, training, sync, count, y1, p1, bn1, y2=None, p2=None,
-                 bn2=None, want_dzm=False, pre=None, elemt_fn=None, lazy=(False, False), q8=(None, None)):
+                 bn2=None, want_dzm=False, pre=None, elemt_fn=None, q8=(None, None)):
     """BN(+second BN)(+ReLU) backward. Returns (dy1, dy2, dzm, grads) with
     grads = [d_g1, d_b1, d_g2, d_b2] for params that were NOT written directly.
     ``pre``: the reduce results already produced by the dgrad that computed
     ``dout`` (fused epilogue), in the order (bn1[, bn2]).  ``elemt_fn(red, count)``
     replaces the elementwise pass of BN 1 (fused stem: it re-derives dz itself;
-    red/count are None in eval mode).  ``lazy[i]``: return dY of BN i as a
-    :class:`LazyDy` (its consumer is a 1x1 conv that applies it on load).  ``q8[i]``:
+    red/count are None in eval mode).  ``q8[i]``:
     (scale, amax) of an e5m2 copy of dY of BN i for an fp8 weight gradient."""
     if pre is not None:
         r1 = pre[0]
@@ -640,11 +601,11 @@ def _bn_backward(P, dout, mask, relu, training, sync, count, y1, p1, bn1, y2=Non
             dy1, dzm = elemt_fn(red[:2 * c1].view(2, c1), count), None
         else:
             dy1, dzm = _elemt(P, dout, mask, y1, p1, bn1.weight, red[:2 * c1].view(2, c1), count,
-                              relu, want_dzm=want_dzm, lazy=lazy[0], q8=q8[0])
+                              relu, want_dzm=want_dzm, q8=q8[0])
         dy2 = None
         if y2 is not None:
             dy2, _ = _elemt(P, dout, mask, y2, p2, bn2.weight, red[2 * c1:].view(2, -1), count,
-                            relu, lazy=lazy[1], q8=q8[1])
+                            relu, q8=q8[1])
         return dy1, dy2, dzm, [None, None, None, None]
     red = P.stats_collapse(r1, r2, None, acc1, acc2)     # local sums; gamma/beta grads += local
     grads = [None, None, None, None]
@@ -666,11 +627,11 @@ def _bn_backward(P, dout, mask, relu, training, sync, count, y1, p1, bn1, y2=Non
             dy1, dzm = elemt_fn(red[:2 * c1].view(2, c1), count), None
         else:
             dy1, dzm = _elemt(P, dout, mask, y1, p1, bn1.weight, red[:2 * c1].view(2, c1),
-                              count, relu, want_dzm=want_dzm, lazy=lazy[0], q8=q8[0])
+                              count, relu, want_dzm=want_dzm, q8=q8[0])
         dy2 = None
         if y2 is not None:
             dy2, _ = _elemt(P, dout, mask, y2, p2, bn2.weight, red[2 * c1:].view(2, -1), count,
-                            relu, lazy=lazy[1], q8=q8[1])
+                            relu, q8=q8[1])
     elif elemt_fn is not None:
         dy1, dy2, dzm = elemt_fn(None, None), None, None
     else:
@@ -846,10 +807,10 @@ class _StemPoolFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, cfg, y, st, g, b):
-        bn, training = cfg
+        bn, training, k1 = cfg
         P = prims_for(y)
         sync = _state["bn_sync"] if training else None
-        p, _, count = _bn_forward_params(P, y, st, bn, training, sync)
+        p, _, count = _bn_forward_params(P, y, st, bn, training, sync, k1=k1)
         out, arg = P.stem_pool_fwd(y, p)
         ctx.cfg = (bn, training, sync, count)
         ctx.arg = arg
@@ -883,8 +844,10 @@ def set_fused_stem(flag: bool):
 
 
 def bn_relu_maxpool(y, stats, bn):
-    """maxpool3x3s2(relu(BN(y))) for the ImageNet stem (fused on the gfx950 path)."""
-    return _StemPoolFn.apply((bn, bn.training), y, stats, bn.weight, bn.bias)
+    """maxpool3x3s2(relu(BN(y))) for the ImageNet stem (fused on the gfx950 path).
+    Consumes the statistics shift :func:`conv` registered for ``stats`` (like
+    :func:`bn_add_act`), so no registry entry outlives the step."""
+    return _StemPoolFn.apply((bn, bn.training, _pop_shift(stats)), y, stats, bn.weight, bn.bias)
 
 
 # ------------------------------------------------------------ residual block
@@ -1058,8 +1021,12 @@ class _ResidualBlockFn(torch.autograd.Function):
 
         def chk(name, t):
             if nan_check and t is not None:
-                if is_lazy(t):
-                    t = t.materialize()
+                q8 = getattr(t, "_pmd_q8", None)
+                if t.dtype == torch.uint8 and q8 is not None:
+                    # an e5m2-only dY (fp8 gradients): the raw bytes are always "finite"
+                    # as floats, so check the dequantised values
+                    from .native import C
+                    t = C.dequant_fp8(t, 1.0 / q8[1], bf8=True)
                 if not torch.isfinite(t.float()).all():
                     raise FloatingPointError(f"non-finite {name} in block backward ({fconv.weight.shape})")
         chk("dout", dout)
@@ -1089,7 +1056,6 @@ class _ResidualBlockFn(torch.autograd.Function):
             wps = tuple(sv[i + 2:i + 2 + nws])
             dyf, dys, _, g = _bn_backward(P, dout, omask, True, training, sync, countf,
                                           yf, pf, fbn, ys, ps, sbn, pre=pre,
-                                          lazy=(_tx_ok(P, fconv, pre, training), False),
                                           q8=(gsite(nst, fbn), gsite(nst + 1, sbn)))
             put(sbn.weight, g[2])
             put(sbn.bias, g[3])
@@ -1099,7 +1065,6 @@ class _ResidualBlockFn(torch.autograd.Function):
             # stage's dgrad epilogue adds dout gated by the mask bits
             dyf, _, _, g = _bn_backward(P, dout, omask, True, training, sync, countf,
                                         yf, pf, fbn, pre=pre,
-                                        lazy=(_tx_ok(P, fconv, pre, training), False),
                                         q8=(gsite(nst, fbn), None))
             dres = (dout, omask)
         put(fbn.weight, g[0])

@@ -36,7 +36,6 @@ def _release(*bufs):
 
 
 SUPPORTS_FP8 = True
-from .lazy import is_lazy  # noqa: E402
 
 
 # ---------------------------------------------------------------------- fp8
@@ -78,24 +77,18 @@ def conv_fwd(x, wpack, stride, pad, want_stats):
 def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None, bnred=None, addend_mask=None):
     """dX (+ addend [* relu bitmask addend_mask]).  ``bnred = (mask, [(y, params)] or
     [(y1, p1), (y2, p2)])`` fuses the BN-backward reduce of dX into the epilogue
-    and returns ``(dx, [slot buffers])`` (same contract as :func:`bn_bwd_reduce`).
-    ``dy`` may be a :class:`.lazy.LazyDy` (1x1 convs): the BN backward is applied
-    while the kernel reads it."""
+    and returns ``(dx, [slot buffers])`` (same contract as :func:`bn_bwd_reduce`)."""
     if len(wpack) < 2:
         raise RuntimeError("dgrad image was not prepared (input did not require grad)")
-    tx = {}
-    if is_lazy(dy):
-        tx = {"tx_y": dy.y, "tx_coef": dy.coef}
-        dy = dy.dzm
     if bnred is None:
         return _C.conv_dgrad(dy, wpack[1], int(x_shape[1]), int(x_shape[2]), int(stride), int(pad),
-                             addend, None, None, None, None, None, None, None, addend_mask, **tx)
+                             addend, None, None, None, None, None, None, None, addend_mask)
     mask, sets = bnred
     bufs = [_acquire(y.shape[-1], y.device) for y, _ in sets]
     (y0, p0), (y1, p1) = sets[0], (sets[1] if len(sets) > 1 else (None, None))
     dx = _C.conv_dgrad(dy, wpack[1], int(x_shape[1]), int(x_shape[2]), int(stride), int(pad),
                        addend, mask, y0, p0, bufs[0], y1, p1, bufs[1] if len(bufs) > 1 else None,
-                       addend_mask, **tx)
+                       addend_mask)
     return dx, bufs
 
 
@@ -120,11 +113,7 @@ def conv_wgrad_fp8(dyq, sdy, xq, sx, wk_shape, stride, pad, out=None):
 
 
 def conv_wgrad(dy, x, wk_shape, stride, pad, out=None):
-    """fp32 [K,R,S,C]; with ``out`` the gradient is accumulated into it.  ``dy`` may
-    be a :class:`.lazy.LazyDy` (BN backward applied on load)."""
-    if is_lazy(dy):
-        return _C.conv_wgrad(dy.dzm, x, int(wk_shape[1]), int(wk_shape[2]), int(stride), int(pad), out,
-                             dy.y, dy.coef)
+    """fp32 [K,R,S,C]; with ``out`` the gradient is accumulated into it."""
     return _C.conv_wgrad(dy, x, int(wk_shape[1]), int(wk_shape[2]), int(stride), int(pad), out)
 
 
@@ -193,16 +182,6 @@ def bn_bwd_elemt(dout, mask, y, p, gamma, red, count, relu, want_dzm=False, q8=N
         d._pmd_q8 = (r[1], q8[0])
         return d, None
     return (r[0], r[1]) if want_dzm else (r[0], None)
-
-
-SUPPORTS_TX = True   # conv_dgrad / conv_wgrad accept a LazyDy (1x1 convs)
-
-
-def bn_bwd_coef(p, gamma, red, count):
-    """[3, Cp] fp32 (a | b | c): dY = a*dzm + b*y + c (the terms of bn_bwd_elemt)."""
-    if torch.is_tensor(count):
-        return _C.bn_bwd_coef(p, gamma.detach(), red, count, 0.0, False)
-    return _C.bn_bwd_coef(p, gamma.detach(), red, None, float(count), False)
 
 
 def bn_bwd_elemt_eval(dout, mask, p, relu, want_dzm=False):

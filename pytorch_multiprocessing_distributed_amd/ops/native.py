@@ -1,10 +1,13 @@
 """Loader for the in-tree gfx950 extension ``_C``.
 
 The extension is built by ``csrc/build.py`` (or ``__graft_entry__.build()``)
-into this package directory so the ``.so`` travels with the repository.  On
-import we rebuild only if a source is newer than the library (cheap mtime
-check) and then load it; a missing or broken build raises loudly -- GPU code
-paths never fall back to PyTorch silently.
+into this package directory so the ``.so`` travels with the repository.  Build
+provenance is content-based: ``_C.stamp.json`` records the sha256 of every
+source the library was built from, and on import that hash is compared with
+the sources in the tree.  A stale or unstamped library is rebuilt (printing
+progress), or -- with ``PMD_NO_AUTOBUILD=1`` -- refused with an ImportError:
+old kernels never run silently.  A missing or broken build raises loudly -- GPU
+code paths never fall back to PyTorch silently.
 """
 from __future__ import annotations
 
@@ -15,15 +18,28 @@ import sys
 _ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def _ensure_built():
+def _build_module():
     sys.path.insert(0, os.path.join(_ROOT, "csrc"))
     try:
         import build as _b  # csrc/build.py
     finally:
         sys.path.pop(0)
-    if os.environ.get("PMD_NO_AUTOBUILD") == "1" and os.path.exists(_b.target_path()):
+    return _b
+
+
+def _ensure_built():
+    """Rebuild unless the library's stamp matches the sources in the tree."""
+    _b = _build_module()
+    st = _b.read_stamp()
+    fresh = (os.path.exists(_b.target_path()) and st is not None
+             and st.get("sources") == _b.source_digest())
+    if fresh:
         return
-    _b.build(verbose=False)
+    if os.environ.get("PMD_NO_AUTOBUILD") == "1":
+        why = "no build stamp" if st is None else "sources changed since the build"
+        raise ImportError(f"stale gfx950 extension {_b.target_path()} ({why}); "
+                          "run `python csrc/build.py` (PMD_NO_AUTOBUILD=1 forbids rebuilding here)")
+    _b.build(verbose=True)
 
 
 def _load():
@@ -40,11 +56,8 @@ def _load():
         sys.modules[spec.name] = mod
         spec.loader.exec_module(mod)
         return mod
-    try:
-        return importlib.import_module("pytorch_multiprocessing_distributed_amd._C")
-    except ImportError:
-        _ensure_built()
-        return importlib.import_module("pytorch_multiprocessing_distributed_amd._C")
+    _ensure_built()
+    return importlib.import_module("pytorch_multiprocessing_distributed_amd._C")
 
 
 C = _load()

@@ -41,6 +41,14 @@ class Comm:
         # and the BN backward (see ops/functional.py::_bn_backward)
         self.overlap_bn_bwd = os.environ.get("PMD_SYNCBN_OVERLAP", "1") != "0"
         self._side = None
+        # native communicators carrying in-step traffic (the gradient reducer's
+        # RcclComm): their asynchronous error state is part of raise_if_failed
+        self.natives = []
+        # set while a native communicator carries the gradient buckets: a c10d
+        # collective inside the step would then run next to them on another
+        # stream (cross-rank deadlock hazard), so the SyncBN path must never fall
+        # back to the process group
+        self.in_step_c10d_forbidden = False
 
     def side_stream(self):
         """High-priority HIP stream for latency-bound SyncBN exchanges (GPU only)."""
@@ -63,9 +71,21 @@ class Comm:
         self.check_same(text, "collective sequence")
 
     def raise_if_failed(self):
-        """Cheap per-step health check (no device sync): xGMI exchange timeouts."""
+        """Cheap per-step health check (no device sync): xGMI exchange timeouts
+        (host-mapped error word) and the asynchronous error state of every
+        attached native RCCL communicator (``ncclCommGetAsyncError``)."""
         if self.xgmi is not None:
             self.xgmi.raise_if_failed()
+        for c in self.natives:
+            if not c.check():
+                raise RuntimeError(f"native RCCL communicator failed or was aborted (rank {self.rank}): "
+                                   "gradient all-reduces of this step are invalid")
+
+    def attach_native(self, c):
+        """Fold a native communicator into :meth:`raise_if_failed`."""
+        if c is not None and c not in self.natives:
+            self.natives.append(c)
+        return c
 
     def enable_xgmi(self, timeout_s: float | None = None):
         """Route small fp32 GPU all-reduces (SyncBN statistics) through the
@@ -89,6 +109,12 @@ class Comm:
         if x is not None and x.accepts(t):
             self._record("xgmi_all_reduce", t)
             return x.all_reduce_(t)
+        if self.in_step_c10d_forbidden:
+            raise RuntimeError(
+                f"SyncBN statistics message of {t.numel()} floats does not fit the xGMI kernel "
+                f"(capacity {x.capacity if x is not None else 0}) and the gradient buckets run on a "
+                "native RCCL communicator: a c10d fallback would put two communicators' collectives "
+                "in flight at once; use --comm c10d")
         return self.all_reduce_(t)
 
     def fused_bn_ok(self, t):

@@ -24,7 +24,9 @@ What it does:
   * transport: ``"c10d"`` -- the torch process group (RCCL via
     ProcessGroupNCCL on GPU, gloo on CPU) -- or ``"rccl"`` -- the framework's
     own RCCL communicator (csrc/runtime/rccl_comm.cpp: uniqueId over the
-    TCPStore, its own HIP stream, hipEvent fences);
+    TCPStore, its own HIP stream, hipEvent fences, exact startup self-test,
+    async-error check every step); ``"auto"`` (default) picks ``rccl`` whenever
+    it can be the only in-step communicator (:func:`resolve_transport`);
   * the bucket bookkeeping + collective launch runs in the native C++
     ``_C.Reducer`` (csrc/runtime/reducer.cpp); ``reducer="python"`` keeps an
     equivalent pure-Python implementation for debugging / cross-checking;
@@ -67,7 +69,16 @@ class _Bucket:
         self.fired = 0
 
 
-def _check_single_in_step_communicator(comm):
+def _max_bn_stats_floats(module):
+    """Largest SyncBN statistics message the model can send through
+    ``Comm.all_reduce_stats_``: a projection block exchanges both of its BNs'
+    [sum | sum^2] in one vector (+1 count), so 4 * max(C) + 1 bounds it."""
+    cs = [int(m.num_features) for m in module.modules()
+          if hasattr(m, "num_features") and hasattr(m, "running_mean")]   # ours and nn.BatchNorm*
+    return 4 * max(cs) + 1 if cs else 0
+
+
+def _check_single_in_step_communicator(comm, module=None):
     """``transport='rccl'`` puts the bucket all-reduces on a SECOND communicator
     (the native ``RcclComm``, its own HIP stream).  Two communicators with
     blocking collective kernels in flight at once on different streams can
@@ -86,6 +97,68 @@ def _check_single_in_step_communicator(comm):
         raise ValueError("transport='rccl' (--comm rccl) with SyncBN over the process group would run "
                          "collectives of two communicators concurrently; use --syncbn_comm xgmi, "
                          "--sync_bn off, or --comm c10d")
+    if sync is not None and module is not None:
+        need = _max_bn_stats_floats(module)
+        if need > sync.xgmi.capacity:
+            raise ValueError(f"transport='rccl': a SyncBN statistics message of up to {need} floats exceeds "
+                             f"the xGMI kernel's capacity ({sync.xgmi.capacity}) and would fall back to a "
+                             "c10d collective inside the step; use --comm c10d")
+
+
+def resolve_transport(comm, module, reducer="native", transport="auto", verbose=True):
+    """Pick the gradient-bucket transport.  ``"auto"`` (the default of main.py and
+    bench.py) takes the native RCCL communicator when it can be the ONLY
+    communicator with collectives inside the step -- native reducer, GPU ranks,
+    SyncBN off or on the one-shot xGMI kernel with room for every statistics
+    message -- and its exact startup self-test passes on every rank; otherwise
+    torch's ProcessGroupNCCL (c10d).  Returns ``(transport, RcclComm or None)``;
+    rank 0 prints the choice and the reason."""
+    if comm is None:
+        return "c10d", None
+    if transport not in ("auto", "c10d", "rccl"):
+        raise ValueError(f"bad transport {transport!r}")
+    if transport == "c10d":
+        return "c10d", None
+    reason = ""
+    if comm.backend != "nccl" and transport == "auto":
+        return "c10d", None                 # CPU / gloo ranks: the process group is the transport
+    if reducer != "native" or comm.backend != "nccl":
+        reason = "needs the native reducer on GPU (nccl) ranks"
+    else:
+        try:
+            _check_single_in_step_communicator(comm, module)
+        except ValueError as e:
+            reason = str(e)
+    if reason:
+        if transport == "rccl":
+            raise ValueError(f"transport='rccl': {reason}")
+        if verbose and comm.rank == 0:
+            print(f"[pmd] gradient transport: c10d ({reason})", flush=True)
+        return "c10d", None
+    from . import rccl
+    c, err = None, ""
+    try:
+        c = rccl.create(comm.group)
+    except Exception as e:  # noqa: BLE001
+        err = str(e)
+    ok = rccl.self_test(c, comm.group) if c is not None else False
+    if c is None:
+        # agree with the ranks that did run the self-test (they all-reduce a flag)
+        flag = torch.tensor([0], device=torch.device("cuda", torch.cuda.current_device()))
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=comm.group)
+    if not ok:
+        if c is not None:
+            c.abort()
+        msg = f"native RCCL communicator self-test failed{': ' + err if err else ''}"
+        if transport == "rccl":
+            raise RuntimeError(msg)
+        if verbose and comm.rank == 0:
+            print(f"[pmd] gradient transport: c10d ({msg})", flush=True)
+        return "c10d", None
+    if verbose and comm.rank == 0:
+        print("[pmd] gradient transport: rccl (native RcclComm, exact self-test passed on "
+              f"{comm.world_size} rank(s))", flush=True)
+    return "rccl", c
 
 
 def _flush_wgrads():
@@ -97,7 +170,7 @@ class DataParallel(nn.Module):
     def __init__(self, module: nn.Module, comm: Comm | None = None, bucket_mb: float = 25.0,
                  first_bucket_mb: float = 1.0, broadcast_buffers: bool = False,
                  check_collectives: bool = True, reducer: str = "native", compress: str = "none",
-                 transport: str = "c10d", rebuild_buckets: bool = True, timeline: bool | None = None,
+                 transport: str = "auto", rebuild_buckets: bool = True, timeline: bool | None = None,
                  last_bucket_mb: float | None = 2.0):
         super().__init__()
         self.last_bucket_mb = last_bucket_mb
@@ -108,7 +181,7 @@ class DataParallel(nn.Module):
         self.check_collectives = check_collectives
         self.bucket_mb, self.first_bucket_mb = bucket_mb, first_bucket_mb
         if reducer not in ("native", "python") or compress not in ("none", "bf16") \
-                or transport not in ("c10d", "rccl"):
+                or transport not in ("auto", "c10d", "rccl"):
             raise ValueError(f"bad reducer/compress/transport: {reducer!r}/{compress!r}/{transport!r}")
         if comm is not None:
             desc = ";".join(f"{n}:{tuple(p.shape)}" for n, p in module.named_parameters())
@@ -116,12 +189,10 @@ class DataParallel(nn.Module):
         self.flat = flatten_module(module)
         self._build_buckets()
         self.rccl = None
-        if comm is not None and transport == "rccl":
-            if reducer != "native" or comm.backend != "nccl":
-                raise ValueError("transport='rccl' needs the native reducer and GPU ranks")
-            _check_single_in_step_communicator(comm)
-            from . import rccl
-            self.rccl = rccl.create(comm.group)
+        transport, self.rccl = resolve_transport(comm, module, reducer, transport)
+        if self.rccl is not None:
+            comm.attach_native(self.rccl)          # per-step ncclCommGetAsyncError check
+            comm.in_step_c10d_forbidden = True     # SyncBN may never fall back to c10d now
         if comm is not None:
             self._sync_module_states()
         self._sync_enabled = True
@@ -377,3 +448,5 @@ class DataParallel(nn.Module):
         """Abort the native communicator (peers blocked in a collective error out)."""
         if self.rccl is not None:
             self.rccl.abort()
+            if self.comm is not None:
+                self.comm.in_step_c10d_forbidden = False

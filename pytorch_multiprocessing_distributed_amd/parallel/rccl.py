@@ -81,3 +81,37 @@ def create_single(device: int | None = None, priority: int = 0):
     from ..ops.native import C
     dev = torch.cuda.current_device() if device is None else device
     return register(C.RcclComm(bytes(C.RcclComm.unique_id()), 0, 1, dev, priority))
+
+
+def self_test(c, group=None, n: int = 4097, rounds: int = 2) -> bool:
+    """Collective over ``group`` (every rank calls it; host-syncing, run once at
+    setup, like ``XgmiAllReduce.self_test``): exact check of the native
+    communicator on rank-dependent integers -- SUM all-reduce, AVG all-reduce
+    (the reducer's op) and a broadcast from rank 0 -- plus its asynchronous error
+    state.  The verdict is agreed on by all ranks (MIN over the process group),
+    so every rank takes the same transport decision."""
+    dev = torch.device("cuda", c.device)
+    W, r0 = c.world, c.rank
+    ok = True
+    try:
+        i = torch.arange(n, device=dev, dtype=torch.float32)
+        for r in range(rounds):
+            s = i + 1000.0 * r0 + r
+            c.all_reduce_(s, 0)
+            a = i * (r0 + 1)
+            c.all_reduce_(a, 1)
+            b = torch.full((n,), float(7 * r0 + 3 + r), device=dev)
+            c.broadcast_(b, 0)
+            torch.cuda.synchronize(dev)
+            want_s = i * W + 1000.0 * (W * (W - 1) / 2) + r * W
+            want_a = i * ((W + 1) / 2.0)
+            ok = (ok and bool(torch.equal(s, want_s))
+                  and bool(torch.allclose(a, want_a, rtol=1e-6, atol=0.0))
+                  and bool(torch.all(b == float(3 + r)).item()) and bool(c.check()))
+    except Exception:  # noqa: BLE001 -- a failing communicator is a failed test, agreed below
+        ok = False
+    if dist.is_initialized():
+        flag = torch.tensor([1 if ok else 0], device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+        ok = bool(flag.item() == 1)
+    return ok

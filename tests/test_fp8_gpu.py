@@ -88,6 +88,10 @@ def test_conv_fp8_fwd(shape):
     yr = F.conv2d(xd, wd, stride=st, padding=pad).permute(0, 2, 3, 1)
     err = (y.float() - yr).abs().max() / yr.abs().max()
     assert err < 1e-2, err
+    # relative L2 at the bf16 output-rounding floor (same oracle contract as the bf16 convs,
+    # tests/test_kernels_gpu.py CONV_REL_L2)
+    rel2 = (y.float() - yr).norm() / yr.norm()
+    assert rel2 < 5e-3, rel2
     s = stats.sum(0)
     yb = y.float().reshape(-1, K)
     torch.testing.assert_close(s[0], yb.sum(0), rtol=1e-3, atol=1e-2)
@@ -176,6 +180,16 @@ def test_conv_dgrad_fp8(shape):
     ref = torch.nn.grad.conv2d_input((N, Cin, H, H), wd, dyd, stride=st, padding=pad).permute(0, 2, 3, 1)
     err = (dx.double() - ref).abs().max() / ref.abs().max()
     assert err < 1e-2, err
+    rel2 = (dx.double() - ref).norm() / ref.norm()
+    assert rel2 < 5e-3, rel2
+    # a weight image with one input channel zeroed must fail that bound (negative control
+    # of the oracle at the smallest reduction under test as well as the largest)
+    if Cin >= 256:
+        wbad = w.clone()
+        wbad[:, 7] = 0.0
+        _, wtq_bad = C.quant_weight_fp8_t(wbad, Cin, sw, None)
+        dxb = HP.conv_dgrad_fp8(dyq, sdy, wtq_bad, sw, (N, H, H, Cin), st, pad)
+        assert (dxb.double() - ref).norm() / ref.norm() > 5e-3
     # fused epilogue: addend + BN-backward reduce over one BN input
     add = torch.randn(N, H, H, Cin, device=DEV).to(torch.bfloat16)
     yb = torch.randn(N, H, H, Cin, device=DEV).to(torch.bfloat16)
@@ -192,8 +206,8 @@ def test_conv_dgrad_fp8(shape):
 
 
 def test_resnet50_fp8_trains():
-    """Config 5 path: ResNet-50 with fp8 block-conv forwards (e4m3, delayed
-    scaling) converges on a fixed batch like the bf16 model, and its first-step
+    """Config 5 path: ResNet-50 with every block conv in fp8 (e4m3 forwards, e5m2 x e4m3
+    data and weight gradients, delayed scaling) converges on a fixed batch like the bf16 model, and its first-step
     loss matches bf16 to quantisation accuracy."""
     from pytorch_multiprocessing_distributed_amd.engine.optim import FusedSGD
     from pytorch_multiprocessing_distributed_amd.models import ResNet50
@@ -223,12 +237,19 @@ def test_resnet50_fp8_trains():
         assert all(v == v for v in losses), losses
         assert losses[-1] < 0.1 * losses[0], (mode, losses)
         if f8 is not None:
-            # a weight site per fp8-eligible conv (default policy: the 16 3x3 convs of
-            # ResNet-50) plus the activation sites of their inputs
+            # a weight site per fp8-eligible conv (default policy "all" with the fp8
+            # gradients and PMD_FP8_MIN_KG=0: every one of ResNet-50's 52 block convs --
+            # 16 blocks x 3 + 4 projection shortcuts; the stem stays bf16) plus the
+            # activation sites of their inputs
             n_elig = sum(1 for mod in m.modules() if getattr(mod, "weight", None) is not None
                          and mod.weight.dim() == 4 and mod is not m.conv1
                          and OF.fp8_eligible(mod, mod.weight.shape[1]))
-            assert n_elig >= 16 and len(f8.sites) > n_elig, (n_elig, len(f8.sites))
+            if OF.FP8_CONVS == "all" and OF.FP8_MIN_KG == 0:
+                assert n_elig == 52, n_elig
+            assert len(f8.sites) > n_elig, (n_elig, len(f8.sites))
+            if OF.FP8_WGRAD:
+                # the e5m2 dY sites of the fp8 weight / data gradients: the gradient path ran
+                assert f8.grads is not None and len(f8.grads.sites) > 0
             assert f8.steps == 24                              # first update() precedes any site
             n = len(f8.sites)
             assert torch.isfinite(f8.scale[:n]).all() and (f8.scale[:n] > 0).all()

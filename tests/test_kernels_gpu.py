@@ -50,6 +50,18 @@ def _close_norm(a, b, rel):
     assert err < rel, f"relative L2 err {err.item():.3e} >= {rel}"
 
 
+# Conv fwd / dgrad oracle: both sides are the same fp32 sums rounded to bf16, so the
+# relative L2 error floor is ~1e-3; 5e-3 is tight enough that a kernel dropping ONE input
+# channel of a 512-channel reduction (~1/sqrt(512) = 4.4% of the output energy) fails
+# (tests below: test_conv_oracle_rejects_dropped_channel).
+CONV_REL_L2 = 5e-3
+
+
+def _close_conv(a, b, rel_max=2e-2):
+    _close(a, b, rel_max)
+    _close_norm(a, b, CONV_REL_L2)
+
+
 def _batch_for(h):
     return 2 if h >= 112 else (4 if h >= 28 else 8)
 
@@ -70,12 +82,12 @@ def test_conv_fwd_dgrad_wgrad(shape):
     assert torch.equal(wp[1], wref[0].permute(3, 1, 2, 0).contiguous())
     y, st_ = HP.conv_fwd(x, wp, st, pad, True)
     yr, sr = TP.conv_fwd(x, wref, st, pad, True)
-    _close(y, yr, 2e-2)
+    _close_conv(y, yr)
     _close(HP.stats_collapse(st_).view(2, -1), sr, 2e-2)
     dy = torch.randn_like(y)
     dx = HP.conv_dgrad(dy, wp, tuple(x.shape), st, pad)
     dxr = TP.conv_dgrad(dy, wref, tuple(x.shape), st, pad)
-    _close(dx, dxr, 2e-2)
+    _close_conv(dx, dxr)
     dw = HP.conv_wgrad(dy, x, tuple(wp[0].shape), st, pad)
     dwr = TP.conv_wgrad(dy, x, tuple(wref[0].shape), st, pad)
     _close(dw, dwr, 2e-3)
@@ -186,9 +198,9 @@ def test_conv_pipeline_variants(shape, impl):
         torch.cuda.synchronize()
     finally:
         _C.conv_set_impl(5)
-    _close(y, yr, 2e-2)
+    _close_conv(y, yr)
     _close(HP.stats_collapse(st_).view(2, -1), sr, 2e-2)
-    _close(dx, dxr, 2e-2)
+    _close_conv(dx, dxr)
 
 
 @pytest.mark.parametrize("tile,pipe", [(2, 0), (2, 1), (2, 2), (2, 3), (3, 0), (3, 2), (3, 3), (4, 0), (5, 0),
@@ -222,9 +234,66 @@ def test_conv_big_tiles(shape, tile, pipe):
     finally:
         _C.conv_set_tile(0)
         _C.conv_set_big_pipe(0)
-    _close(y, yr, 2e-2)
+    _close_conv(y, yr)
     _close(HP.stats_collapse(st_).view(2, -1), sr, 2e-2)
-    _close(dx, dxr, 2e-2)
+    _close_conv(dx, dxr)
+
+
+# every forced kernel variant of the fwd/dgrad tests above: ("impl", conv_set_impl) or
+# ("tile", conv_set_tile, big_pipe)
+_VARIANTS = ([("impl", i, 0) for i in (0, 1, 3, 4, 6, 7)]
+             + [("tile", t, p) for (t, p) in ((2, 0), (2, 1), (2, 2), (2, 3), (3, 0), (3, 2), (3, 3), (4, 0),
+                                              (5, 0), (6, 0), (7, 0), (8, 0), (9, 0), (10, 0), (11, 0),
+                                              (12, 0))])
+
+
+@pytest.mark.parametrize("variant", _VARIANTS, ids=lambda v: "%s%d_%d" % v)
+@pytest.mark.parametrize("shape", [(512, 14, 512, 3, 2), (512, 28, 128, 1, 1), (512, 7, 512, 3, 1)],
+                         ids=lambda s: "C%d_H%d_K%d_R%d_s%d" % s)
+def test_conv_oracle_rejects_dropped_channel(shape, variant):
+    """Negative control of the conv oracle: the same kernel variant run with ONE input
+    channel of a 512-channel reduction zeroed in its weight image must FAIL the check the
+    positive tests use, in both passes (fwd drops input channel c; dgrad drops output
+    channel c of dX), while the intact weights pass it."""
+    from pytorch_multiprocessing_distributed_amd.ops.native import C as _C
+    HP = _hp()
+    torch.manual_seed(9)
+    C, H, K, R, st = shape
+    pad = R // 2
+    N = _batch_for(H)
+    x = torch.randn(N, H, H, C, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(K, C, R, R, device=DEV) / (C * R * R) ** 0.5).contiguous(
+        memory_format=torch.channels_last)
+    wref = TP.conv_weight(w, torch.bfloat16, C)
+    yr, _ = TP.conv_fwd(x, wref, st, pad, False)
+    dy = torch.randn_like(yr)
+    dxr = TP.conv_dgrad(dy, wref, tuple(x.shape), st, pad)
+    wbad = w.clone()
+    wbad[:, 137] = 0.0
+    kind, v, pipe = variant
+    if kind == "impl":
+        _C.conv_set_impl(v)
+    else:
+        _C.conv_set_tile(v)
+        _C.conv_set_big_pipe(pipe)
+    try:
+        outs = {}
+        for name, ww in (("good", w), ("bad", wbad)):
+            wp = HP.conv_weight(ww, torch.bfloat16, C, True)
+            y, _ = HP.conv_fwd(x, wp, st, pad, False)
+            dx = HP.conv_dgrad(dy, wp, tuple(x.shape), st, pad)
+            outs[name] = (y, dx)
+        torch.cuda.synchronize()
+    finally:
+        _C.conv_set_impl(5)
+        _C.conv_set_tile(0)
+        _C.conv_set_big_pipe(0)
+    _close_conv(outs["good"][0], yr)
+    _close_conv(outs["good"][1], dxr)
+    with pytest.raises(AssertionError):
+        _close_conv(outs["bad"][0], yr)
+    with pytest.raises(AssertionError):
+        _close_conv(outs["bad"][1], dxr)
 
 
 @pytest.mark.parametrize("train", [True, False])

@@ -198,6 +198,54 @@ def test_native_rccl_comm_single_rank_reducer():
         dist.destroy_process_group()
 
 
+def test_auto_transport_picks_native_rccl_with_selftest_and_error_check():
+    """--comm auto (the default of main.py / bench.py) on a single-rank nccl group
+    with SyncBN on the one-shot xGMI kernel: DataParallel takes the native
+    RcclComm after its exact self-test, attaches it to the per-step health check,
+    trains a step through it, and an aborted communicator makes
+    ``Comm.raise_if_failed`` raise (ncclCommGetAsyncError folded in)."""
+    import datetime
+    import torch.distributed as dist
+    from pytorch_multiprocessing_distributed_amd.engine.optim import FusedSGD
+    from pytorch_multiprocessing_distributed_amd.models import build_model
+    from pytorch_multiprocessing_distributed_amd.ops import functional as OF
+    from pytorch_multiprocessing_distributed_amd.parallel import rccl
+    from pytorch_multiprocessing_distributed_amd.parallel.comm import Comm
+    from pytorch_multiprocessing_distributed_amd.parallel.dp import DataParallel
+    torch.cuda.set_device(0)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, timeout=datetime.timedelta(seconds=60),
+                            device_id=torch.device("cuda", 0))
+    try:
+        comm = Comm()
+        comm.enable_xgmi(timeout_s=20.0)
+        assert comm.xgmi.self_test()
+        OF.set_bn_sync(comm)
+        torch.manual_seed(0)
+        dp = DataParallel(build_model("res").cuda(), comm, bucket_mb=0.5, first_bucket_mb=0.1)
+        assert dp.transport == "rccl" and dp.rccl is not None
+        assert comm.natives == [dp.rccl] and comm.in_step_c10d_forbidden
+        assert rccl.self_test(dp.rccl, comm.group)
+        opt = FusedSGD(dp, lr=0.05)
+        x, y = _data(8, 32)
+        calls0 = dp.rccl.calls
+        for _ in range(2):
+            loss = OF.cross_entropy(dp(x), y)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            comm.raise_if_failed()
+        torch.cuda.synchronize()
+        assert bool(torch.isfinite(loss).item()) and dp.rccl.calls > calls0
+        dp.shutdown()                       # ncclCommAbort
+        with pytest.raises(RuntimeError, match="native RCCL communicator failed"):
+            comm.raise_if_failed()
+    finally:
+        OF.set_bn_sync(None)
+        dist.destroy_process_group()
+
+
 # ---------------------------------------------------------- straggler -> raise
 def _straggler_worker(rank, world, port, out):
     os.environ["MASTER_ADDR"] = "127.0.0.1"

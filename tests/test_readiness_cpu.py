@@ -61,10 +61,121 @@ def test_run_rank_failure_aborts_native_comm(monkeypatch):
 
 
 def test_comm_flag():
-    assert config.parse_args([]).comm == "c10d"
+    assert config.parse_args([]).comm == "auto"
     assert config.parse_args(["--comm", "rccl"]).comm == "rccl"
+    assert config.parse_args(["--comm", "c10d"]).comm == "c10d"
     with pytest.raises(SystemExit):
         config.parse_args(["--comm", "mpi"])
+
+
+class _SelComm:
+    """Enough of parallel.comm.Comm for resolve_transport."""
+    def __init__(self, backend="nccl"):
+        self.backend, self.rank, self.world_size, self.group = backend, 0, 8, None
+
+
+class _Native:
+    def __init__(self):
+        self.aborted = 0
+
+    def abort(self):
+        self.aborted += 1
+
+
+class _Xgmi:
+    def __init__(self, capacity):
+        self.capacity = capacity
+
+
+@pytest.fixture
+def bn_sync_guard():
+    from pytorch_multiprocessing_distributed_amd.ops import functional as OF
+    prev = OF.get_bn_sync()
+    yield OF
+    OF.set_bn_sync(prev)
+
+
+def test_auto_transport_selection(monkeypatch, bn_sync_guard, capsys):
+    """--comm auto: rccl exactly when the native communicator can be the only
+    in-step communicator AND its self-test passes on every rank; c10d otherwise,
+    with the reason printed.  Explicit rccl raises where auto falls back."""
+    from pytorch_multiprocessing_distributed_amd.models import build_model
+    from pytorch_multiprocessing_distributed_amd.parallel import dp as DP
+    OF = bn_sync_guard
+    m = build_model("resnet50", num_classes=10, stem="imagenet")
+    made = []
+
+    def create(group=None, priority=0, store=None):
+        c = _Native()
+        made.append(c)
+        return c
+    result = {"ok": True}
+    monkeypatch.setattr(rccl, "create", create)
+    monkeypatch.setattr(rccl, "self_test", lambda c, group=None: result["ok"])
+
+    class Sync:
+        xgmi = _Xgmi(32768)
+    # SyncBN on the xGMI kernel, self-test passes -> rccl
+    OF.set_bn_sync(Sync())
+    t, c = DP.resolve_transport(_SelComm(), m, "native", "auto")
+    assert t == "rccl" and c is made[-1] and c.aborted == 0
+    assert "rccl" in capsys.readouterr().out
+    # self-test fails -> c10d, the communicator is torn down
+    result["ok"] = False
+    t, c = DP.resolve_transport(_SelComm(), m, "native", "auto")
+    assert t == "c10d" and c is None and made[-1].aborted == 1
+    assert "self-test failed" in capsys.readouterr().out
+    with pytest.raises(RuntimeError, match="self-test"):
+        DP.resolve_transport(_SelComm(), m, "native", "rccl")
+    result["ok"] = True
+    # SyncBN over the process group -> c10d (two communicators in the step)
+    OF.set_bn_sync(type("S", (), {"xgmi": None})())
+    n = len(made)
+    assert DP.resolve_transport(_SelComm(), m, "native", "auto") == ("c10d", None)
+    assert len(made) == n                      # no communicator was even created
+    with pytest.raises(ValueError, match="two communicators"):
+        DP.resolve_transport(_SelComm(), m, "native", "rccl")
+    # a statistics message that does not fit the xGMI kernel (R50: 4*2048+1 floats)
+    class Small:
+        xgmi = _Xgmi(4096)
+    OF.set_bn_sync(Small())
+    assert DP.resolve_transport(_SelComm(), m, "native", "auto")[0] == "c10d"
+    assert "capacity" in capsys.readouterr().out
+    # SyncBN off, python reducer, gloo, no comm, explicit c10d
+    OF.set_bn_sync(None)
+    assert DP.resolve_transport(_SelComm(), m, "native", "auto")[0] == "rccl"
+    assert DP.resolve_transport(_SelComm(), m, "python", "auto")[0] == "c10d"
+    assert DP.resolve_transport(_SelComm("gloo"), m, "native", "auto") == ("c10d", None)
+    assert DP.resolve_transport(None, m, "native", "auto") == ("c10d", None)
+    assert DP.resolve_transport(_SelComm(), m, "native", "c10d") == ("c10d", None)
+
+
+def test_native_comm_errors_raise_every_step_and_no_c10d_fallback():
+    """Comm.raise_if_failed folds in ncclCommGetAsyncError of the attached native
+    communicators; with the native transport a SyncBN message the xGMI kernel
+    cannot take raises instead of falling back to a c10d collective."""
+    from pytorch_multiprocessing_distributed_amd.parallel.comm import Comm
+
+    class C:
+        def __init__(self):
+            self.ok = True
+
+        def check(self):
+            return self.ok
+    comm = Comm.__new__(Comm)
+    comm.xgmi, comm.rank, comm.natives, comm.in_step_c10d_forbidden = None, 0, [], False
+    nat = C()
+    comm.attach_native(nat)
+    comm.attach_native(nat)
+    assert comm.natives == [nat]
+    comm.raise_if_failed()
+    nat.ok = False
+    with pytest.raises(RuntimeError, match="native RCCL communicator failed"):
+        comm.raise_if_failed()
+    comm.in_step_c10d_forbidden = True
+    comm._seq = comm._ncoll = 0
+    with pytest.raises(RuntimeError, match="two communicators"):
+        comm.all_reduce_stats_(torch.zeros(8))
 
 
 def test_rccl_transport_needs_single_in_step_communicator():
@@ -79,7 +190,7 @@ def test_rccl_transport_needs_single_in_step_communicator():
         with pytest.raises(ValueError, match="two communicators"):
             _check_single_in_step_communicator(Sync())
         s = Sync()
-        s.xgmi = object()                    # one-shot xGMI exchange: allowed
+        s.xgmi = _Xgmi(32768)                # one-shot xGMI exchange: allowed
         OF.set_bn_sync(s)
         _check_single_in_step_communicator(s)
         OF.set_bn_sync(None)                 # --sync_bn off: allowed
