@@ -370,6 +370,19 @@ Tensor conv_dgrad_fp8(Tensor dyq, Tensor wtq, Tensor sdy, Tensor sw, int64_t H, 
   return dx;
 }
 
+// split-K workspaces of the reductions queued in deferred mode (pmd::wgrad_set_defer): kept
+// alive until wgrad_flush has launched the grouped reduction that reads them (stream-ordered
+// on the same stream, so the caching allocator may recycle them right after)
+static thread_local std::vector<Tensor> t_ws_keep;
+static void keep_ws(const Tensor& ws) {
+  if (pmd::wgrad_defer() && ws.defined()) t_ws_keep.push_back(ws);
+}
+void wgrad_flush() {
+  const int rc = pmd::wgrad_flush(cur_stream());
+  TORCH_CHECK(rc == 0, "wgrad_flush: the queued split reductions belong to another stream");
+  t_ws_keep.clear();
+}
+
 // out: optional [K,R,S,C] fp32 accumulation target (e.g. a grad-arena view); dW is ADDED to it
 Tensor conv_wgrad(Tensor dy, Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad,
                   c10::optional<Tensor> out) {
@@ -398,6 +411,7 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int64_t R, int64_t S, int64_t stride, int
                                         splits > 1 ? ws.data_ptr<float>() : nullptr, N, H, W, C, P, Q,
                                         K, (int)R, (int)S, (int)stride, (int)pad, cur_stream());
   CHECK_RC(rc, "conv_wgrad");
+  keep_ws(ws);
   return dw;
 }
 
@@ -431,6 +445,7 @@ Tensor conv_wgrad_fp8(Tensor dyq, Tensor xq, Tensor sdy, Tensor sx, int64_t R, i
                                       splits > 1 ? ws.data_ptr<float>() : nullptr, N, H, W, C, P, Q, K, (int)R,
                                       (int)S, (int)stride, (int)pad, cur_stream()),
            "conv_wgrad_fp8");
+  keep_ws(ws);
   return dw;
 }
 
@@ -984,6 +999,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 (MI355X) kernels for pytorch_multiprocessing_distributed_amd";
   pmd::register_runtime(m);
   m.def("conv_weight_prep", &conv_weight_prep);
+  m.def("wgrad_set_defer", &pmd::wgrad_set_defer,
+        "queue the split-K reductions of the following weight gradients (this thread)");
+  m.def("wgrad_pending", &pmd::wgrad_pending);
+  m.def("wgrad_flush", &wgrad_flush, "launch the queued split-K reductions as one grouped kernel");
+  m.def("conv1x1_set_policy", &pmd::conv1x1_set_policy,
+        "streaming 1x1 conv: 0 off, 1 data gradients, 2 data gradients + forwards");
+  m.def("conv1x1_policy", &pmd::conv1x1_policy);
+  m.def("conv1x1_launches", &pmd::conv1x1_launches);
+  m.def("conv1x1_set_bn", &pmd::conv1x1_set_bn, "streaming 1x1 conv column tile: 64 / 128, 0 = auto");
   m.def("conv_set_impl", &pmd::conv_set_impl, "conv staging/pipeline variant 0-4, 5 = per-shape default");
   m.def("conv_set_tile", &pmd::conv_set_tile,
         "conv fwd/dgrad tile policy: 0 auto, 1 128-row only, 2 256x128, 3 256x256 where legal");

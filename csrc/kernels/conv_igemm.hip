@@ -1632,6 +1632,21 @@ static int conv_igemm_launch_b(const bf16_t* src, const bf16_t* wt, bf16_t* out,
   a.Kg = R * S * Cs;
   a.f8_sa = nullptr;
   a.f8_sb = nullptr;
+  // short-reduction 1x1 stride-1 convolutions: the persistent streaming kernel
+  // (kernels/conv1x1_stream.hip) when the policy selects it for this pass
+  const int s1p = conv1x1_policy();
+  if (R == 1 && S == 1 && stride == 1 && pad == 0 && batch == 1 && (dgrad ? s1p >= 1 : s1p >= 2)) {
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+    }
+    if (conv1x1_stream_launch(src, wt, out, a.M, Cs, Nout, dgrad, stats, stats ? shift : nullptr, addend,
+                              a.addend_mask, bnr, st, cus) == 0)
+      return 0;
+  }
   if (dgrad) {
     if (stats) launch_sel<true, true>(a, st);
     else launch_sel<true, false>(a, st);

@@ -814,41 +814,6 @@ static bool halo_cfg(const WgradArgs& a, HaloArgs* h, int* nich) {
 
 static int halo_splits(const HaloArgs& h) { return (h.bands + h.bpb - 1) / h.bpb; }
 
-// dW[i] += sum_s ws[s][i], in a fixed order (bitwise reproducible).  blockIdx.y = split
-// group of <= kSplitGroup slices: with one group the block adds straight into dW; with
-// several (tiny outputs with hundreds of splits) a group stage (to_ws = 1) leaves each
-// group's sum in its first slice, and a second launch (sst = kSplitGroup) adds those
-// group sums into dW in group order.  (The round-2 version combined the groups with fp32
-// atomics, whose order -- hence the last bits of the l1 weight gradients -- varied run to run.)
-constexpr int kSplitGroup = 32;
-__global__ void wgrad_reduce_kernel(float* __restrict__ ws, float* __restrict__ dw, int splits,
-                                    long long n4, int sst, int to_ws) {
-  const int s0 = blockIdx.y * kSplitGroup;
-  const int s1 = s0 + kSplitGroup < splits ? s0 + kSplitGroup : splits;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
-       i += (long long)gridDim.x * blockDim.x) {
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll 4
-    for (int s = s0; s < s1; ++s) {
-      const float4 v = ld16fn<NT_WS_LD>(reinterpret_cast<const float4*>(ws) + ((long long)s * sst * n4 + i));
-      acc.x += v.x;
-      acc.y += v.y;
-      acc.z += v.z;
-      acc.w += v.w;
-    }
-    if (to_ws) {
-      reinterpret_cast<float4*>(ws)[(long long)s0 * n4 + i] = acc;  // this thread read it first
-    } else {
-      float4 d = reinterpret_cast<float4*>(dw)[i];
-      d.x += acc.x;
-      d.y += acc.y;
-      d.z += acc.z;
-      d.w += acc.w;
-      reinterpret_cast<float4*>(dw)[i] = d;
-    }
-  }
-}
-
 static int ilog2w(int v) {
   int l = 0;
   while ((1 << l) < v) ++l;
@@ -1039,18 +1004,132 @@ static void wgrad_run(int impl, WgradArgs a, float* ws, hipStream_t st) {
   if (splits > 1) wgrad_reduce_launch(a, splits, st);
 }
 
-static void wgrad_reduce_launch(const WgradArgs& a, int splits, hipStream_t st) {
-  const long long n4 = (long long)a.K * a.Kg / 4;
-  const int groups = (splits + kSplitGroup - 1) / kSplitGroup;
-  long long b = (n4 + 255) / 256;
-  if (b > 4096) b = 4096;
-  if (groups == 1) {
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)b, 1), dim3(256), 0, st, a.ws, a.dw, splits, n4, 1, 0);
-  } else {
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)b, groups), dim3(256), 0, st, a.ws, a.dw, splits, n4, 1, 1);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)b, 1), dim3(256), 0, st, a.ws, a.dw, groups, n4,
-                       kSplitGroup, 0);
+// ---- split-K reduction, grouped: ONE launch adds the partial slices of up to 16 weight
+// gradients into their dW (a block backward's 3-4 convs when deferred, see wgrad_set_defer).
+// Block b of descriptor d owns EB = 256 / G float4 elements; its G thread groups each sum the
+// slices s = grp, grp + G, ... in increasing order, and the group partials are combined in
+// group order through LDS: a fixed summation order, so the result is bitwise reproducible
+// run to run (no fp32 atomics), in a single pass even for tiny outputs with hundreds of
+// slices (the layer-1 1x1 gradients: 64 x 64 outputs, ~200 slices).
+struct WsDesc {
+  const float* ws;
+  float* dw;
+  long long n4;
+  int splits, G, blocks;
+};
+constexpr int kWsGroupMax = 16;
+struct WsGroup {
+  WsDesc d[kWsGroupMax];
+  int start[kWsGroupMax + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void wgrad_reduce_grouped_kernel(WsGroup g) {
+  __shared__ float4 part[256];
+  int e = 0;
+  while (e + 1 < g.n && g.start[e + 1] <= (int)blockIdx.x) ++e;
+  const WsDesc d = g.d[e];
+  const int lb = blockIdx.x - g.start[e];
+  const int EB = 256 / d.G;
+  const int t = threadIdx.x, el = t % EB, grp = t / EB;
+  const float4* ws = reinterpret_cast<const float4*>(d.ws);
+  for (long long base = (long long)lb * EB; base < d.n4; base += (long long)d.blocks * EB) {
+    const long long i = base + el;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < d.n4) {
+#pragma unroll 4
+      for (int s = grp; s < d.splits; s += d.G) {
+        const float4 v = ld16fn<NT_WS_LD>(ws + (long long)s * d.n4 + i);
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
+      }
+    }
+    part[t] = acc;
+    __syncthreads();
+    if (grp == 0 && i < d.n4) {
+      float4 tot = part[el];
+      for (int q = 1; q < d.G; ++q) {
+        const float4 v = part[q * EB + el];
+        tot.x += v.x;
+        tot.y += v.y;
+        tot.z += v.z;
+        tot.w += v.w;
+      }
+      float4 o = reinterpret_cast<float4*>(d.dw)[i];
+      o.x += tot.x;
+      o.y += tot.y;
+      o.z += tot.z;
+      o.w += tot.w;
+      reinterpret_cast<float4*>(d.dw)[i] = o;
+    }
+    __syncthreads();
   }
+}
+
+static WsDesc ws_desc(const float* ws, float* dw, long long n4, int splits) {
+  WsDesc d;
+  d.ws = ws;
+  d.dw = dw;
+  d.n4 = n4;
+  d.splits = splits;
+  d.G = splits >= 64 ? 8 : (splits >= 16 ? 4 : (splits >= 4 ? 2 : 1));
+  const int EB = 256 / d.G;
+  long long b = (n4 + EB - 1) / EB;
+  d.blocks = (int)(b > 2048 ? 2048 : b);
+  return d;
+}
+
+static void ws_group_launch(const std::vector<WsDesc>& v, hipStream_t st) {
+  for (size_t i0 = 0; i0 < v.size(); i0 += kWsGroupMax) {
+    WsGroup g{};
+    g.n = 0;
+    int tot = 0;
+    for (size_t i = i0; i < v.size() && g.n < kWsGroupMax; ++i) {
+      g.d[g.n] = v[i];
+      g.start[g.n] = tot;
+      tot += v[i].blocks;
+      ++g.n;
+    }
+    g.start[g.n] = tot;
+    hipLaunchKernelGGL(wgrad_reduce_grouped_kernel, dim3(tot), dim3(256), 0, st, g);
+  }
+}
+
+// Deferred mode (per thread, set around the weight gradients of one block backward on the
+// side stream): the split reductions are queued and launched by wgrad_flush as ONE grouped
+// launch, instead of one (or two) launches per weight gradient.
+static thread_local bool t_ws_defer = false;
+static thread_local std::vector<WsDesc> t_ws_pending;
+static thread_local hipStream_t t_ws_stream = nullptr;
+void wgrad_set_defer(bool on) { t_ws_defer = on; }
+bool wgrad_defer() { return t_ws_defer; }
+int wgrad_pending() { return (int)t_ws_pending.size(); }
+int wgrad_flush(hipStream_t st) {
+  if (t_ws_pending.empty()) return 0;
+  if (st != t_ws_stream) return 1;  // must run on the stream that wrote the partial slices
+  ws_group_launch(t_ws_pending, st);
+  t_ws_pending.clear();
+  return 0;
+}
+
+static void ws_reduce(const float* ws, float* dw, long long n4, int splits, hipStream_t st) {
+  const WsDesc d = ws_desc(ws, dw, n4, splits);
+  if (t_ws_defer) {
+    if (!t_ws_pending.empty() && t_ws_stream != st) {
+      ws_group_launch(t_ws_pending, t_ws_stream);  // never mix streams in one group
+      t_ws_pending.clear();
+    }
+    t_ws_stream = st;
+    t_ws_pending.push_back(d);
+    return;
+  }
+  ws_group_launch(std::vector<WsDesc>{d}, st);
+}
+
+static void wgrad_reduce_launch(const WgradArgs& a, int splits, hipStream_t st) {
+  ws_reduce(a.ws, a.dw, (long long)a.K * a.Kg / 4, splits, st);
 }
 
 // FP8 wgrad split plan: 128-row chunks, the bf16 kernels' block targets, workspace <= 96 MiB
@@ -1121,6 +1200,11 @@ int conv_wgrad_fp8_launch(const uint8_t* dyq, const uint8_t* xq, const float* sd
 
 static int wgrad_tune(const WgradArgs& a0, float* ws, hipStream_t st) {
   WgradArgs a = a0;
+  struct NoDefer {  // the timed candidates include their own (immediate) reduction
+    bool prev = t_ws_defer;
+    NoDefer() { t_ws_defer = false; }
+    ~NoDefer() { t_ws_defer = prev; }
+  } nodefer;
   static float* scratch = nullptr;
   static size_t scratch_n = 0;
   const size_t need = (size_t)a.K * a.Kg;

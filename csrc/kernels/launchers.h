@@ -31,6 +31,15 @@ int winograd_filter_launch(const bf16_t* wk, bf16_t* U, int K, int Cp, bool flip
 int winograd_input_launch(const bf16_t* x, bf16_t* V, int N, int H, int W, int C, hipStream_t st);
 int winograd_output_launch(const bf16_t* M, bf16_t* y, float* stats, int N, int H, int W, int K,
                            hipStream_t st, const float* shift = nullptr);
+// Persistent streaming 1x1 (stride 1) conv for short reductions (kernels/conv1x1_stream.hip):
+// policy 0 off, 1 data gradients, 2 data gradients + forwards; bn: force 64 / 128 (0 auto)
+void conv1x1_set_policy(int p);
+int conv1x1_policy();
+void conv1x1_set_bn(int bn);
+long long conv1x1_launches();
+int conv1x1_stream_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, int M, int KR, int Nout, bool dgrad,
+                          float* stats, const float* shift, const bf16_t* addend, const uint8_t* addend_mask,
+                          const BnReduceArgs* bnr, hipStream_t st, int cus);
 void conv_set_impl(int impl);
 void conv_wgrad_set_impl(int impl);
 void conv_set_tile(int t);
@@ -62,6 +71,12 @@ int conv_wgrad_splits(int N, int H, int W, int C, int P, int Q, int K, int R, in
 // dw += dW (dw must be initialised: zeros or an accumulation target)
 int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, float* ws, int N, int H, int W,
                       int C, int P, int Q, int K, int R, int S, int stride, int pad, hipStream_t st);
+// deferred split-K reductions: queue them (per thread) while on, launch them grouped with
+// wgrad_flush on the stream that computed the partial slices (returns nonzero on a mismatch)
+void wgrad_set_defer(bool on);
+bool wgrad_defer();
+int wgrad_pending();
+int wgrad_flush(hipStream_t st);
 // FP8 weight gradient: e5m2 dY x e4m3 X on the scaled 16x16x128 MFMA (kernels/conv_wgrad.hip)
 // FP8 data gradient: e5m2 dY [N,P,Q,K] x e4m3 wkt image [Cp][R][S][K] -> bf16 dX [N,H,W,Cp] with the
 // bf16 dgrad's epilogue (addend (+mask), fused BN-backward reduce) (kernels/conv_igemm.hip)

@@ -310,6 +310,9 @@ def _wgrad(P, dy, x, wpack, stride, pad, w, xq=None):
     return dwk.permute(0, 3, 1, 2)                                   # [K,C,R,S] channels_last
 
 
+# the split-K reductions of one block's side-stream weight gradients as ONE grouped launch
+# (kernels/conv_wgrad.hip wgrad_flush) instead of one per weight gradient; PMD_WS_GROUP=0: per wgrad
+_WS_GROUP = os.environ.get("PMD_WS_GROUP", "1") != "0"
 _WGRAD_STREAM = {"on": os.environ.get("PMD_WGRAD_STREAM", "1") != "0", "streams": {},
                  "defer": int(os.environ.get("PMD_WGRAD_DEFER", "1") or 0)}  # join lag in blocks
 # dgrad weight images refreshed on the side stream during the forward: PMD_SPLIT_WPREP=1
@@ -353,7 +356,10 @@ class _WgradSide:
     def __init__(self, t):
         self.on = _WGRAD_STREAM["on"] and t.is_cuda and not _state["force_torch"]
         self.ready = []
+        self.deferred = False
         if self.on:
+            from .native import C
+            self.C = C
             dev = t.device
             self.side = _wgrad_stream(dev)
             self.main = torch.cuda.current_stream(dev)
@@ -365,7 +371,15 @@ class _WgradSide:
         self.side.wait_stream(self.main)
         with torch.cuda.stream(self.side):
             tgt = _grad_target(w)
-            _conv_wgrad_any(P, dy, x, xq, tuple(wpack[0].shape), stride, pad, out=tgt.permute(0, 2, 3, 1))
+            if _WS_GROUP:
+                # split-K reductions queued; join() launches them as ONE grouped kernel
+                self.C.wgrad_set_defer(True)
+                self.deferred = True
+            try:
+                _conv_wgrad_any(P, dy, x, xq, tuple(wpack[0].shape), stride, pad, out=tgt.permute(0, 2, 3, 1))
+            finally:
+                if _WS_GROUP:
+                    self.C.wgrad_set_defer(False)
         dy.record_stream(self.side)
         x.record_stream(self.side)
         dq = getattr(dy, "_pmd_q8", None)
@@ -386,6 +400,10 @@ class _WgradSide:
         bucket is force-launched)."""
         if not (self.on and self.ready):
             return
+        if self.deferred:
+            with torch.cuda.stream(self.side):
+                self.C.wgrad_flush()        # the block's split reductions: one launch
+            self.deferred = False
         if not _WGRAD_STREAM["defer"]:
             self.main.wait_stream(self.side)
             for w in self.ready:
