@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--classes", type=int, default=1000)
+    ap.add_argument("--stem", default="imagenet", choices=["imagenet", "cifar"],
+                    help="cifar = the reference's 3x3 stem (ResNet-18-ref CIFAR shapes: --model res "
+                         "--image 32 --classes 10)")
     ap.add_argument("--sync_bn", default="on", choices=["on", "off"])
     ap.add_argument("--bucket_mb", type=float, default=25.0)
     ap.add_argument("--first_bucket_mb", type=float, default=1.0)
@@ -131,7 +134,7 @@ def bench_rank(rank, world, a):
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    model = build_model(a.model, num_classes=a.classes, stem="imagenet").to(dev)
+    model = build_model(a.model, num_classes=a.classes, stem=a.stem).to(dev)
     if rehearsal:
         # the W>1 machinery on a single-rank group: get_comm() would return None at W=1
         from pytorch_multiprocessing_distributed_amd.parallel.comm import Comm
@@ -161,7 +164,17 @@ def bench_rank(rank, world, a):
     else:
         tune_source, _ = tuning.load_default()
 
+    # the step on its own high-priority stream with PMD_STREAM_PRIO=1 (ops/functional.py
+    # STREAM_PRIO: every stream of the step in the high-priority hardware-queue pool)
+    step_stream = torch.cuda.Stream(priority=-1) if OF.STREAM_PRIO else None
+
     def step(i):
+        if step_stream is not None:
+            with torch.cuda.stream(step_stream):
+                return _step(i)
+        return _step(i)
+
+    def _step(i):
         x, y = data.batch_at(i)
         out = model(x)
         loss = OF.cross_entropy(out, y)
@@ -209,10 +222,14 @@ def bench_rank(rank, world, a):
         comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    from pytorch_multiprocessing_distributed_amd.utils import trace as _trace
+    sync_debug = _trace.sync_debug_enabled()
     for i in range(a.steps):
         loss = step(a.warmup + i)
         if comm is not None:
             comm.raise_if_failed()          # host-mapped xGMI error word, no device sync
+        if sync_debug:
+            _trace.check_stream_budget(comm, model)
     # host time to ENQUEUE the timed steps (nothing in the loop waits on the device): when
     # it approaches ms_per_step the step is launch-/host-bound, not device-bound
     host_dt = time.perf_counter() - t0

@@ -1007,6 +1007,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "streaming 1x1 conv: 0 off, 1 data gradients, 2 data gradients + forwards");
   m.def("conv1x1_policy", &pmd::conv1x1_policy);
   m.def("conv1x1_launches", &pmd::conv1x1_launches);
+  m.def("conv1x1_stream_bn", &pmd::conv1x1_stream_bn,
+        "column tile the streaming 1x1 conv picks for (reduction, out channels, epilogue tensors, masks); 0 = ineligible");
   m.def("conv1x1_set_bn", &pmd::conv1x1_set_bn, "streaming 1x1 conv column tile: 64 / 128, 0 = auto");
   m.def("conv_set_impl", &pmd::conv_set_impl, "conv staging/pipeline variant 0-4, 5 = per-shape default");
   m.def("conv_set_tile", &pmd::conv_set_tile,

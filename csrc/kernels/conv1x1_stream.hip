@@ -164,10 +164,6 @@ __device__ __forceinline__ void dma4(const void* src, void* lds) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds, 4, 0, 0);
 }
-__device__ __forceinline__ void dma2(const void* src, void* lds) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)lds, 2, 0, 0);
-}
 
 // KR: reduction length (= A row length), BN: channels per workgroup column tile,
 // NB: BN-input sets of the fused reduce (dgrad), FWD: forward (statistics epilogue)
@@ -236,10 +232,14 @@ __global__ __launch_bounds__(256, 1) void conv1x1_stream_kernel(Stream1x1Args a)
     e_row[i] = r;
     e_col[i] = n0 + ((ph ^ s1_swz<RE>(r)) << 3);
   }
-  // masks: BN / 8 bytes per row, 16 rows: BN = 128 -> 4-B DMA (lane -> row l/4, dword l%4),
-  //        BN = 64 -> 2-B DMA (lane -> row l/4, half l%4)
-  const int mk_row = lane >> 2;
-  const int mk_col = n0 / 8 + (lane & 3) * (BN / 32);
+  // masks: BN / 8 bytes per row, 16 rows, one 4-B DMA (a 256-B mask slot):
+  //   BN = 128 -> lane -> row l/4, dword l%4;
+  //   BN = 64  -> lanes < 32: row l/2, dword l%2; lanes >= 32 read the zero page into the
+  //               unused upper half (a 1- or 2-B LDS-DMA still advances the LDS address by
+  //               4 B per lane, so it cannot pack 8-B rows)
+  const int mk_row = BN == 128 ? lane >> 2 : (lane & 31) >> 1;
+  const int mk_col = BN == 128 ? n0 / 8 + (lane & 3) * 4 : n0 / 8 + (lane & 1) * 4;
+  const bool mk_lane = BN == 128 || lane < 32;
   const int rowsN8 = a.Nout / 8;
 
   // fused-reduce / statistics state
@@ -310,10 +310,9 @@ __global__ __launch_bounds__(256, 1) void conv1x1_stream_kernel(Stream1x1Args a)
     if (NB > 0) dma_e(a.y[0], eo_y0);
     if (NB > 1) dma_e(a.y[1], eo_y1);
     auto dma_m = [&](const uint8_t* base, int mo) {
-      const bool ok = live && m0 + mk_row < a.M;
+      const bool ok = live && mk_lane && m0 + mk_row < a.M;
       const void* src = ok ? (const void*)(base + (size_t)(m0 + mk_row) * rowsN8 + mk_col) : (const void*)g_s1_zero;
-      if constexpr (BN == 128) dma4(src, st + mo);
-      else dma2(src, st + mo);
+      dma4(src, st + mo);
     };
     if (has_am) dma_m(a.amask, mo_am);
     if (has_bm) dma_m(a.bnmask, mo_bm);
@@ -548,12 +547,51 @@ static void s1_dispatch_nb(const Stream1x1Args& a, int nb, int grid, int lds, hi
   }
 }
 
+// BN and ring depth: keep >= ~96 KiB of DMA in flight per CU (4 waves x D stages;
+// MI355X_MICROARCH.md: 72 KiB/CU in flight reads HBM at ~6 TB/s) with the slab resident.
+// nE: bf16 epilogue tensors per tile, nM: bit masks per tile, force_bn: 0 (auto) / 64 / 128.
+// Returns 0 with the plan, nonzero when no plan fits (LDS or the 63-op vmcnt window).
+static int s1_plan(int KR, int Nout, int nE, int nM, int force_bn, int* bn_out, int* D_out, int* stage_out,
+                   int* slab_out) {
+  if (KR != 64 && KR != 128 && KR != 256) return 1;
+  if (Nout % 64 != 0) return 2;
+  auto plan = [&](int bn, int* D, int* stage, int* slab) {
+    *slab = bn * 2 * KR;
+    *stage = 16 * (2 * KR + nE * 2 * bn) + nM * 256;   // 256-B mask slots (one 4-B DMA)
+    *stage = (*stage + 15) & ~15;
+    int d = (kS1Lds - *slab) / (4 * *stage);
+    if (d > 8) d = 8;
+    const int n_dma = KR / 32 + nE * (bn / 32) + nM, n_st = bn / 32;
+    while (d > 2 && d * n_st + (d - 1) * n_dma > 63) --d;
+    *D = d;
+    // the final cross-wave combine reuses the ring as scratch
+    return d >= 2 && d * n_st + (d - 1) * n_dma <= 63 && 4 * d * *stage >= 4 * 2 * 2 * bn * 4;
+  };
+  int bn = force_bn;
+  if (bn == 128 || bn == 64) {
+    if (Nout % bn || !plan(bn, D_out, stage_out, slab_out)) return 3;
+  } else {
+    bn = 0;
+    if (Nout % 128 == 0 && plan(128, D_out, stage_out, slab_out) && 4 * *D_out * *stage_out >= 96 * 1024) bn = 128;
+    else if (plan(64, D_out, stage_out, slab_out)) bn = 64;
+    else return 3;
+  }
+  *bn_out = bn;
+  return 0;
+}
+
+// Column tile the launcher would pick for this problem under the current conv1x1_set_bn
+// (0 = not eligible): the tests' and the autotuner's eligibility oracle.
+int conv1x1_stream_bn(int KR, int Nout, int nE, int nM) {
+  int bn = 0, D = 0, stage = 0, slab = 0;
+  return s1_plan(KR, Nout, nE, nM, g_s1_bn, &bn, &D, &stage, &slab) ? 0 : bn;
+}
+
 // Returns 0 when launched, nonzero when the shape / options are outside this kernel.
 int conv1x1_stream_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, int M, int KR, int Nout, bool dgrad,
                           float* stats, const float* shift, const bf16_t* addend, const uint8_t* addend_mask,
                           const BnReduceArgs* bnr, hipStream_t st, int cus) {
-  if (KR != 64 && KR != 128 && KR != 256) return 1;
-  if (Nout % 64 != 0 || M <= 0) return 2;
+  if (M <= 0) return 2;
   const int nb = (dgrad && bnr) ? (bnr->red[1] ? 2 : 1) : 0;
   Stream1x1Args a{};
   a.a = src;
@@ -573,29 +611,9 @@ int conv1x1_stream_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, int 
   a.Nout = Nout;
   a.nE = (a.addend ? 1 : 0) + nb;
   a.nM = (a.amask ? 1 : 0) + (a.bnmask ? 1 : 0);
-  // BN and ring depth: keep >= ~96 KiB of DMA in flight per CU (4 waves x D stages;
-  // MI355X_MICROARCH.md: 72 KiB/CU in flight reads HBM at ~6 TB/s) with the slab resident
-  auto plan = [&](int bn, int* D, int* stage, int* slab) {
-    *slab = bn * 2 * KR;
-    *stage = 16 * (2 * KR + a.nE * 2 * bn) + a.nM * 16 * (bn / 8);
-    *stage = (*stage + 15) & ~15;
-    int d = (kS1Lds - *slab) / (4 * *stage);
-    if (d > 8) d = 8;
-    const int n_dma = KR / 32 + a.nE * (bn / 32) + a.nM, n_st = bn / 32;
-    while (d > 2 && d * n_st + (d - 1) * n_dma > 63) --d;
-    *D = d;
-    return d >= 2 && d * n_st + (d - 1) * n_dma <= 63;
-  };
-  int bn = g_s1_bn;
-  int D = 0, stage = 0, slab = 0;
-  if (bn == 128 || bn == 64) {
-    if (Nout % bn || !plan(bn, &D, &stage, &slab)) return 3;
-  } else {
-    bn = 0;
-    if (Nout % 128 == 0 && plan(128, &D, &stage, &slab) && 4 * D * stage >= 96 * 1024) bn = 128;
-    else if (plan(64, &D, &stage, &slab)) bn = 64;
-    else return 3;
-  }
+  int bn = 0, D = 0, stage = 0, slab = 0;
+  const int rc = s1_plan(KR, Nout, a.nE, a.nM, g_s1_bn, &bn, &D, &stage, &slab);
+  if (rc) return rc;
   a.D = D;
   a.stage = stage;
   a.slab = slab;
@@ -606,7 +624,7 @@ int conv1x1_stream_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, int 
   }
   for (int t = 0; t < 2; ++t) {
     a.moff[t] = off;
-    if (t < a.nM) off += 16 * (bn / 8);
+    if (t < a.nM) off += 256;
   }
   a.tilesN = Nout / bn;
   a.tiles64 = (M + 63) / 64;
@@ -618,8 +636,6 @@ int conv1x1_stream_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, int 
   a.mgroups = mgroups;
   const int grid = mgroups * a.tilesN;
   const int lds = slab + 4 * D * stage;
-  const int need_part = 4 * 2 * 2 * bn * 4;  // final combine scratch inside the ring
-  if (4 * D * stage < need_part) return 4;
 #define S1K(KRV)                                                           \
   if (bn == 128) {                                                         \
     if (dgrad) s1_dispatch_nb<KRV, 128, false>(a, nb, grid, lds, st);     \

@@ -196,6 +196,54 @@ class XgmiComm {
     calls_++;
   }
 
+  // ---- compact per-step entry points (the host path of 106 (R50) / 310 (R152) SyncBN
+  // exchanges per step): a BN module's persistent tensors (gamma, beta, running stats,
+  // num_batches_tracked -- the Parameter / buffer objects themselves, so a flat-arena
+  // relayout that re-points their storage is followed) are registered ONCE as a site;
+  // each exchange then passes only its per-step tensors.
+  int64_t add_site(at::Tensor gamma, at::Tensor beta, c10::optional<at::Tensor> rm, c10::optional<at::Tensor> rv,
+                   c10::optional<at::Tensor> nbt, double eps, double momentum) {
+    Site st;
+    st.gamma = gamma;
+    st.beta = beta;
+    st.rm = rm && rm->defined() ? *rm : at::Tensor();
+    st.rv = rv && rv->defined() ? *rv : at::Tensor();
+    st.nbt = nbt && nbt->defined() ? *nbt : at::Tensor();
+    st.eps = (float)eps;
+    st.mom = (float)momentum;
+    sites_.push_back(st);
+    return (int64_t)sites_.size() - 1;
+  }
+
+  void bn_fwd(at::Tensor slots_a, c10::optional<at::Tensor> slots_b, double count, int64_t site_a, int64_t site_b,
+              at::Tensor params_a, c10::optional<at::Tensor> params_b, at::Tensor count_out,
+              c10::optional<at::Tensor> shift_a, c10::optional<at::Tensor> shift_b) {
+    TORCH_CHECK(site_a >= 0 && site_a < (int64_t)sites_.size() && site_b < (int64_t)sites_.size(),
+                "xgmi bn: unknown site");
+    const Site& A = sites_[site_a];
+    auto opt = [](const at::Tensor& t) { return t.defined() ? c10::optional<at::Tensor>(t) : c10::nullopt; };
+    if (site_b < 0) {
+      bn_(0, slots_a, c10::nullopt, count, A.gamma, A.beta, params_a, opt(A.rm), opt(A.rv), opt(A.nbt), A.eps,
+          A.mom, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt, 1e-5, 0.1,
+          count_out, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt, shift_a,
+          c10::nullopt);
+    } else {
+      const Site& B = sites_[site_b];
+      bn_(0, slots_a, slots_b, count, A.gamma, A.beta, params_a, opt(A.rm), opt(A.rv), opt(A.nbt), A.eps, A.mom,
+          B.gamma, B.beta, params_b, opt(B.rm), opt(B.rv), opt(B.nbt), B.eps, B.mom, count_out, c10::nullopt,
+          c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt, shift_a, shift_b);
+    }
+  }
+
+  void bn_bwd(at::Tensor slots_a, c10::optional<at::Tensor> slots_b, c10::optional<at::Tensor> acc_a0,
+              c10::optional<at::Tensor> acc_a1, c10::optional<at::Tensor> acc_b0,
+              c10::optional<at::Tensor> acc_b1, at::Tensor out_a, c10::optional<at::Tensor> out_b) {
+    bn_(1, slots_a, slots_b, 0.0, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt,
+        c10::nullopt, 1e-5, 0.1, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt, c10::nullopt,
+        c10::nullopt, 1e-5, 0.1, c10::nullopt, acc_a0, acc_a1, acc_b0, acc_b1, out_a, out_b, c10::nullopt,
+        c10::nullopt);
+  }
+
   // host-blocking: did any call time out waiting for a peer?
   bool check() {
     c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, device_));
@@ -221,6 +269,11 @@ class XgmiComm {
   int64_t wall_khz_ = 100000;
   bool opened_ = false;
   int64_t calls_ = 0;
+  struct Site {
+    at::Tensor gamma, beta, rm, rv, nbt;
+    float eps = 1e-5f, mom = 0.1f;
+  };
+  std::vector<Site> sites_;
 };
 
 void register_xgmi(pybind11::module& m) {
@@ -234,6 +287,9 @@ void register_xgmi(pybind11::module& m) {
       .def("open", &XgmiComm::open)
       .def("all_reduce_", &XgmiComm::all_reduce_)
       .def("bn_", &XgmiComm::bn_)
+      .def("add_site", &XgmiComm::add_site)
+      .def("bn_fwd", &XgmiComm::bn_fwd)
+      .def("bn_bwd", &XgmiComm::bn_bwd)
       .def("check", &XgmiComm::check)
       .def("failed", &XgmiComm::failed)
       .def("set_timeout", &XgmiComm::set_timeout, py::arg("timeout_s"))

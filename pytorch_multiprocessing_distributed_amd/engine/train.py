@@ -20,7 +20,7 @@ from ..data.cifar import get_cifar10
 from ..data.loader import DeviceLoader, SyntheticImageNet
 from ..models import build_model
 from ..ops import functional as OF
-from ..utils.trace import region
+from ..utils.trace import check_stream_budget, region, sync_debug_enabled
 from ..parallel.comm import get_comm
 from ..parallel.dp import DataParallel
 from ..utils.checkpoint import load_resume, save_model, save_resume
@@ -67,6 +67,9 @@ def _first_step_tuning(args, rank, comm):
         tuning.save(path)
 
 
+_SYNC_DEBUG = sync_debug_enabled()
+
+
 def train_epoch(loader, model, optimizer, epoch, logger, args, rank, dev, comm=None,
                 step_offset=0):
     batch_time = DeviceMeter()
@@ -91,6 +94,8 @@ def train_epoch(loader, model, optimizer, epoch, logger, args, rank, dev, comm=N
             optimizer.step()
         if comm is not None:
             comm.raise_if_failed()      # xGMI SyncBN timeout of a finished step (no device sync)
+        if _SYNC_DEBUG and dev.type == "cuda":
+            check_stream_budget(comm, model)   # step work fits the hardware queues
         if step_offset + i == 0 and dev.type == "cuda":
             _first_step_tuning(args, rank, comm)
         if comm is not None and comm.order_check_every and (step_offset + i) % comm.order_check_every == 0:

@@ -58,6 +58,9 @@ class Comm:
         return self._side
 
     def _record(self, op, t):
+        if not self.order_check_every:          # checker off: no per-collective hashing
+            self._ncoll += 1
+            return
         key = f"{op}:{t.numel()}:{t.dtype}".encode()
         self._seq = (self._seq * 1000003 + zlib.crc32(key)) & 0x7FFFFFFFFFFFFFF
         self._ncoll += 1

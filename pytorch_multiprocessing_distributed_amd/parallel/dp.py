@@ -138,7 +138,8 @@ def resolve_transport(comm, module, reducer="native", transport="auto", verbose=
     from . import rccl
     c, err = None, ""
     try:
-        c = rccl.create(comm.group)
+        from ..ops.functional import STREAM_PRIO
+        c = rccl.create(comm.group, priority=STREAM_PRIO)
     except Exception as e:  # noqa: BLE001
         err = str(e)
     ok = rccl.self_test(c, comm.group) if c is not None else False
@@ -171,8 +172,17 @@ class DataParallel(nn.Module):
                  first_bucket_mb: float = 1.0, broadcast_buffers: bool = False,
                  check_collectives: bool = True, reducer: str = "native", compress: str = "none",
                  transport: str = "auto", rebuild_buckets: bool = True, timeline: bool | None = None,
-                 last_bucket_mb: float | None = 2.0):
+                 last_bucket_mb: float | None = 2.0, post_hooks: str = "auto"):
         super().__init__()
+        if post_hooks not in ("auto", "always"):
+            raise ValueError(f"bad post_hooks {post_hooks!r}")
+        # "auto": the fused model (ops/functional.py) writes EVERY parameter's gradient
+        # straight into the arena and marks it itself (functional._ready), so the per-
+        # parameter AccumulateGrad post-hooks -- which autograd runs for every parameter of
+        # every step even when its node returned no gradient -- are pure host overhead
+        # there (161 Python calls per ResNet-50 step, 467 for ResNet-152); an unmarked
+        # gradient would still be all-reduced by the finalize, just without overlap
+        self.post_hooks = post_hooks
         self.last_bucket_mb = last_bucket_mb
         self.module = module
         self.comm = comm
@@ -273,14 +283,19 @@ class DataParallel(nn.Module):
     def bucket_sizes_mb(self):
         return [(b.end - b.start) * 4 / 2 ** 20 for b in self.buckets]
 
+    def _direct_only(self):
+        return self.post_hooks == "auto" and getattr(self.module, "impl", None) == "fused"
+
     def _install_hooks(self):
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        direct_only = self._direct_only()
         for i, p in enumerate(self.flat.params):
             h = self._make_native_hook(i) if self._native is not None else self._make_hook(i)
             # AccumulateGrad path (params whose grad is returned to autograd) ...
-            self._hooks.append(p.register_post_accumulate_grad_hook(self._post_hook(h)))
+            if not direct_only:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._post_hook(h)))
             # ... and the direct path (fused ops that wrote into the arena call this)
             p._pmd_ready = h
 

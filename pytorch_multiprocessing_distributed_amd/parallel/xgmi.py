@@ -95,27 +95,30 @@ class XgmiAllReduce:
         return self._c.calls
 
     # ------------------------------------------------------------ SyncBN fused
+    def _site(self, bn):
+        """Native site id of a BN module: its Parameter / buffer objects registered once
+        (XgmiComm.add_site), so a step's exchange passes only its per-step tensors."""
+        key = getattr(bn, "_pmd_xgmi_site", None)
+        if key is None or key[0] != id(self):
+            sid = self._c.add_site(bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                   bn.num_batches_tracked, float(bn.eps), float(bn.momentum))
+            key = (id(self), sid)
+            bn._pmd_xgmi_site = key
+        return key[1]
+
     def bn_fwd(self, slots_a, slots_b, count, bn_a, bn_b, params_a, params_b, count_out,
                shift_a=None, shift_b=None):
         """Collapse the conv-epilogue statistic slots, exchange, finalize: ONE
         kernel per BN site (see xgmi_bn_kernel).  Slots are cleared.  ``shift_*``:
         the statistics shifts the slots were accumulated about (identical on every
         rank), overwritten with the global batch means."""
-        b = bn_b
-        self._c.bn_(0, slots_a, slots_b, float(count),
-                    bn_a.weight.detach(), bn_a.bias.detach(), params_a, bn_a.running_mean,
-                    bn_a.running_var, bn_a.num_batches_tracked, float(bn_a.eps), float(bn_a.momentum),
-                    None if b is None else b.weight.detach(), None if b is None else b.bias.detach(),
-                    params_b, None if b is None else b.running_mean,
-                    None if b is None else b.running_var, None if b is None else b.num_batches_tracked,
-                    float(b.eps) if b is not None else 1e-5, float(b.momentum) if b is not None else 0.1,
-                    count_out, None, None, None, None, None, None, shift_a, shift_b)
+        self._c.bn_fwd(slots_a, slots_b, float(count), self._site(bn_a),
+                       -1 if bn_b is None else self._site(bn_b), params_a, params_b, count_out,
+                       shift_a, shift_b)
 
     def bn_bwd(self, slots_a, slots_b, acc_a, acc_b, out_a, out_b):
         """Collapse the BN-backward reduce slots (+= local sums into the gamma/beta
         gradient arena), exchange, write global [2][C] sums."""
         aa = acc_a or (None, None)
         ab = acc_b or (None, None)
-        self._c.bn_(1, slots_a, slots_b, 0.0, None, None, None, None, None, None, 1e-5, 0.1,
-                    None, None, None, None, None, None, 1e-5, 0.1, None,
-                    aa[0], aa[1], ab[0], ab[1], out_a, out_b, None, None)
+        self._c.bn_bwd(slots_a, slots_b, aa[0], aa[1], ab[0], ab[1], out_a, out_b)

@@ -259,3 +259,38 @@ def test_native_extension_imports():
     takes); it is built by csrc/build.py for gfx950 but imports on any host."""
     from pytorch_multiprocessing_distributed_amd.ops.native import C
     assert C.__file__.endswith(".so") and hasattr(C, "conv_fwd")
+
+
+def test_stream_budget_check_counts_streams():
+    """PMD_SYNC_DEBUG's stream-budget check: framework streams + the SyncBN side stream +
+    the bucket transport's stream must fit the hardware queues (one stream per queue)."""
+    from pytorch_multiprocessing_distributed_amd.utils import trace
+
+    class Side:
+        cuda_stream = 111
+
+    class Comm:
+        _side = Side()
+        backend = "nccl"
+
+    class Model:
+        transport = "rccl"
+
+        class rccl:
+            stream_handle = 222
+    saved = set(trace.STEP_STREAMS)
+    try:
+        trace.STEP_STREAMS.clear()
+        trace.STEP_STREAMS.update({1, 2})
+        assert trace.check_stream_budget(Comm(), Model()) == 4
+        trace.STEP_STREAMS.add(3)
+        with pytest.raises(RuntimeError, match="hardware"):
+            trace.check_stream_budget(Comm(), Model())
+        m = Model()
+        m.rccl = None
+        m.transport = "c10d"
+        trace.STEP_STREAMS.discard(3)
+        assert trace.check_stream_budget(Comm(), m) == 4      # + ProcessGroupNCCL's stream
+    finally:
+        trace.STEP_STREAMS.clear()
+        trace.STEP_STREAMS.update(saved)

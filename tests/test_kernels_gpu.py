@@ -805,6 +805,17 @@ S1_CASES = [
 ]
 
 
+def _s1_expect(KR, Nout, nE, nM, bn):
+    """1 when the streaming kernel has a plan for this problem under column tile bn (the
+    launcher's own planner, conv1x1_stream_bn), else 0 (the tiled kernel runs instead)."""
+    from pytorch_multiprocessing_distributed_amd.ops.native import C as _C
+    _C.conv1x1_set_bn(bn)
+    try:
+        return 1 if _C.conv1x1_stream_bn(KR, Nout, nE, nM) else 0
+    finally:
+        _C.conv1x1_set_bn(0)
+
+
 def _s1_run(fn, policy, bn):
     from pytorch_multiprocessing_distributed_amd.ops.native import C as _C
     _C.conv1x1_set_policy(policy)
@@ -856,7 +867,10 @@ def test_conv1x1_stream_dgrad(case, bn):
     (dx_t, red_t), n_t = _s1_run(run, 0, 0)
     (dx_s, red_s), n_s = _s1_run(run, 1, bn)
     assert n_t == 0
-    assert n_s == (0 if (bn == 128 and C % 128) else 1), n_s
+    want_n = _s1_expect(K, C, (1 if add else 0) + nsets, (1 if add and amask else 0) + (1 if nsets else 0), bn)
+    if bn == 0 or bn == 64:
+        assert want_n == 1, "every ResNet 1x1 dgrad class must have a streaming plan"
+    assert n_s == want_n, n_s
     _close_norm(dx_s, dx_t, CONV_REL_L2)
     _close(dx_s, dx_t, 2e-2)
     # oracle: fp32 dgrad + gated addend, masked by the BN ReLU bits
@@ -895,7 +909,9 @@ def test_conv1x1_stream_fwd_stats(shape, bn):
         return y, HP.stats_collapse(st).view(2, K)
     (y_t, s_t), n_t = _s1_run(run, 0, 0)
     (y_s, s_s), n_s = _s1_run(run, 2, bn)
-    assert n_t == 0 and n_s == (0 if (bn == 128 and K % 128) else 1), n_s
+    assert n_t == 0 and n_s == _s1_expect(Cin, K, 0, 0, bn), n_s
+    if Cin <= 256 and bn != 128:
+        assert n_s == 1
     _close_norm(y_s, y_t, CONV_REL_L2)
     yr, _ = TP.conv_fwd(x, TP.conv_weight(w, torch.bfloat16, Cin), 1, 0, False)
     _close_norm(y_s, yr, CONV_REL_L2)
