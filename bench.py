@@ -133,6 +133,13 @@ def bench_rank(rank, world, a):
     else:
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
+    if OF.STREAM_PRIO:
+        # the rank runs on one high-priority stream: with the weight-gradient, SyncBN and
+        # gradient-bucket streams it gets the high-priority hardware-queue pool to itself,
+        # one queue per stream (ops/functional.py STREAM_PRIO, profiles/queues_r04.txt)
+        st = torch.cuda.Stream(device=dev, priority=OF.STREAM_PRIO)
+        st.wait_stream(torch.cuda.current_stream(dev))
+        torch.cuda.set_stream(st)
     torch.manual_seed(0)
     model = build_model(a.model, num_classes=a.classes, stem=a.stem).to(dev)
     if rehearsal:
@@ -164,17 +171,7 @@ def bench_rank(rank, world, a):
     else:
         tune_source, _ = tuning.load_default()
 
-    # the step on its own high-priority stream with PMD_STREAM_PRIO=1 (ops/functional.py
-    # STREAM_PRIO: every stream of the step in the high-priority hardware-queue pool)
-    step_stream = torch.cuda.Stream(priority=-1) if OF.STREAM_PRIO else None
-
     def step(i):
-        if step_stream is not None:
-            with torch.cuda.stream(step_stream):
-                return _step(i)
-        return _step(i)
-
-    def _step(i):
         x, y = data.batch_at(i)
         out = model(x)
         loss = OF.cross_entropy(out, y)

@@ -153,6 +153,19 @@ __device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// fp8 operand rows (128 B = 128 e4m3/e5m2 reduction elements): lane l of a
+// 16x16x128 fragment read takes row l & 15 and the 16-B chunk PAIR 2 (l >> 4) + {0, 1}.
+// A ds_read_b128 lane group (MI355X_MICROARCH.md §LDS: {0-3,12-15,20-27}, ...) then holds
+// rows {0-3,12-15} at chunk x and rows 4-11 at chunk x ^ 2; the bf16 swizzles give those
+// two row sets the same bank slots (2-way).  Map row pairs {0,1,6,7} (row >> 1) to odd and
+// {2,3,4,5} to even XOR values: the x ^ 2 half then lands on the complementary slots,
+// conflict-free for both chunks of the pair (brute-force check:
+// tests/test_host_logic.py::test_fp8_fragment_swizzle_conflict_free).
+__device__ __forceinline__ int swz_f8(int row) {
+  constexpr unsigned kPerm = 0x75642031u;  // nibble p = XOR of row pair p
+  return (kPerm >> (4 * ((row >> 1) & 7))) & 7;
+}
+
 // Bijective XCD-aware block remap (MI355X: 8 XCDs, blocks dispatched
 // round-robin).  Blocks that share an XCD (same id % 8) get consecutive
 // logical tile ids so neighbouring tiles reuse operand panels in that XCD's

@@ -266,8 +266,9 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
   //      holding logical chunk (l%CH) ^ swz(row)
   // DMA: LDS chunk lane % CH of A (B) instruction i's tile row holds logical chunk
   // achunk(i) (bchunk(i)); the swizzle is taken of the absolute tile row
-  auto achunk = [&](int i) { return DMA ? ((lane % CH) ^ swz<BK>(wid * (BM / NW) + RPI * i + lane / CH)) : (tid & 7); };
-  auto bchunk = [&](int i) { return DMA ? ((lane % CH) ^ swz<BK>(wid * (BN / NW) + RPI * i + lane / CH)) : (tid & 7); };
+  auto swzk = [](int row) { return F8 ? swz_f8(row) : swz<BK>(row); };
+  auto achunk = [&](int i) { return DMA ? ((lane % CH) ^ swzk(wid * (BM / NW) + RPI * i + lane / CH)) : (tid & 7); };
+  auto bchunk = [&](int i) { return DMA ? ((lane % CH) ^ swzk(wid * (BN / NW) + RPI * i + lane / CH)) : (tid & 7); };
   const int chunk = tid & 7;  // register staging
   const int rsub = tid >> 3;  // 0..31
   auto a_row_of = [&](int i) { return DMA ? wid * (BM / NW) + RPI * i + lane / CH : rsub + 32 * i; };
@@ -491,8 +492,8 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
       // lane l holds row l & 15, reduction bytes 32 (l >> 4) .. +31 = logical chunks q0, q0+1
       const int q0 = 2 * (lane >> 4);
       auto frag8 = [&](const bf16_t* base, int r) {
-        const uint4 lo = *reinterpret_cast<const uint4*>(base + r * LDR + ((q0 ^ swz<BK>(r)) << 3));
-        const uint4 hi = *reinterpret_cast<const uint4*>(base + r * LDR + (((q0 + 1) ^ swz<BK>(r)) << 3));
+        const uint4 lo = *reinterpret_cast<const uint4*>(base + r * LDR + ((q0 ^ swz_f8(r)) << 3));
+        const uint4 hi = *reinterpret_cast<const uint4*>(base + r * LDR + (((q0 + 1) ^ swz_f8(r)) << 3));
         i32x8_c v;
         v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
         v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
@@ -504,19 +505,33 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
       // formats: the gathered operand is e5m2 (bf8) in dgrad (dY), e4m3 in fwd; weights e4m3
       constexpr int FA = DGRAD ? 1 : 0;
       if constexpr (NST1) {
-        // single-stage (short-reduction, epilogue-bound) variant: ONE A and ONE B fragment
-        // live at a time (the A fragments are re-read NI times from LDS -- 1-4 K-tiles per
-        // block, negligible) so the kernel stays at 4 waves per SIMD like the bf16 one
+        // single-stage (short-reduction, epilogue-bound) variant: NJ B fragments and ONE A
+        // fragment live at a time, i.e. every A fragment is read NI / NJ times from LDS.
+        // NJ = NI (default) reads each fragment once: the fused-epilogue instantiation
+        // (128x128, 2 BN sets) compiles to 152 VGPRs at NJ = 1 or 2 and 158 at NJ = 4 --
+        // 3 waves per SIMD in every case (the epilogue, not the held fragments, sets the
+        // register peak), so the re-reads bought no occupancy
+#ifndef PMD_F8_NJ
+#define PMD_F8_NJ 4
+#endif
+        constexpr int NJ = PMD_F8_NJ < NI ? PMD_F8_NJ : NI;
+        static_assert(NI % NJ == 0, "NJ divides NI");
 #pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          const i32x8_c bf = frag8(Bs, wn * (BN / WN) + j * 16 + frow);
+        for (int j0 = 0; j0 < NI; j0 += NJ) {
+          i32x8_c bf[NJ];
+#pragma unroll
+          for (int jj = 0; jj < NJ; ++jj) bf[jj] = frag8(Bs, wn * (BN / WN) + (j0 + jj) * 16 + frow);
 #pragma unroll
           for (int i = 0; i < MI; ++i) {
             const i32x8_c af = frag8(As, wm * (BM / WM) + i * 16 + frow);
-            acc[i][j] = SWAPC ? __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bf, af, acc[i][j], 0, FA, 0, 127,
-                                                                                0, 127)
-                              : __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bf, acc[i][j], FA, 0, 0, 127,
-                                                                                0, 127);
+#pragma unroll
+            for (int jj = 0; jj < NJ; ++jj) {
+              const int j = j0 + jj;
+              acc[i][j] = SWAPC ? __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bf[jj], af, acc[i][j], 0, FA, 0,
+                                                                                  127, 0, 127)
+                                : __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bf[jj], acc[i][j], FA, 0, 0,
+                                                                                  127, 0, 127);
+            }
             __builtin_amdgcn_sched_barrier(0);
           }
         }

@@ -232,8 +232,8 @@ __device__ __attribute__((aligned(16))) unsigned char g_zero16_f8[64];
 // (e4m3 x e4m3, unit block scales; 2x the bf16 MFMA rate per clock):
 //   Y[m][k] = (1 / (sx * sw)) * sum_{r,s,c} Xq[n, ...] * Wq[k, r, s, c]
 // Same tiling as the bf16 kernel (BM x BN tile, 4 waves in 2x2, LDS-DMA
-// double buffer) with a K-tile of 128 fp8 = 128-B LDS rows (chunk swizzle
-// row & 7) and one 16x16x128 MFMA per fragment pair.  bf16 output + fused
+// double buffer) with a K-tile of 128 fp8 = 128-B LDS rows (fp8 chunk swizzle
+// swz_f8, common.h: conflict-free 32-B fragment reads) and one 16x16x128 MFMA per fragment pair.  bf16 output + fused
 // per-channel (sum, sum^2) statistics for BatchNorm, as the bf16 kernel.
 struct Fp8ConvArgs {
   const uint8_t* src;  // NHWC e4m3 [N,H,W,C]
@@ -268,7 +268,9 @@ __global__ __launch_bounds__(256, 2) void conv_fp8_fwd_kernel(Fp8ConvArgs a) {
   const int m0 = (L / tilesN) * BM, n0 = (L % tilesN) * BN;
   if (m0 >= a.M) return;
 
-  const int chunk = (lane & 7) ^ ((lane >> 3) & 7);  // logical 16-B chunk this lane fetches
+  // logical 16-B chunk this lane fetches into row 8 i + lane / 8 (mod 16) of its 8-row piece:
+  // fp8 swizzle (common.h swz_f8), which depends on the row parity of the piece (i & 1)
+  const int chunk2[2] = {(lane & 7) ^ swz_f8(lane >> 3), (lane & 7) ^ swz_f8(8 + (lane >> 3))};
   int a_base[PA], a_h[PA], a_w[PA];
   bool a_ok[PA];
   const int ohw = a.OH * a.OW;
@@ -293,14 +295,23 @@ __global__ __launch_bounds__(256, 2) void conv_fp8_fwd_kernel(Fp8ConvArgs a) {
   }
   const int nk = (a.Kg + BK - 1) / BK;
   auto load_tile = [&](int kt, int buf) {
-    const int k0 = kt * BK + chunk * 16;
-    const bool kok = k0 < a.Kg;
-    const int tap = k0 >> a.log2Cs;
-    const int c = k0 & (a.Cs - 1);
-    const int r = tap / a.S, s = tap - (tap / a.S) * a.S;
-    const int boff = ((r * a.S + s) << a.log2Cs) + c;
+    // the two chunk variants' taps (a K-tile of 128 spans two taps when Cs = 64)
+    int kr[2], ks[2], kc[2], kb[2];
+    bool kk[2];
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int k0 = kt * BK + chunk2[v] * 16;
+      kk[v] = k0 < a.Kg;
+      const int tap = k0 >> a.log2Cs;
+      kc[v] = k0 & (a.Cs - 1);
+      kr[v] = tap / a.S;
+      ks[v] = tap - kr[v] * a.S;
+      kb[v] = ((kr[v] * a.S + ks[v]) << a.log2Cs) + kc[v];
+    }
 #pragma unroll
     for (int i = 0; i < PA; ++i) {
+      const int r = kr[i & 1], s = ks[i & 1], c = kc[i & 1];
+      const bool kok = kk[i & 1];
       const int ih = a_h[i] + r, iw = a_w[i] + s;
       const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
       const void* src = g_zero16_f8;
@@ -311,7 +322,7 @@ __global__ __launch_bounds__(256, 2) void conv_fp8_fwd_kernel(Fp8ConvArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
-      const void* src = (b_ok[i] && kok) ? (const void*)(b_row[i] + boff) : (const void*)g_zero16_f8;
+      const void* src = (b_ok[i] && kk[i & 1]) ? (const void*)(b_row[i] + kb[i & 1]) : (const void*)g_zero16_f8;
       uint8_t* dst = lds + buf * STAGE + A_B + (wid * (BN / 4) + 8 * i) * BK;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
@@ -325,8 +336,8 @@ __global__ __launch_bounds__(256, 2) void conv_fp8_fwd_kernel(Fp8ConvArgs a) {
   const int frow = lane & 15;
   const int q0 = 2 * (lane >> 4);  // lane holds k = 32 (lane>>4) + 0..31 = chunks q0, q0+1
   auto frag = [&](const uint8_t* base, int r) {
-    const uint4 lo = *reinterpret_cast<const uint4*>(base + r * BK + ((q0 ^ (r & 7)) << 4));
-    const uint4 hi = *reinterpret_cast<const uint4*>(base + r * BK + (((q0 + 1) ^ (r & 7)) << 4));
+    const uint4 lo = *reinterpret_cast<const uint4*>(base + r * BK + ((q0 ^ swz_f8(r)) << 4));
+    const uint4 hi = *reinterpret_cast<const uint4*>(base + r * BK + (((q0 + 1) ^ swz_f8(r)) << 4));
     i32x8 v;
     v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
     v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;

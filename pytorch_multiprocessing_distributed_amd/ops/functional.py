@@ -320,15 +320,15 @@ _WGRAD_STREAM = {"on": os.environ.get("PMD_WGRAD_STREAM", "1") != "0", "streams"
 _SPLIT_WPREP = os.environ.get("PMD_SPLIT_WPREP", "0") == "1"
 
 
-# Priority of the step's own HIP streams (PMD_STREAM_PRIO=1: high, -1).  HIP keeps one pool
-# of hardware queues per priority (GPU_MAX_HW_QUEUES each) and hands a new stream the least
-# shared queue of its pool; RCCL / c10d create several long-lived streams of their own in
+# Priority of the step's own HIP streams (default high, -1; PMD_STREAM_PRIO=0: normal).
+# HIP keeps one pool of hardware queues per priority (GPU_MAX_HW_QUEUES each) and hands a
+# new stream the least shared queue of its pool; RCCL / c10d create several long-lived streams of their own in
 # the normal pool, so a normal-priority side stream can land on the SAME hardware queue as
 # the main stream and lose all its overlap (bench/queue_map.py, profiles/queues_r04.txt).
 # With the step's streams (main, weight gradients, SyncBN exchange, gradient buckets) all in
 # the high-priority pool they get one queue each (see docs/ARCHITECTURE.md, "Streams ->
 # hardware queues").
-STREAM_PRIO = -1 if os.environ.get("PMD_STREAM_PRIO", "0") == "1" else 0
+STREAM_PRIO = 0 if os.environ.get("PMD_STREAM_PRIO", "1") == "0" else -1
 
 
 def _wgrad_stream(dev):

@@ -885,8 +885,16 @@ def test_conv1x1_stream_dgrad(case, bn):
         bits = (mk.view(-1, 1).int() >> torch.arange(8, device=DEV).view(1, 8)) & 1
         dxr = dxr * bits.view(dxr.shape).float()
     _close_norm(dx_s, dxr, CONV_REL_L2)
-    for a_, b_ in zip(red_s, red_t):
-        torch.testing.assert_close(a_, b_, rtol=2e-3, atol=2e-3 * b_.abs().max().item())
+    # BN-backward reduce: the streaming kernel sums the STORED (bf16-rounded, masked) dz --
+    # exact against fp32 sums of its own output; the tiled kernel sums the fp32 values
+    # before rounding, so the two differ by the bf16 rounding of dz (a random ~2^-9 per
+    # term: ~2e-3 of a cancelling channel sum), which bounds their mutual check
+    for (yb, pb), a_, b_ in zip(sets, red_s, red_t):
+        dz = dx_s.float().reshape(-1, C)
+        ref = torch.stack([dz.sum(0), (dz * (yb.float().reshape(-1, C) - pb[0])).sum(0) * pb[1]])
+        scale = ref.abs().max().item()
+        torch.testing.assert_close(a_, ref, rtol=1e-4, atol=1e-4 * scale)
+        assert (b_ - ref).norm() / ref.norm() < 5e-3
 
 
 @pytest.mark.parametrize("bn", [0, 64, 128])
