@@ -86,6 +86,9 @@ def parse():
     ap.add_argument("--timeline", action="store_true",
                     help="print the gradient-bucket launch/overlap timeline of the last step")
     ap.add_argument("--profile", default="", help="write a torch.profiler table here (rank 0)")
+    ap.add_argument("--host_profile", default="",
+                    help="after the timed run: cProfile the host side of 10 more steps (rank 0) and "
+                         "write the top functions by own time here")
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole training step (fwd+bwd+SGD) in a HIP graph and replay it "
                          "(single GPU); each replay is a full step on a freshly generated batch")
@@ -292,6 +295,28 @@ def bench_rank(rank, world, a):
             rec["vs_stock_pytorch_rocm_recorded"] = round(ips / STOCK_IPS_PER_GPU_RECORDED, 3)
             rec["stock_recorded_source"] = STOCK_RECORDED_SOURCE
         print(json.dumps(rec), flush=True)
+    if a.host_profile:
+        # host cost of the step alone (the JSON above is unaffected): where the enqueue
+        # time goes, per Python function and per native call, over 10 steps
+        import cProfile
+        import io
+        import pstats
+        torch.cuda.synchronize()
+        pr = cProfile.Profile()
+        pr.enable()
+        for i in range(10):
+            step(i)
+            if comm is not None:
+                comm.raise_if_failed()
+        pr.disable()
+        torch.cuda.synchronize()
+        if rank == 0:
+            buf = io.StringIO()
+            pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(45)
+            with open(a.host_profile, "w") as f:
+                f.write(f"# bench.py host profile, 10 steps, {a.model} batch {a.batch}, "
+                        f"parallelism {parallelism}\n")
+                f.write(buf.getvalue())
     if a.profile and rank == 0:
         from torch.profiler import ProfilerActivity, profile
         with profile(activities=[ProfilerActivity.CUDA]) as prof:

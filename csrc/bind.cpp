@@ -122,6 +122,23 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor wk, int64_t stride, int64_t pad, b
   return conv_fwd_impl(x, wk, stride, pad, want_stats, stats_buf, -1, -1, shift);
 }
 
+// BN-apply prologue experiment: y = conv(relu(x * p[2] + p[3])) for a 1x1 stride-1 conv,
+// x the PRE-BN activation, without materialising the BN output
+std::vector<Tensor> conv_fwd_pro(Tensor x, Tensor wk, Tensor p, bool want_stats, c10::optional<Tensor> stats_buf,
+                                 c10::optional<Tensor> shift) {
+  CHECK_DEV(p); CHECK_CONT(p);
+  TORCH_CHECK(p.scalar_type() == torch::kFloat32 && p.numel() == 4 * x.size(3), "p: fp32 [4][C]");
+  pmd::conv_set_prologue(p.data_ptr<float>());
+  try {
+    auto r = conv_fwd_impl(x, wk, 1, 0, want_stats, stats_buf, -1, -1, shift);
+    pmd::conv_set_prologue(nullptr);
+    return r;
+  } catch (...) {
+    pmd::conv_set_prologue(nullptr);
+    throw;
+  }
+}
+
 std::vector<Tensor> conv_fwd_hw(Tensor x, Tensor wk, int64_t stride, int64_t pad, int64_t out_h,
                                 int64_t out_w, bool want_stats, c10::optional<Tensor> stats_buf,
                                 c10::optional<Tensor> shift) {
@@ -1028,6 +1045,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   namespace py = pybind11;
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("wk"), py::arg("stride"), py::arg("pad"),
         py::arg("want_stats"), py::arg("stats_buf"), py::arg("shift") = py::none());
+  m.def("conv_fwd_pro", &conv_fwd_pro, py::arg("x"), py::arg("wk"), py::arg("p"), py::arg("want_stats") = true,
+        py::arg("stats_buf") = py::none(), py::arg("shift") = py::none(),
+        "1x1 conv forward of relu(x * p[2] + p[3]) (BN-apply prologue experiment)");
   m.def("conv_fwd_hw", &conv_fwd_hw, py::arg("x"), py::arg("wk"), py::arg("stride"), py::arg("pad"),
         py::arg("out_h"), py::arg("out_w"), py::arg("want_stats"), py::arg("stats_buf"),
         py::arg("shift") = py::none());
