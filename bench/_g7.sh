@@ -3,6 +3,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 bash bench/gpu_run.sh \
  "s1tests:300:python -u -m pytest tests/test_kernels_gpu.py -k \"conv1x1_stream\" -q --timeout 120 --timeout-method thread" \
  "f8tests:400:python -u -m pytest tests/test_fp8_gpu.py -x -q --timeout 200 --timeout-method thread" \
+ "protest:200:python -u -m pytest tests/test_kernels_gpu.py -k bn_prologue -q --timeout 100 --timeout-method thread" \
  "pro:200:python bench/bn_prologue_bench.py" \
  "r50:200:python bench.py --steps 30 --warmup 10" \
  "r50_f8:200:python bench.py --steps 30 --warmup 10 --dtype fp8" \

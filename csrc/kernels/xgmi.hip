@@ -29,7 +29,47 @@
 // check runs before any checkpoint is written: a poisoned state is never saved.
 #include "common.h"
 
+// Memory ordering of the exchange (PMD_XGMI_LIGHT, default 1).  Receive buffers and flags
+// live in UNCACHED memory (MTYPE UC, runtime/xgmi.cpp): stores to them bypass the L2s and
+// loads from them always reach memory, so publishing needs no cache maintenance, only
+// completion: the writer waits for its payload stores (s_waitcnt vmcnt(0)) before the flag
+// store, and the reader's spin reads the flag with plain (relaxed) system-scope loads and
+// reads the payload only after a load returned the epoch.  The C++ release / acquire forms
+// (__threadfence_system, release store, acquire loads) add an L2 write-back (buffer_wbl2)
+// per block and an L2 invalidate per spin iteration -- writing back the dirty conv output
+// lines of the XCD's L2 on every SyncBN call.  Measured at W = 1 (rehearsal, full R50 step):
+// PMD_XGMI_LIGHT=0 spends 24 us per call (98 calls, 2.4 ms per step) -- profiles/rehearsal_r04.txt.
+#ifndef PMD_XGMI_LIGHT
+#define PMD_XGMI_LIGHT 1
+#endif
+
 namespace pmd {
+
+// payload stores complete (acknowledged) before the flag store that publishes them
+__device__ __forceinline__ void xgmi_publish_fence() {
+  if constexpr (PMD_XGMI_LIGHT)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else
+    __threadfence_system();
+}
+__device__ __forceinline__ void xgmi_flag_store(uint32_t* f, uint32_t e) {
+  if constexpr (PMD_XGMI_LIGHT)
+    __hip_atomic_store(f, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  else
+    __hip_atomic_store(f, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t xgmi_flag_load(const uint32_t* f) {
+  if constexpr (PMD_XGMI_LIGHT)
+    return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  else
+    return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// payload read of the receive buffer: a system-scope load (sc0 sc1: bypasses the CU's
+// vector L1 as well, which no acquire invalidates any more in the light protocol)
+__device__ __forceinline__ float xgmi_ld(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 struct XgmiPeers {
   float* data[kXgmiMaxRanks];
@@ -41,7 +81,7 @@ struct XgmiPeers {
 __device__ __forceinline__ bool xgmi_wait_flag(const uint32_t* f, uint32_t e, unsigned long long ticks,
                                                uint32_t* err, uint32_t* err_host) {
   const unsigned long long t0 = (unsigned long long)wall_clock64();
-  while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+  while ((int)(xgmi_flag_load(f) - e) < 0) {
     if ((unsigned long long)wall_clock64() - t0 > ticks) {
       atomicOr(err, 1u);
       if (err_host) __hip_atomic_store(err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -83,24 +123,22 @@ __global__ __launch_bounds__(256) void xgmi_allreduce_kernel(XgmiPeers peers, fl
       for (int i = tid; i < len; i += 256) dst[i] = x[lo + i];
     }
   }
-  __threadfence_system();
+  xgmi_publish_fence();
   __syncthreads();
   // 2) raise my flag (block b) in every rank's buffer
-  if (tid < world)
-    __hip_atomic_store(peers.flags[tid] + rank * kXgmiMaxBlocks + b, e, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid < world) xgmi_flag_store(peers.flags[tid] + rank * kXgmiMaxBlocks + b, e);
   // 3) wait until every rank's chunk for epoch e has landed in MY buffer
   if (tid < world) {
     const uint32_t* f = peers.flags[rank] + tid * kXgmiMaxBlocks + b;
     if (!xgmi_wait_flag(f, e, timeout_ticks, err, err_host)) bad_sh = 1;
   }
-  __syncthreads();
+  __syncthreads();   // (the flag loads returned before any thread reads the payload below)
   // 4) sum the W slots in rank order (identical on every rank); NaN on timeout
   const float* mine = peers.data[rank] + (size_t)p * world * kXgmiCap + lo;
   const bool bad = bad_sh != 0;
   for (int i = tid; i < len; i += 256) {
     float s = 0.f;
-    for (int r = 0; r < world; ++r) s += mine[(size_t)r * kXgmiCap + i];
+    for (int r = 0; r < world; ++r) s += xgmi_ld(mine + (size_t)r * kXgmiCap + i);
     x[lo + i] = bad ? __builtin_nanf("") : s;
   }
   (void)nb;
@@ -205,27 +243,25 @@ __global__ __launch_bounds__(256) void xgmi_bn_kernel(XgmiPeers peers, XgmiBnArg
     for (int i = tid; i < 2 * np; i += 256) dst[i] = loc[i];
     if (tid == 0) dst[2 * kBnPairs] = loc[2 * kBnPairs];
   }
-  __threadfence_system();
+  xgmi_publish_fence();
   __syncthreads();
   // 2) flag, 3) wait
-  if (tid < world)
-    __hip_atomic_store(peers.flags[tid] + rank * kXgmiMaxBlocks + b, e, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid < world) xgmi_flag_store(peers.flags[tid] + rank * kXgmiMaxBlocks + b, e);
   if (tid < world) {
     const uint32_t* f = peers.flags[rank] + tid * kXgmiMaxBlocks + b;
     if (!xgmi_wait_flag(f, e, timeout_ticks, err, err_host)) bad_sh = 1;
   }
-  __syncthreads();
+  __syncthreads();   // (the flag loads returned before any thread reads the payload below)
   const bool bad = bad_sh != 0;
   // 4) global sums in rank order, then finalize / publish (NaN outputs on timeout)
   const float* mine = peers.data[rank] + (size_t)par * world * kXgmiCap + (size_t)b * kXgmiChunk;
   float cnt = 0.f;
-  for (int r = 0; r < world; ++r) cnt += mine[(size_t)r * kXgmiCap + 2 * kBnPairs];
+  for (int r = 0; r < world; ++r) cnt += xgmi_ld(mine + (size_t)r * kXgmiCap + 2 * kBnPairs);
   for (int j = tid; j < np; j += 256) {
     float g0 = 0.f, g1 = 0.f;
     for (int r = 0; r < world; ++r) {
-      g0 += mine[(size_t)r * kXgmiCap + 2 * j];
-      g1 += mine[(size_t)r * kXgmiCap + 2 * j + 1];
+      g0 += xgmi_ld(mine + (size_t)r * kXgmiCap + 2 * j);
+      g1 += xgmi_ld(mine + (size_t)r * kXgmiCap + 2 * j + 1);
     }
     const int pi = p0 + j;
     const bool isA = pi < a.CA;

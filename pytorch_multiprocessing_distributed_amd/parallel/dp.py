@@ -350,7 +350,12 @@ class DataParallel(nn.Module):
             by_dtype.setdefault(b.dtype, []).append(b)
         for bufs in by_dtype.values():
             flat = torch.cat([b.reshape(-1) for b in bufs])
-            self.comm.broadcast_(flat, 0)
+            # in-step: on the gradient transport's own communicator (the native one never
+            # shares the step with a c10d collective, Comm.in_step_c10d_forbidden)
+            if self.rccl is not None:
+                self.rccl.broadcast_(flat, 0)
+            else:
+                self.comm.broadcast_(flat, 0)
             off = 0
             for b in bufs:
                 n = b.numel()

@@ -958,3 +958,30 @@ def test_wgrad_deferred_grouped_reduce_matches_immediate():
     torch.cuda.synchronize()
     for o, r in zip(outs, ref):
         assert torch.equal(o, r)
+
+
+@pytest.mark.parametrize("C,K,H", [(64, 256, 9), (128, 512, 7), (32, 64, 5)])
+def test_conv_fwd_bn_prologue(C, K, H):
+    """BN-apply prologue experiment (conv_igemm_kernel<..., PRO>): the 1x1 forward of
+    relu(y * scale + shift) formed on the A fragments == the conv of bn_apply's z, and ==
+    the fp32 oracle; statistics match; ragged M; a 64-column tile (K = 64)."""
+    from pytorch_multiprocessing_distributed_amd.ops.native import C as _C
+    HP = _hp()
+    torch.manual_seed(21)
+    N = 3
+    y = (torch.randn(N, H, H, C, device=DEV) * 2 + 0.5).to(torch.bfloat16)
+    p = torch.stack([torch.zeros(C, device=DEV), torch.ones(C, device=DEV),
+                     torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.5]).contiguous()
+    w = (torch.randn(K, C, 1, 1, device=DEV) / C ** 0.5).contiguous(memory_format=torch.channels_last)
+    wp = HP.conv_weight(w, torch.bfloat16, C, True)
+    shift = torch.randn(K, device=DEV) * 0.05
+    z, _ = HP.bn_apply(y, p, relu=True)
+    ref, st_ref = _C.conv_fwd(z, wp[0], 1, 0, True, None, shift)
+    out, st = _C.conv_fwd_pro(y, wp[0], p, True, None, shift)
+    _close_norm(out, ref, CONV_REL_L2)
+    zr = torch.relu(y.float() * p[2] + p[3]).to(torch.bfloat16)
+    assert torch.equal(z, zr)
+    oracle = (zr.float().reshape(-1, C) @ w.float().reshape(K, C).t()).reshape(out.shape)
+    _close_norm(out, oracle, CONV_REL_L2)
+    a_, b_ = HP.stats_collapse(st).view(2, K), HP.stats_collapse(st_ref).view(2, K)
+    torch.testing.assert_close(a_, b_, rtol=2e-3, atol=2e-3 * b_.abs().max().item())
