@@ -176,7 +176,7 @@ namespace pmd {
 //      running stats, num_batches_tracked, global count); backward: writes the
 //      global (sum dz, sum dz*xhat) as [2][C] for bn_bwd_elemt.
 constexpr int kBnPairs = (kXgmiChunk - 2) / 2;  // 255 channels per block; [2*kBnPairs] = count
-static int g_bn_pairs = 128;  // measured best of {255,128,64,32} (tests/test_xgmi_gpu.py)
+static int g_bn_pairs = 64;  // one 64-channel collapse pass per block (see the kernel)
 void xgmi_set_bn_pairs(int pairs) { g_bn_pairs = pairs < 1 ? 1 : (pairs > kBnPairs ? kBnPairs : pairs); }
 
 __global__ __launch_bounds__(256) void xgmi_bn_kernel(XgmiPeers peers, XgmiBnArgs a, int rank, int world,
@@ -184,6 +184,7 @@ __global__ __launch_bounds__(256) void xgmi_bn_kernel(XgmiPeers peers, XgmiBnArg
                                                      uint32_t* __restrict__ err, uint32_t* err_host,
                                                      unsigned long long timeout_ticks) {
   __shared__ float loc[kXgmiChunk];
+  __shared__ float part[4][64][2];
   __shared__ uint32_t e_sh;
   __shared__ int bad_sh;
   const int b = blockIdx.x, tid = threadIdx.x;
@@ -195,41 +196,57 @@ __global__ __launch_bounds__(256) void xgmi_bn_kernel(XgmiPeers peers, XgmiBnArg
   const int P = a.CA + a.CB;
   const int p0 = b * a.pairs;
   const int np = min(a.pairs, P - p0);
-  // 0) collapse my channels' slots: one channel per thread (np <= kBnPairs < 256), all
-  //    2 * kStatSlots slot loads issued before the first add -- the slots were filled
-  //    by memory-side atomics, so each read is a full memory round trip and a
-  //    dependent chain would cost kStatSlots of them
-  static_assert(kBnPairs <= 256, "one channel per thread");
-  if (tid < np) {
-    const int pi = p0 + tid;
-    const bool isA = pi < a.CA;
-    float* slots = isA ? a.slotsA : a.slotsB;
-    const int C = isA ? a.CA : a.CB;
-    const int c = isA ? pi : pi - a.CA;
-    float v0[kStatSlots], v1[kStatSlots];
+  // 0) collapse my channels' slots, laid out like the local stats_collapse kernel: 64
+  //    channels per pass, the 4 waves each summing 16 of the kStatSlots slots (all loads
+  //    issued before the first add -- the slots were filled by memory-side atomics, so each
+  //    read is a full memory round trip), then a fixed-order combine of the 4 partials
+  //    through LDS.  (One thread per channel summing all 64 slots was 2.5x slower per
+  //    call: 4x less memory-level parallelism per channel.)
+  static_assert(kStatSlots == 64, "4 groups of 16 slots");
+  {
+    const int li = tid & 63, g = tid >> 6;
+    for (int j0 = 0; j0 < np; j0 += 64) {
+      const int j = j0 + li;
+      const int pi = p0 + j;
+      const bool isA = pi < a.CA;
+      float* slots = isA ? a.slotsA : a.slotsB;
+      const int C = isA ? a.CA : a.CB;
+      const int c = isA ? pi : pi - a.CA;
+      float s0 = 0.f, s1 = 0.f;
+      if (j < np) {
+        float v0[16], v1[16];
 #pragma unroll
-    for (int k = 0; k < kStatSlots; ++k) {
-      v0[k] = slots[(size_t)k * 2 * C + c];
-      v1[k] = slots[(size_t)k * 2 * C + C + c];
-    }
-    float s0 = 0.f, s1 = 0.f;
+        for (int k = 0; k < 16; ++k) {
+          v0[k] = slots[(size_t)(16 * g + k) * 2 * C + c];
+          v1[k] = slots[(size_t)(16 * g + k) * 2 * C + C + c];
+        }
 #pragma unroll
-    for (int k = 0; k < kStatSlots; ++k) {
-      s0 += v0[k];
-      s1 += v1[k];
-    }
+        for (int k = 0; k < 16; ++k) {
+          s0 += v0[k];
+          s1 += v1[k];
+        }
 #pragma unroll
-    for (int k = 0; k < kStatSlots; ++k) {
-      slots[(size_t)k * 2 * C + c] = 0.f;
-      slots[(size_t)k * 2 * C + C + c] = 0.f;
-    }
-    loc[2 * tid] = s0;
-    loc[2 * tid + 1] = s1;
-    if (a.mode == 1) {
-      float* acc0 = isA ? a.accA0 : a.accB0;
-      float* acc1 = isA ? a.accA1 : a.accB1;
-      if (acc0) acc0[c] += s0;
-      if (acc1) acc1[c] += s1;
+        for (int k = 0; k < 16; ++k) {
+          slots[(size_t)(16 * g + k) * 2 * C + c] = 0.f;
+          slots[(size_t)(16 * g + k) * 2 * C + C + c] = 0.f;
+        }
+      }
+      part[g][li][0] = s0;
+      part[g][li][1] = s1;
+      __syncthreads();
+      if (g == 0 && j < np) {
+        s0 = ((part[0][li][0] + part[1][li][0]) + part[2][li][0]) + part[3][li][0];
+        s1 = ((part[0][li][1] + part[1][li][1]) + part[2][li][1]) + part[3][li][1];
+        loc[2 * j] = s0;
+        loc[2 * j + 1] = s1;
+        if (a.mode == 1) {
+          float* acc0 = isA ? a.accA0 : a.accB0;
+          float* acc1 = isA ? a.accA1 : a.accB1;
+          if (acc0) acc0[c] += s0;
+          if (acc1) acc1[c] += s1;
+        }
+      }
+      __syncthreads();   // part[] is reused by the next pass
     }
   }
   if (tid == 0) loc[2 * kBnPairs] = a.count;

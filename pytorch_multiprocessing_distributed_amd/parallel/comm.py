@@ -36,10 +36,13 @@ class Comm:
         self.order_check_every = int(os.environ.get("PMD_CHECK_ORDER", "0"))
         self._seq = 0
         self._ncoll = 0
-        # backward SyncBN exchanges run on a high-priority side stream so they
-        # overlap the weight-gradient GEMM issued between the producing dgrad
-        # and the BN backward (see ops/functional.py::_bn_backward)
-        self.overlap_bn_bwd = os.environ.get("PMD_SYNCBN_OVERLAP", "1") != "0"
+        # PMD_SYNCBN_OVERLAP=1: backward SyncBN exchanges on a high-priority side stream
+        # (forked after the producing dgrad, joined before bn_bwd_elemt).  Off by default
+        # since round 4: the main stream has nothing to run between the two (the weight
+        # gradients already live on their own stream), so the fork/join only added two
+        # cross-stream hops per BN site -- 21.14 vs 20.86 ms per ResNet-50 step in the
+        # W=1 rehearsal (profiles/rehearsal_r04.txt)
+        self.overlap_bn_bwd = os.environ.get("PMD_SYNCBN_OVERLAP", "0") == "1"
         self._side = None
         # native communicators carrying in-step traffic (the gradient reducer's
         # RcclComm): their asynchronous error state is part of raise_if_failed
