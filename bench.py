@@ -243,6 +243,20 @@ def bench_rank(rank, world, a):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
     final_loss = float(loss.item())
+    # host cost of ONE step from an idle device (nothing queued ahead, so no enqueue ever
+    # blocks on a full hardware queue): the pure host side of the step, after the timed
+    # region; host_enqueue_ms_per_step above includes such blocking once the host runs
+    # ahead of the device
+    iso = []
+    for i in range(3):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        step(i)
+        iso.append(time.perf_counter() - t1)
+        if comm is not None:
+            comm.raise_if_failed()
+    torch.cuda.synchronize()
+    host_iso_ms = 1000.0 * min(iso)
     if comm is not None and comm.xgmi is not None:
         comm.xgmi.check()         # raises if any statistics exchange timed out
     choice_hash = tuning.table_hash()
@@ -287,6 +301,7 @@ def bench_rank(rank, world, a):
             "tune_source": tune_source,
             "kernel_choice_hash": choice_hash,
             "host_enqueue_ms_per_step": round(1000.0 * host_dt / a.steps, 3),
+            "host_ms_per_step_idle_device": round(host_iso_ms, 3),
         }
         if stock is not None:
             rec["stock_pytorch_rocm_ips_measured"] = round(stock, 1)

@@ -26,9 +26,20 @@ def family(name):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
+    ap.add_argument("--steps-only", action="store_true",
+                    help="only kernels inside the training steps (first to last synth_images_kernel "
+                         "of each process): setup-time copies / fills on library streams excluded")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
-    rows = c.execute("select pid, stream_id, stream, queue_id, queue, name from kernels").fetchall()
+    rows = c.execute("select pid, stream_id, stream, queue_id, queue, name, start from kernels").fetchall()
+    if a.steps_only:
+        win = {}
+        for pid, _sid, _sn, _qid, _qn, name, t in rows:
+            if "synth_images_kernel" in name:
+                lo, hi = win.get(pid, (t, t))
+                win[pid] = (min(lo, t), max(hi, t))
+        rows = [r for r in rows if r[0] in win and win[r[0]][0] <= r[6] <= win[r[0]][1]]
+    rows = [r[:6] for r in rows]
     per = collections.defaultdict(lambda: collections.defaultdict(lambda: {"queues": collections.Counter(),
                                                                           "fams": collections.Counter()}))
     for pid, sid, sname, qid, qname, name in rows:
@@ -43,12 +54,13 @@ def main():
             qs = ", ".join(f"{qn or qid} x{n}" for (qid, qn), n in e["queues"].most_common())
             fams = ", ".join(f"{f} x{n}" for f, n in e["fams"].most_common(6))
             print(f"  stream {sid} ({sname}): queues [{qs}]\n      kernels: {fams}")
-            for (qid, _qn) in e["queues"]:
-                q2s[qid].add(sid)
-        for qid, ss in sorted(q2s.items()):
+            for (qid, qn) in e["queues"]:
+                q2s[qn or qid].add((sid, sname))
+        for q, ss in sorted(q2s.items(), key=lambda kv: str(kv[0])):
             if len(ss) > 1:
                 bad += 1
-                print(f"  !! queue {qid} carries streams {sorted(ss)}")
+                names = ", ".join(f"{sid} ({sn})" for sid, sn in sorted(ss))
+                print(f"  !! {q} carries streams {names}")
     print("one queue per stream" if bad == 0 else f"{bad} shared queue(s)")
 
 
