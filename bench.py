@@ -136,13 +136,9 @@ def bench_rank(rank, world, a):
     else:
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
-    if OF.STREAM_PRIO:
-        # the rank runs on one high-priority stream: with the weight-gradient, SyncBN and
-        # gradient-bucket streams it gets the high-priority hardware-queue pool to itself,
-        # one queue per stream (ops/functional.py STREAM_PRIO, profiles/queues_r04.txt)
-        st = torch.cuda.Stream(device=dev, priority=OF.STREAM_PRIO)
-        st.wait_stream(torch.cuda.current_stream(dev))
-        torch.cuda.set_stream(st)
+    if not (world > 1 or rehearsal):
+        # (init_process does this for the distributed runs, before the process group exists)
+        OF.init_step_streams(dev)
     torch.manual_seed(0)
     model = build_model(a.model, num_classes=a.classes, stem=a.stem).to(dev)
     if rehearsal:

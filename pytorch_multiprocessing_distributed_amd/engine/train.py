@@ -218,13 +218,6 @@ def _run(rank, world_size, args, dev):
             raise ValueError("--dtype fp8 needs the gfx950 path (GPU)")
         from ..ops.fp8 import Fp8Scaling
         OF.set_fp8(Fp8Scaling(dev))
-    if on_gpu and OF.STREAM_PRIO:
-        # the whole rank runs on one high-priority stream, so the step's streams (this one,
-        # weight gradients, SyncBN exchange, gradient buckets) share the high-priority
-        # hardware-queue pool and never a queue (ops/functional.py STREAM_PRIO)
-        st = torch.cuda.Stream(device=dev, priority=OF.STREAM_PRIO)
-        st.wait_stream(torch.cuda.current_stream(dev))
-        torch.cuda.set_stream(st)
     cpad = 8 if on_gpu else 3
     train_loader, test_loader = build_loaders(args, rank, world_size, dev, dtype, cpad)
     if args.seed is not None:

@@ -49,6 +49,10 @@ def init_process(rank, world_size, backend="auto", device="auto", master_addr=No
         local = int(os.environ.get("LOCAL_RANK", rank))
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
+        # the step's own streams before the process group creates any (one hardware
+        # queue each: ops/functional.py init_step_streams)
+        from .ops import functional as OF
+        OF.init_step_streams(dev)
     else:
         dev = torch.device("cpu")
     kw = dict(backend=backend, rank=rank, world_size=world_size,

@@ -346,6 +346,20 @@ def _wait_weight_images():
         torch.cuda.current_stream().wait_event(ev)
 
 
+def init_step_streams(dev):
+    """Make the current stream of ``dev`` a new stream at STREAM_PRIO and create the
+    weight-gradient side stream right after it, BEFORE any communicator exists: HIP hands a
+    new stream the least-used hardware queue of its priority pool, so creating the step's
+    streams first gives each its own queue whatever streams RCCL / c10d / gloo create later
+    (profiles/queues_r04.txt).  Returns the new current stream."""
+    st = torch.cuda.Stream(device=dev, priority=STREAM_PRIO)
+    st.wait_stream(torch.cuda.current_stream(dev))
+    torch.cuda.set_stream(st)
+    if _WGRAD_STREAM["on"]:
+        _wgrad_stream(dev)
+    return st
+
+
 def set_wgrad_stream(flag: bool):
     """Run the block weight gradients on a side HIP stream (default on)."""
     _WGRAD_STREAM["on"] = bool(flag)
