@@ -1092,6 +1092,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear_dgrad", &linear_dgrad);
   m.def("linear_wgrad", &linear_wgrad);
   m.def("zero_", &zero_, "in-place zero of a contiguous GPU tensor (framework fill kernel)");
+  m.def(
+      "create_stream",
+      [](int64_t device, int64_t priority) {
+        c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, device));
+        hipStream_t s = nullptr;
+        const hipError_t e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, (int)priority);
+        TORCH_CHECK(e == hipSuccess, "hipStreamCreateWithPriority: ", hipGetErrorString(e));
+        return (int64_t) reinterpret_cast<uintptr_t>(s);
+      },
+      py::arg("device"), py::arg("priority"),
+      "a new non-blocking HIP stream (lives for the process; wrap with torch.cuda.ExternalStream): the "
+      "step's streams are created up front so each gets its own hardware queue");
   m.def("sgd_", &sgd_);
   m.def("synth_images", &synth_images);
   m.def("cifar_augment", &cifar_augment);

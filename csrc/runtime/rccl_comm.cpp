@@ -39,7 +39,8 @@ std::string RcclComm::unique_id() {
   return std::string(id.internal, sizeof(id.internal));
 }
 
-RcclComm::RcclComm(const std::string& uid, int64_t rank, int64_t world, int64_t device, int64_t priority)
+RcclComm::RcclComm(const std::string& uid, int64_t rank, int64_t world, int64_t device, int64_t priority,
+                   int64_t stream)
     : rank_(rank), world_(world), device_(device) {
   TORCH_CHECK(uid.size() == NCCL_UNIQUE_ID_BYTES, "rccl: unique id must be ", NCCL_UNIQUE_ID_BYTES,
               " bytes");
@@ -48,7 +49,12 @@ RcclComm::RcclComm(const std::string& uid, int64_t rank, int64_t world, int64_t 
   ncclUniqueId id;
   std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
   RCCL_OK(ncclCommInitRank(&comm_, (int)world, id, (int)rank));
-  HIP_OK2(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, (int)priority));
+  if (stream) {
+    stream_ = reinterpret_cast<hipStream_t>(stream);
+    owns_stream_ = false;
+  } else {
+    HIP_OK2(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, (int)priority));
+  }
   HIP_OK2(hipEventCreateWithFlags(&in_ev_, hipEventDisableTiming));
   ring_.resize(64);
   for (auto& e : ring_) HIP_OK2(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -66,7 +72,7 @@ RcclComm::~RcclComm() {
   }
   for (auto& e : ring_) (void)hipEventDestroy(e);
   if (in_ev_) (void)hipEventDestroy(in_ev_);
-  if (stream_) (void)hipStreamDestroy(stream_);
+  if (stream_ && owns_stream_) (void)hipStreamDestroy(stream_);
 }
 
 hipEvent_t RcclComm::next_event_() {
@@ -141,8 +147,9 @@ void register_rccl(pybind11::module& m) {
   namespace py = pybind11;
   py::class_<RcclComm>(m, "RcclComm")
       .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
-      .def(py::init<const std::string&, int64_t, int64_t, int64_t, int64_t>(), py::arg("unique_id"),
-           py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("priority") = 0)
+      .def(py::init<const std::string&, int64_t, int64_t, int64_t, int64_t, int64_t>(), py::arg("unique_id"),
+           py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("priority") = 0,
+           py::arg("stream") = 0)
       .def("all_reduce_", &RcclComm::all_reduce_, py::arg("tensor"), py::arg("op") = 0)
       .def("broadcast_", &RcclComm::broadcast_, py::arg("tensor"), py::arg("root") = 0)
       .def("check", &RcclComm::check)

@@ -31,7 +31,10 @@ class RcclComm {
   // 128-byte ncclUniqueId (call on ONE rank, share through the store)
   static std::string unique_id();
 
-  RcclComm(const std::string& uid, int64_t rank, int64_t world, int64_t device, int64_t priority);
+  // stream: an existing HIP stream handle to run the collectives on (the rank's step
+  // streams are created up front, ops/functional.py init_step_streams), 0 = create one
+  RcclComm(const std::string& uid, int64_t rank, int64_t world, int64_t device, int64_t priority,
+           int64_t stream = 0);
   ~RcclComm();
   RcclComm(const RcclComm&) = delete;
   RcclComm& operator=(const RcclComm&) = delete;
@@ -66,6 +69,7 @@ class RcclComm {
 
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;
+  bool owns_stream_ = true;
   hipEvent_t in_ev_ = nullptr;
   std::vector<hipEvent_t> ring_;  // done-events, reused round robin
   size_t ring_pos_ = 0;

@@ -346,18 +346,41 @@ def _wait_weight_images():
         torch.cuda.current_stream().wait_event(ev)
 
 
+_STEP_STREAMS: dict = {}
+
+
+def _new_stream(dev):
+    # a NEW HIP stream: torch.cuda.Stream(priority=...) hands out streams of torch's fixed
+    # per-priority pool (32 streams created together and spread round-robin over the hardware
+    # queues, shared with whatever else -- gloo, c10d -- draws from the pool), so two of the
+    # step's streams could land on one queue depending on the pool cursor
+    from .native import C
+    return torch.cuda.ExternalStream(C.create_stream(dev.index, STREAM_PRIO), device=dev)
+
+
 def init_step_streams(dev):
-    """Make the current stream of ``dev`` a new stream at STREAM_PRIO and create the
-    weight-gradient side stream right after it, BEFORE any communicator exists: HIP hands a
-    new stream the least-used hardware queue of its priority pool, so creating the step's
-    streams first gives each its own queue whatever streams RCCL / c10d / gloo create later
-    (profiles/queues_r04.txt).  Returns the new current stream."""
-    st = torch.cuda.Stream(device=dev, priority=STREAM_PRIO)
-    st.wait_stream(torch.cuda.current_stream(dev))
-    torch.cuda.set_stream(st)
-    if _WGRAD_STREAM["on"]:
-        _wgrad_stream(dev)
-    return st
+    """Create the rank's step streams -- main (made current), weight gradients, gradient
+    collectives (RcclComm) -- as new HIP streams at STREAM_PRIO, in that order, BEFORE any
+    communicator or torch stream pool exists: HIP hands a new stream the least-used hardware
+    queue of its priority pool, so the three take three different queues whatever is created
+    later (profiles/queues_r04.txt).  Idempotent per device.  Returns the main stream."""
+    if dev in _STEP_STREAMS:
+        torch.cuda.set_stream(_STEP_STREAMS[dev]["main"])
+        return _STEP_STREAMS[dev]["main"]
+    main = _new_stream(dev)
+    main.wait_stream(torch.cuda.current_stream(dev))
+    torch.cuda.set_stream(main)
+    side = _new_stream(dev)
+    _WGRAD_STREAM["streams"][dev] = side
+    comm = _new_stream(dev)
+    _STEP_STREAMS[dev] = {"main": main, "wgrad": side, "comm": comm}
+    return main
+
+
+def comm_stream_handle(dev) -> int:
+    """HIP handle of the pre-created gradient-collective stream of ``dev`` (0: none)."""
+    e = _STEP_STREAMS.get(torch.device(dev) if not isinstance(dev, torch.device) else dev)
+    return int(e["comm"].cuda_stream) if e else 0
 
 
 def set_wgrad_stream(flag: bool):

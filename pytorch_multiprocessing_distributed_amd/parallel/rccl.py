@@ -58,8 +58,9 @@ def _store():
     return c10d._get_default_store()
 
 
-def create(group=None, priority: int = 0, store=None):
-    """Collective over ``group`` (every rank calls it).  Returns ``_C.RcclComm``."""
+def create(group=None, priority: int = 0, store=None, stream: int = 0):
+    """Collective over ``group`` (every rank calls it).  Returns ``_C.RcclComm``.
+    ``stream``: HIP handle of an existing stream to run on (0: the communicator creates one)."""
     from ..ops.native import C
     if not dist.is_initialized():
         raise RuntimeError("torch.distributed must be initialised first (it hosts the TCPStore)")
@@ -71,7 +72,7 @@ def create(group=None, priority: int = 0, store=None):
         store.set(key, C.RcclComm.unique_id())
     uid = store.get(key)                      # blocks until rank 0 published it
     dev = torch.cuda.current_device()
-    comm = C.RcclComm(bytes(uid), rank, world, dev, priority)
+    comm = C.RcclComm(bytes(uid), rank, world, dev, priority, stream)
     return register(comm)
 
 
