@@ -109,6 +109,9 @@ __device__ __forceinline__ void wait_vmcnt() {
 #ifndef PMD_CONV_ST_PASS
 #define PMD_CONV_ST_PASS 0
 #endif
+#ifndef PMD_CONV_SETPRIO
+#define PMD_CONV_SETPRIO 0
+#endif
 #ifndef PMD_CONV_MINB4
 #define PMD_CONV_MINB4 2  // __launch_bounds__ min blocks per CU of the 4-wave tiles (VGPR cap A/B knob)
 #endif
@@ -621,12 +624,16 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) vo
           af[i] = __builtin_bit_cast(bf16x8, pack8(v));
         }
       }
+      // PMD_CONV_SETPRIO (A/B knob): raise the wave's issue priority around the MFMA cluster
+      // (cdna_hip_programming.md T5: keeps hipcc from moving MFMAs in among the loads)
+      if constexpr (PMD_CONV_SETPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j)
           acc[i][j] = SWAPC ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0)
                             : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+      if constexpr (PMD_CONV_SETPRIO) __builtin_amdgcn_s_setprio(0);
     }
   };
 

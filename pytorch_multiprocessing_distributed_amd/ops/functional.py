@@ -349,13 +349,13 @@ def _wait_weight_images():
 _STEP_STREAMS: dict = {}
 
 
-def _new_stream(dev):
+def _new_stream(dev, prio=None):
     # a NEW HIP stream: torch.cuda.Stream(priority=...) hands out streams of torch's fixed
     # per-priority pool (32 streams created together and spread round-robin over the hardware
     # queues, shared with whatever else -- gloo, c10d -- draws from the pool), so two of the
     # step's streams could land on one queue depending on the pool cursor
     from .native import C
-    return torch.cuda.ExternalStream(C.create_stream(dev.index, STREAM_PRIO), device=dev)
+    return torch.cuda.ExternalStream(C.create_stream(dev.index, STREAM_PRIO if prio is None else prio), device=dev)
 
 
 def init_step_streams(dev):
@@ -370,7 +370,7 @@ def init_step_streams(dev):
     main = _new_stream(dev)
     main.wait_stream(torch.cuda.current_stream(dev))
     torch.cuda.set_stream(main)
-    side = _new_stream(dev)
+    side = _new_stream(dev, int(os.environ.get("PMD_WGRAD_PRIO", STREAM_PRIO)))
     _WGRAD_STREAM["streams"][dev] = side
     comm = _new_stream(dev)
     _STEP_STREAMS[dev] = {"main": main, "wgrad": side, "comm": comm}
