@@ -109,6 +109,9 @@ __device__ __forceinline__ void wait_vmcnt() {
 #ifndef PMD_CONV_ST_PASS
 #define PMD_CONV_ST_PASS 0
 #endif
+#ifndef PMD_F8_MINB
+#define PMD_F8_MINB 2  // min blocks per CU of the single-stage fp8 dgrad (4: 128-VGPR cap, 4 waves/SIMD)
+#endif
 #ifndef PMD_CONV_SETPRIO
 #define PMD_CONV_SETPRIO 0
 #endif
@@ -153,7 +156,8 @@ __device__ __forceinline__ int swz(int row) {
 template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA, bool MF32 = false,
           int WM = 2, int WN = 2, bool P8 = false, bool HALO = false, int NB = 2, bool F8 = false,
           int NST1 = 0, bool PRO = false>
-__global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? PMD_CONV_MINB4 : 2) void conv_igemm_kernel(ConvArgs a) {
+__global__ __launch_bounds__(64 * WM * WN, (F8 && NST1) ? PMD_F8_MINB : (WM * WN == 4 ? PMD_CONV_MINB4 : 2))
+    void conv_igemm_kernel(ConvArgs a) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   static_assert(DMA || (BK == 64 && NST == 2 && NW == 4), "register staging: BK=64, 2 stages, 4 waves");
   // F8: fp8 operands (1 B per element) in the same 128-B LDS rows (BK = 64 bf16 slots =
