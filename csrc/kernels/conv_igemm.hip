@@ -110,7 +110,10 @@ __device__ __forceinline__ void wait_vmcnt() {
 #define PMD_CONV_ST_PASS 0
 #endif
 #ifndef PMD_F8_MINB
-#define PMD_F8_MINB 2  // min blocks per CU of the single-stage fp8 dgrad (4: 128-VGPR cap, 4 waves/SIMD)
+// min blocks per CU of the single-stage fp8 dgrad with 0 / 1 fused BN-reduce sets: 4 = the
+// 128-VGPR cap (4 waves/SIMD; no spills with one B fragment held, NJ = 1); the 2-set
+// instantiation spills at that cap and keeps 2 (158 VGPRs, 3 waves/SIMD, NJ = NI)
+#define PMD_F8_MINB 4
 #endif
 #ifndef PMD_CONV_SETPRIO
 #define PMD_CONV_SETPRIO 0
@@ -156,7 +159,8 @@ __device__ __forceinline__ int swz(int row) {
 template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA, bool MF32 = false,
           int WM = 2, int WN = 2, bool P8 = false, bool HALO = false, int NB = 2, bool F8 = false,
           int NST1 = 0, bool PRO = false>
-__global__ __launch_bounds__(64 * WM * WN, (F8 && NST1) ? PMD_F8_MINB : (WM * WN == 4 ? PMD_CONV_MINB4 : 2))
+__global__ __launch_bounds__(64 * WM * WN,
+                             (F8 && NST1 && NB < 2) ? PMD_F8_MINB : (WM * WN == 4 ? PMD_CONV_MINB4 : 2))
     void conv_igemm_kernel(ConvArgs a) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   static_assert(DMA || (BK == 64 && NST == 2 && NW == 4), "register staging: BK=64, 2 stages, 4 waves");
@@ -531,14 +535,15 @@ __global__ __launch_bounds__(64 * WM * WN, (F8 && NST1) ? PMD_F8_MINB : (WM * WN
       if constexpr (NST1) {
         // single-stage (short-reduction, epilogue-bound) variant: NJ B fragments and ONE A
         // fragment live at a time, i.e. every A fragment is read NI / NJ times from LDS.
-        // NJ = NI (default) reads each fragment once: the fused-epilogue instantiation
-        // (128x128, 2 BN sets) compiles to 152 VGPRs at NJ = 1 or 2 and 158 at NJ = 4 --
-        // 3 waves per SIMD in every case (the epilogue, not the held fragments, sets the
-        // register peak), so the re-reads bought no occupancy
+        // With 2 fused BN sets the 128x128 instantiation compiles to 152 VGPRs at NJ = 1 or 2
+        // and 158 at NJ = 4 -- 3 waves per SIMD in every case (the epilogue sets the peak), so
+        // it reads each fragment once (NJ = NI).  With 0 / 1 sets NJ = 1 fits the 128-VGPR cap
+        // of 4 waves per SIMD without spills (PMD_F8_MINB, at the kernel template)
 #ifndef PMD_F8_NJ
 #define PMD_F8_NJ 4
 #endif
-        constexpr int NJ = PMD_F8_NJ < NI ? PMD_F8_NJ : NI;
+        constexpr int NJW = (NB < 2 && PMD_F8_MINB >= 4) ? 1 : PMD_F8_NJ;
+        constexpr int NJ = NJW < NI ? NJW : NI;
         static_assert(NI % NJ == 0, "NJ divides NI");
 #pragma unroll
         for (int j0 = 0; j0 < NI; j0 += NJ) {
