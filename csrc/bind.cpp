@@ -912,6 +912,8 @@ Tensor fp8_mfma_probe(Tensor A, Tensor Bt) {
 }
 
 // sx, sw: device scalars the operands were quantised with (y = conv(xq, wq) / (sx * sw))
+static int g_fp8_fwd_impl = -1;  // -1: PMD_FP8_FWD_IMPL (default 0)
+
 std::vector<Tensor> conv_fp8_fwd(Tensor xq, Tensor wq, Tensor sx, Tensor sw, int64_t stride, int64_t pad,
                                  bool want_stats, c10::optional<Tensor> stats_buf,
                                  c10::optional<Tensor> shift) {
@@ -932,11 +934,26 @@ std::vector<Tensor> conv_fp8_fwd(Tensor xq, Tensor wq, Tensor sx, Tensor sw, int
       stats = pmd_zeros({pmd_slots(), 2, K}, xq.options().dtype(torch::kFloat32));
     }
   }
-  CHECK_RC(pmd::conv_fp8_fwd_launch(xq.data_ptr<uint8_t>(), wq.data_ptr<uint8_t>(), bfp_mut(y),
-                                    want_stats ? stats.data_ptr<float>() : nullptr,
-                                    sx.data_ptr<float>(), sw.data_ptr<float>(), N, H, W, C, P, Q, K, R, S,
-                                    (int)stride, (int)pad, cur_stream(), shift_ptr(shift, K)),
-           "conv_fp8_fwd");
+  // implementation: 0 = conv_fp8_fwd_kernel (fp8.hip), 1 = the implicit-GEMM kernel's fp8 path
+  static int impl = -1;
+  if (impl < 0) {
+    const char* e = getenv("PMD_FP8_FWD_IMPL");
+    impl = (e && e[0] == '1') ? 1 : 0;
+  }
+  if (g_fp8_fwd_impl >= 0) impl = g_fp8_fwd_impl;
+  if (impl == 1) {
+    CHECK_RC(pmd::conv_fwd_fp8_igemm_launch(xq.data_ptr<uint8_t>(), wq.data_ptr<uint8_t>(), bfp_mut(y),
+                                            want_stats ? stats.data_ptr<float>() : nullptr,
+                                            sx.data_ptr<float>(), sw.data_ptr<float>(), N, H, W, C, P, Q, K, R,
+                                            S, (int)stride, (int)pad, cur_stream(), shift_ptr(shift, K)),
+             "conv_fp8_fwd (igemm)");
+  } else {
+    CHECK_RC(pmd::conv_fp8_fwd_launch(xq.data_ptr<uint8_t>(), wq.data_ptr<uint8_t>(), bfp_mut(y),
+                                      want_stats ? stats.data_ptr<float>() : nullptr,
+                                      sx.data_ptr<float>(), sw.data_ptr<float>(), N, H, W, C, P, Q, K, R, S,
+                                      (int)stride, (int)pad, cur_stream(), shift_ptr(shift, K)),
+             "conv_fp8_fwd");
+  }
   if (want_stats) return {y, stats};
   return {y};
 }
@@ -1024,6 +1041,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "streaming 1x1 conv: 0 off, 1 data gradients, 2 data gradients + forwards");
   m.def("conv1x1_policy", &pmd::conv1x1_policy);
   m.def("conv1x1_launches", &pmd::conv1x1_launches);
+  m.def("conv_fp8_fwd_set_impl", [](int64_t i) { g_fp8_fwd_impl = (int)i; },
+        "fp8 forward conv kernel: 0 conv_fp8_fwd_kernel, 1 the implicit-GEMM kernel's fp8 path, -1 env");
   m.def("conv1x1_stream_bn", &pmd::conv1x1_stream_bn,
         "column tile the streaming 1x1 conv picks for (reduction, out channels, epilogue tensors, masks); 0 = ineligible");
   m.def("conv1x1_set_bn", &pmd::conv1x1_set_bn, "streaming 1x1 conv column tile: 64 / 128, 0 = auto");

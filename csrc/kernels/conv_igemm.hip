@@ -1761,6 +1761,54 @@ static void launch_f8(const ConvArgs& a, hipStream_t st) {
 #undef F8K
 }
 
+// fp8 FORWARD on the same implicit-GEMM kernel (the e4m3 x e4m3 path of conv_igemm_kernel<...,
+// F8>: swz_f8 LDS layout, XCD remap, the bf16 kernel's statistics epilogue) -- an alternative
+// to conv_fp8_fwd_kernel (fp8.hip) selected by conv_fp8_fwd_set_impl / PMD_FP8_FWD_IMPL.
+template <int BM, int BN, bool ONE, bool STATS>
+static void launch_f8_fwd(const ConvArgs& a, hipStream_t st) {
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.Nout + BN - 1) / BN);
+  hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, 64, 2, false, STATS, true, false, 2, 2, false, false, 0, true,
+                                        ONE ? 1 : 0>), dim3(tiles, 1, 1), dim3(256), 0, st, a);
+}
+int conv_fwd_fp8_igemm_launch(const uint8_t* xq, const uint8_t* wq, bf16_t* out, float* stats, const float* sx,
+                              const float* sw, int N, int H, int W, int Cs, int OH, int OW, int Nout, int R, int S,
+                              int stride, int pad, hipStream_t st, const float* shift) {
+  if (Cs % 16 != 0 || (Cs & (Cs - 1)) != 0) return 1;  // a 16-B chunk = 16 channels of one tap
+  if (Nout % 8 != 0) return 2;
+  if (stride != 1 && stride != 2) return 3;
+  ConvArgs a{};
+  a.batch = 1;
+  a.src = reinterpret_cast<const bf16_t*>(xq);
+  a.wt = reinterpret_cast<const bf16_t*>(wq);
+  a.out = out;
+  a.stats = stats;
+  a.shift = stats ? shift : nullptr;
+  a.N = N; a.H = H; a.W = W; a.Cs = Cs; a.log2Cs = ilog2(Cs);
+  a.OH = OH; a.OW = OW; a.Nout = Nout; a.R = R; a.S = S;
+  a.stride = stride; a.log2stride = ilog2(stride); a.pad = pad;
+  const long long M = (long long)N * OH * OW;
+  if (M >= (1ll << 31) || (long long)N * H * W >= (1ll << 31)) return 4;
+  a.M = (int)M;
+  a.Kg = R * S * Cs;
+  a.f8_sa = sx;
+  a.f8_sb = sw;
+  const bool one = a.Kg <= 512;
+#define F8F(BMV, BNV)                                              \
+  do {                                                             \
+    if (one) {                                                     \
+      if (stats) launch_f8_fwd<BMV, BNV, true, true>(a, st);       \
+      else launch_f8_fwd<BMV, BNV, true, false>(a, st);            \
+    } else {                                                       \
+      if (stats) launch_f8_fwd<BMV, BNV, false, true>(a, st);      \
+      else launch_f8_fwd<BMV, BNV, false, false>(a, st);           \
+    }                                                              \
+  } while (0)
+  if (a.Nout <= 64) F8F(128, 64);
+  else F8F(128, 128);
+#undef F8F
+  return 0;
+}
+
 int conv_dgrad_fp8_launch(const uint8_t* dyq, const uint8_t* wtq, const float* sdy, const float* sw, bf16_t* out,
                           int N, int H, int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
                           const bf16_t* addend, const uint8_t* addend_mask, const BnReduceArgs* bnr,

@@ -178,6 +178,9 @@ int dequant_fp8_launch(const uint8_t* q, float* out, const float* inv_scale, lon
                        bool bf8 = false);
 int fp8_mfma_probe_launch(const uint8_t* A, const uint8_t* Bt, float* C, hipStream_t st);
 // y(bf16) = conv(xq, wq) / (sx * sw) with e4m3 NHWC input / KRSC weight; optional BN stats slots
+int conv_fwd_fp8_igemm_launch(const uint8_t* xq, const uint8_t* wq, bf16_t* out, float* stats, const float* sx,
+                              const float* sw, int N, int H, int W, int Cs, int OH, int OW, int Nout, int R, int S,
+                              int stride, int pad, hipStream_t st, const float* shift);
 int conv_fp8_fwd_launch(const uint8_t* x, const uint8_t* w, bf16_t* out, float* stats, const float* sx,
                         const float* sw, int N, int H, int W, int C, int OH, int OW, int K, int R,
                         int S, int stride, int pad, hipStream_t st, const float* shift = nullptr);

@@ -65,8 +65,19 @@ def test_bn_apply_fp8_copy_saturates():
                                    (256, 56, 128, 1, 1), (128, 28, 128, 3, 2), (512, 7, 2048, 1, 1),
                                    (256, 14, 256, 3, 1)],
                          ids=lambda s: "C%d_H%d_K%d_R%d_s%d" % s)
-def test_conv_fp8_fwd(shape):
+@pytest.mark.parametrize("impl", [0, 1], ids=["fp8kernel", "igemm"])
+def test_conv_fp8_fwd(shape, impl):
+    """conv_fp8_fwd on both implementations: conv_fp8_fwd_kernel (fp8.hip) and the
+    implicit-GEMM kernel's e4m3 path (conv_igemm_kernel<..., F8>, PMD_FP8_FWD_IMPL=1)."""
     C = _C()
+    C.conv_fp8_fwd_set_impl(impl)
+    try:
+        _conv_fp8_fwd_case(C, shape)
+    finally:
+        C.conv_fp8_fwd_set_impl(-1)
+
+
+def _conv_fp8_fwd_case(C, shape):
     torch.manual_seed(0)
     Cin, H, K, R, st = shape
     pad = R // 2
