@@ -912,7 +912,7 @@ Tensor fp8_mfma_probe(Tensor A, Tensor Bt) {
 }
 
 // sx, sw: device scalars the operands were quantised with (y = conv(xq, wq) / (sx * sw))
-static int g_fp8_fwd_impl = -1;  // -1: PMD_FP8_FWD_IMPL (default 0)
+static int g_fp8_fwd_impl = -1;  // -1: PMD_FP8_FWD_IMPL (default 1)
 
 std::vector<Tensor> conv_fp8_fwd(Tensor xq, Tensor wq, Tensor sx, Tensor sw, int64_t stride, int64_t pad,
                                  bool want_stats, c10::optional<Tensor> stats_buf,
@@ -934,11 +934,12 @@ std::vector<Tensor> conv_fp8_fwd(Tensor xq, Tensor wq, Tensor sx, Tensor sw, int
       stats = pmd_zeros({pmd_slots(), 2, K}, xq.options().dtype(torch::kFloat32));
     }
   }
-  // implementation: 0 = conv_fp8_fwd_kernel (fp8.hip), 1 = the implicit-GEMM kernel's fp8 path
+  // implementation: 1 (default) = the implicit-GEMM kernel's fp8 path, 0 = conv_fp8_fwd_kernel
+  // (fp8.hip); the igemm path measured +2.5% on the fp8 step (16.87-16.96 vs 17.31-17.40 ms)
   static int impl = -1;
   if (impl < 0) {
     const char* e = getenv("PMD_FP8_FWD_IMPL");
-    impl = (e && e[0] == '1') ? 1 : 0;
+    impl = (e && e[0] == '0') ? 0 : 1;
   }
   if (g_fp8_fwd_impl >= 0) impl = g_fp8_fwd_impl;
   if (impl == 1) {
@@ -1042,7 +1043,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_policy", &pmd::conv1x1_policy);
   m.def("conv1x1_launches", &pmd::conv1x1_launches);
   m.def("conv_fp8_fwd_set_impl", [](int64_t i) { g_fp8_fwd_impl = (int)i; },
-        "fp8 forward conv kernel: 0 conv_fp8_fwd_kernel, 1 the implicit-GEMM kernel's fp8 path, -1 env");
+        "fp8 forward conv kernel: 0 conv_fp8_fwd_kernel, 1 the implicit-GEMM kernel's fp8 path (default), -1 env");
   m.def("conv1x1_stream_bn", &pmd::conv1x1_stream_bn,
         "column tile the streaming 1x1 conv picks for (reduction, out channels, epilogue tensors, masks); 0 = ineligible");
   m.def("conv1x1_set_bn", &pmd::conv1x1_set_bn, "streaming 1x1 conv column tile: 64 / 128, 0 = auto");
