@@ -1451,6 +1451,10 @@ template <bool DGRAD, bool STATS>
 static void launch_choice(int c, const ConvArgs& a, hipStream_t st) {
   if ((c == 11 || c == 12) && halo_ok(a)) {
     launch_halo<DGRAD, STATS>(a, st, c == 12 ? 3 : 2);
+  } else if (c == 13 && a.Cs % 64 == 0) {
+    // 32x32x16 MFMA on the 128-row LDS-DMA tile (BK = 64, uniform-tap loader)
+    if (a.Nout <= 64) launch_k<128, 64, 64, 2, DGRAD, STATS, true, true>(a, st);
+    else launch_k<128, 128, 64, 2, DGRAD, STATS, true, true>(a, st);
   } else if (c == 10 && a.Nout > 64) {
     launch_k<64, 128, 32, 2, DGRAD, STATS, true>(a, st);
   } else if (c >= 6 && c <= 9 && p8_ok(c - 6, a)) {
@@ -1568,9 +1572,15 @@ static int tune(const ConvArgs& a0, hipStream_t st) {
   // (profiles/conv_p8_r02.txt): forced-policy only, not timed by the tuner
   // (10, the 64x128 tile, measured slower than 0..5 on every short-K dgrad --
   // profiles/dgrad_epi_r02_tile10.txt -- so it is a forced policy only)
-  for (int c : {0, 1, 2, 3, 4, 5}) {
+  static int tune_mf32 = -1;  // PMD_TUNE_MF32=1: also time the 32x32x16 MFMA tile (candidate 13)
+  if (tune_mf32 < 0) {
+    const char* e = getenv("PMD_TUNE_MF32");
+    tune_mf32 = (e && e[0] == '1') ? 1 : 0;
+  }
+  for (int c : {0, 1, 2, 3, 4, 5, 13}) {
     if ((c == 2 && !(big_ok(a) && a.Nout >= 256)) || (c == 3 && !big_ok(a)) || (c == 4 && a.Nout <= 64) ||
-        (c == 5 && (DGRAD || a.Cs < 64)) || (c == 10 && a.Nout <= 64))
+        (c == 5 && (DGRAD || a.Cs < 64)) || (c == 10 && a.Nout <= 64) ||
+        (c == 13 && (!tune_mf32 || a.Cs % 64 != 0)))
       continue;
     launch_choice<DGRAD, STATS>(c, a, st);  // warm (code object load, caches)
     float t = 1e30f;
