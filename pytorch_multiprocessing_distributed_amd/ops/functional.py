@@ -377,8 +377,13 @@ def init_step_streams(dev):
     return main
 
 
-def comm_stream_handle(dev) -> int:
-    """HIP handle of the pre-created gradient-collective stream of ``dev`` (0: none)."""
+def comm_stream_handle(dev=None) -> int:
+    """HIP handle of the pre-created gradient-collective stream of ``dev`` (default: the
+    current device; 0: none was created)."""
+    if not _STEP_STREAMS:
+        return 0
+    if dev is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
     e = _STEP_STREAMS.get(torch.device(dev) if not isinstance(dev, torch.device) else dev)
     return int(e["comm"].cuda_stream) if e else 0
 

@@ -139,8 +139,7 @@ def resolve_transport(comm, module, reducer="native", transport="auto", verbose=
     c, err = None, ""
     try:
         from ..ops.functional import STREAM_PRIO, comm_stream_handle
-        c = rccl.create(comm.group, priority=STREAM_PRIO,
-                        stream=comm_stream_handle(torch.device("cuda", torch.cuda.current_device())))
+        c = rccl.create(comm.group, priority=STREAM_PRIO, stream=comm_stream_handle())
     except Exception as e:  # noqa: BLE001
         err = str(e)
     ok = rccl.self_test(c, comm.group) if c is not None else False

@@ -374,3 +374,24 @@ def test_bench_two_ranks_gloo_same_device():
     rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2-same-gpu-gloo"
     assert rec["config"]["syncbn_comm"] == "xgmi" and rec["value"] > 0
+
+
+@pytest.mark.parametrize("comm", ["auto", "c10d"])
+def test_bench_dp_rehearsal_production_step(comm):
+    """bench.py --dp_rehearsal: the production W>1 per-rank step on one GPU (DataParallel
+    over a single-rank RCCL group, native reducer, bucket all-reduces on the native RcclComm
+    -- or c10d --, SyncBN through the xGMI kernel) runs, reports itself as such, and its
+    loss is finite."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--dp_rehearsal", "--comm", comm,
+           "--steps", "3", "--warmup", "2", "--batch", "16", "--image", "64", "--bucket_mb", "4"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    cfg = rec["config"]
+    assert rec["n_gpus"] == 1 and cfg["parallelism"] == "dp1-rehearsal"
+    assert cfg["sync_bn"] is True and cfg["syncbn_comm"] == "xgmi"
+    assert cfg["grad_transport"] == ("rccl" if comm == "auto" else "c10d")
+    assert len(cfg["grad_buckets_mb"]) >= 2
+    assert rec["final_loss"] == rec["final_loss"] and rec["value"] > 0
+    if comm == "auto":
+        assert "exact self-test passed" in r.stdout

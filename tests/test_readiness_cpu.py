@@ -105,7 +105,7 @@ def test_auto_transport_selection(monkeypatch, bn_sync_guard, capsys):
     m = build_model("resnet50", num_classes=10, stem="imagenet")
     made = []
 
-    def create(group=None, priority=0, store=None):
+    def create(group=None, priority=0, store=None, stream=0):
         c = _Native()
         made.append(c)
         return c
