@@ -110,7 +110,8 @@ __device__ __forceinline__ void wait_vmcnt() {
 #define PMD_CONV_ST_PASS 0
 #endif
 #ifndef PMD_TIMING_NO_ATOMICS
-#define PMD_TIMING_NO_ATOMICS 0  // 1: drop the BN statistics / fused-reduce atomics (WRONG numerics; timing A/B only)
+#define PMD_TIMING_NO_ATOMICS 0  // bit 0 / 1: drop the forward BN statistics / the dgrad fused-reduce atomics
+                                 // (WRONG numerics; timing A/B only)
 #endif
 #ifndef PMD_F8_MINB
 // min blocks per CU of the single-stage fp8 dgrad with 0 / 1 fused BN-reduce sets: 4 = the
@@ -1003,7 +1004,7 @@ __global__ __launch_bounds__(64 * WM * WN,
         float v = 0.f;
 #pragma unroll
         for (int w = 0; w < WM; ++w) v += st[(w * 2 + which) * BN + col];
-        if constexpr (!PMD_TIMING_NO_ATOMICS)  // timing-only A/B knob: what the statistics atomics cost
+        if constexpr (!(PMD_TIMING_NO_ATOMICS & 1))  // timing-only A/B knob: what the statistics atomics cost
           atomicAdd(a.stats + ((size_t)((m0 / BM) % kStatSlots) * 2 + which) * a.Nout + n0 + col, v);
       }
     }
@@ -1183,7 +1184,7 @@ __global__ __launch_bounds__(64 * WM * WN,
         float acc2 = 0.f;
         for (int r = col; r < NT; r += CPR) acc2 += part[r * PSTR + k];
         const int n = n0 + col * 8 + (k & 7);
-        if (n < a.Nout && !PMD_TIMING_NO_ATOMICS)
+        if (n < a.Nout && !(PMD_TIMING_NO_ATOMICS & 2))
           atomicAdd(a.bn_red[t] + ((size_t)((m0 / BM) % kStatSlots) * 2 + (k >> 3)) * a.Nout + n, acc2);
       }
       __syncthreads();
