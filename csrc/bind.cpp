@@ -1042,8 +1042,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "streaming 1x1 conv: 0 off, 1 data gradients, 2 data gradients + forwards");
   m.def("conv1x1_policy", &pmd::conv1x1_policy);
   m.def("conv1x1_launches", &pmd::conv1x1_launches);
-  m.def("conv_set_fwd_tpb", &pmd::conv_set_fwd_tpb,
-        "row tiles per workgroup of the forward convs with BN statistics (statistics added once per workgroup)");
   m.def("conv_fp8_fwd_set_impl", [](int64_t i) { g_fp8_fwd_impl = (int)i; },
         "fp8 forward conv kernel: 0 conv_fp8_fwd_kernel, 1 the implicit-GEMM kernel's fp8 path (default), -1 env");
   m.def("conv1x1_stream_bn", &pmd::conv1x1_stream_bn,

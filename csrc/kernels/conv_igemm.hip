@@ -69,10 +69,6 @@ struct ConvArgs {
   // producing conv and the A operand is relu(y * scale + shift) per input channel, with
   // (scale, shift) rows 2 and 3 of this [4][Cs] BN parameter block
   const float* pro_p;
-  // row tiles per workgroup (<= 1: one).  A forward with BN statistics walks tpb row tiles
-  // of one column tile and adds its statistics ONCE, after the last (tpb x fewer atomic
-  // bytes and per-tile LDS combines; launch_k, PMD_FWD_TPB)
-  int tpb;
 };
 typedef __attribute__((ext_vector_type(8))) int i32x8_c;
 
@@ -281,35 +277,13 @@ __global__ __launch_bounds__(64 * WM * WN,
   const int hw_out = a.OH * a.OW;
   const int halo_T = HALO ? (hw_out + BM - 1) / BM : 1;  // HALO: M tiles never straddle images
   const int tilesM = HALO ? a.N * halo_T : (Mgrid + BM - 1) / BM;  // grid.x sized for the largest phase
-  const int TPBr = a.tpb > 1 ? a.tpb : 1;
-  const int tilesMB = (tilesM + TPBr - 1) / TPBr;
-  const int L = xcd_remap(blockIdx.x, tilesMB * tilesN);
-  const int n0 = (L % tilesN) * BN;
-  const int Mp_all = Mp;
-  // epilogue constants and the BN-statistics accumulators, which span the row tiles
-  bf16_t* Cs = lds;
-  const int crow0 = wm * (BM / WM) + (lane >> 4) * 4;
-  const int ccol0 = wn * (BN / WN) + (lane & 15);
-  constexpr int NI2F = MF32 ? BN / (32 * WN) : 1;  // 32x32 column tiles per wave (MF32)
-  float csum[NI], csq[NI], cshift[NI];
-#pragma unroll
-  for (int j = 0; j < NI; ++j) {
-    csum[j] = 0.f;
-    csq[j] = 0.f;
-    cshift[j] = 0.f;
-    if (STATS && a.shift) {
-      const int col = n0 + (MF32 ? wn * (BN / WN) + j * 32 + (lane & 31) : ccol0 + j * 16);
-      if ((!MF32 || j < NI2F) && col < a.Nout) cshift[j] = a.shift[col];
-    }
-  }
-  for (int tb = 0; tb < TPBr; ++tb) {  // row tiles of this workgroup (one unless a.tpb > 1)
-  const int mt = (L / tilesN) * TPBr + tb;
-  if (mt >= tilesM) break;  // uniform per block
+  const int L = xcd_remap(blockIdx.x, tilesM * tilesN);
+  const int mt = L / tilesN;
   const int halo_img = HALO ? mt / halo_T : 0, halo_t = HALO ? mt - (mt / halo_T) * halo_T : 0;
   const int m0 = HALO ? halo_img * hw_out + halo_t * BM : mt * BM;
-  Mp = Mp_all;
+  const int n0 = (L % tilesN) * BN;
   if (HALO) Mp = m0 + min(BM, hw_out - halo_t * BM);  // rows of this image only
-  if (m0 >= Mp) break;  // uniform per block, before any barrier
+  if (m0 >= Mp) return;  // uniform per block, before any barrier
   if constexpr (PRO) {
     // published by the pipeline's first barrier (its s_waitcnt lgkmcnt(0) covers these writes)
     for (int c = threadIdx.x; c < a.Cs; c += 64 * WM * WN) {
@@ -927,7 +901,21 @@ __global__ __launch_bounds__(64 * WM * WN,
     }
   }
 
-  // ---- epilogue (Cs, crow0, ccol0 and the statistics accumulators: above the row-tile loop)
+  // ---- epilogue
+  bf16_t* Cs = lds;
+  const int crow0 = wm * (BM / WM) + (lane >> 4) * 4;
+  const int ccol0 = wn * (BN / WN) + (lane & 15);
+  float csum[NI], csq[NI], cshift[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    csum[j] = 0.f;
+    csq[j] = 0.f;
+    cshift[j] = 0.f;
+    if (STATS && a.shift) {
+      const int col = n0 + (MF32 ? wn * (BN / WN) + j * 32 + (lane & 31) : ccol0 + j * 16);
+      if ((!MF32 || j < NI2) && col < a.Nout) cshift[j] = a.shift[col];
+    }
+  }
   if constexpr (MF32) {
     // 32x32 C layout: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
 #pragma unroll
@@ -978,7 +966,49 @@ __global__ __launch_bounds__(64 * WM * WN,
           }
         }
   }
-  __syncthreads();  // the C tile is staged (its statistics are added after the last row tile)
+  if (STATS && MF32) {
+    // column sums: lanes l and l+32 hold the two row halves of column l & 31
+    float* st = reinterpret_cast<float*>(smem + SMEM);  // [WM][2][BN]
+#pragma unroll
+    for (int j = 0; j < NI2; ++j) {
+      float s1 = csum[j], s2 = csq[j];
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (lane < 32) {
+        st[(wm * 2 + 0) * BN + wn * (BN / WN) + j * 32 + lane] = s1;
+        st[(wm * 2 + 1) * BN + wn * (BN / WN) + j * 32 + lane] = s2;
+      }
+    }
+  }
+  if (STATS && !MF32) {
+    float* st = reinterpret_cast<float*>(smem + SMEM);  // [WM][2][BN]
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      float s1 = csum[j], s2 = csq[j];
+      s1 += __shfl_xor(s1, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (lane < 16) {
+        st[(wm * 2 + 0) * BN + ccol0 + j * 16] = s1;
+        st[(wm * 2 + 1) * BN + ccol0 + j * 16] = s2;
+      }
+    }
+  }
+  __syncthreads();
+  if (STATS) {
+    const float* st = reinterpret_cast<const float*>(smem + SMEM);
+    for (int c = tid; c < 2 * BN; c += NT) {
+      const int which = c / BN, col = c % BN;
+      if (n0 + col < a.Nout) {
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) v += st[(w * 2 + which) * BN + col];
+        if constexpr (!(PMD_TIMING_NO_ATOMICS & 1))  // timing-only A/B knob: what the statistics atomics cost
+          atomicAdd(a.stats + ((size_t)((m0 / BM) % kStatSlots) * 2 + which) * a.Nout + n0 + col, v);
+      }
+    }
+  }
   constexpr int CPR = BN / 8;  // 16-B chunks per output row
   // fused BN-backward reduce: each thread owns one 8-channel chunk column (NT % CPR == 0)
   static_assert(NT % CPR == 0, "chunk column per thread");
@@ -1160,55 +1190,6 @@ __global__ __launch_bounds__(64 * WM * WN,
       __syncthreads();
     }
   }
-  if (TPBr > 1) __syncthreads();  // the next row tile's loads overwrite the staged C tile
-  }  // row tiles
-  // ---- BN statistics of this workgroup's row tiles: per-column sums over the tiles' rows,
-  //      combined across the waves through LDS, one atomic add per channel and workgroup
-  if constexpr (STATS) {
-    if (MF32) {
-      // column sums: lanes l and l+32 hold the two row halves of column l & 31
-      float* st = reinterpret_cast<float*>(smem + SMEM);  // [WM][2][BN]
-#pragma unroll
-      for (int j = 0; j < NI2F; ++j) {
-        float s1 = csum[j], s2 = csq[j];
-        s1 += __shfl_xor(s1, 32, 64);
-        s2 += __shfl_xor(s2, 32, 64);
-        if (lane < 32) {
-          st[(wm * 2 + 0) * BN + wn * (BN / WN) + j * 32 + lane] = s1;
-          st[(wm * 2 + 1) * BN + wn * (BN / WN) + j * 32 + lane] = s2;
-        }
-      }
-    }
-    if (!MF32) {
-      float* st = reinterpret_cast<float*>(smem + SMEM);  // [WM][2][BN]
-#pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        float s1 = csum[j], s2 = csq[j];
-        s1 += __shfl_xor(s1, 16, 64);
-        s1 += __shfl_xor(s1, 32, 64);
-        s2 += __shfl_xor(s2, 16, 64);
-        s2 += __shfl_xor(s2, 32, 64);
-        if (lane < 16) {
-          st[(wm * 2 + 0) * BN + ccol0 + j * 16] = s1;
-          st[(wm * 2 + 1) * BN + ccol0 + j * 16] = s2;
-        }
-      }
-    }
-    __syncthreads();
-    {
-      const float* st = reinterpret_cast<const float*>(smem + SMEM);
-      for (int c = tid; c < 2 * BN; c += NT) {
-        const int which = c / BN, col = c % BN;
-        if (n0 + col < a.Nout) {
-          float v = 0.f;
-#pragma unroll
-          for (int w = 0; w < WM; ++w) v += st[(w * 2 + which) * BN + col];
-          if constexpr (!(PMD_TIMING_NO_ATOMICS & 1))  // timing-only A/B knob: what the statistics atomics cost
-            atomicAdd(a.stats + ((size_t)(((L / tilesN) * TPBr) % kStatSlots) * 2 + which) * a.Nout + n0 + col, v);
-        }
-      }
-    }
-  }
 }
 
 // fp32 param (physical K,R,S,C = channels_last [K,C,R,S]) -> bf16 images:
@@ -1320,28 +1301,13 @@ static int conv_impl() {
   return g_conv_impl;
 }
 
-// row tiles per workgroup of the forward convs with BN statistics (PMD_FWD_TPB, default 1)
-static int g_fwd_tpb = 0;
-void conv_set_fwd_tpb(int t) { g_fwd_tpb = t < 1 ? 1 : t; }
-static int fwd_tpb() {
-  if (g_fwd_tpb < 1) {
-    const char* e = getenv("PMD_FWD_TPB");
-    const int v = e ? atoi(e) : 1;
-    g_fwd_tpb = v < 1 ? 1 : (v > 16 ? 16 : v);
-  }
-  return g_fwd_tpb;
-}
-
 template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA, bool MF32 = false,
           int WM = 2, int WN = 2, bool P8 = false, bool HALO = false, bool PRO = false>
-static void launch_k(const ConvArgs& a0, hipStream_t st) {
-  ConvArgs a = a0;
-  // forward with BN statistics: fwd_tpb() row tiles per workgroup, statistics added once
-  a.tpb = (!DGRAD && STATS && !HALO && !P8 && a.batch == 1) ? fwd_tpb() : 1;
+static void launch_k(const ConvArgs& a, hipStream_t st) {
   const bool ph2 = DGRAD && a.stride == 2;
   const int Mgrid = ph2 ? a.N * ((a.OH + 1) >> 1) * ((a.OW + 1) >> 1) : a.M;
   const int mtiles = HALO ? a.N * ((a.OH * a.OW + BM - 1) / BM) : (Mgrid + BM - 1) / BM;
-  const int tiles = ((mtiles + a.tpb - 1) / a.tpb) * ((a.Nout + BN - 1) / BN);
+  const int tiles = mtiles * ((a.Nout + BN - 1) / BN);
   const int phases = ph2 ? 4 : 1;
   const dim3 grid(tiles, phases, a.batch), block(64 * WM * WN);
   if constexpr (DGRAD) {  // instantiation per count of fused BN-reduce input sets (register peak)
@@ -1707,7 +1673,6 @@ static int conv_igemm_launch_b(const bf16_t* src, const bf16_t* wt, bf16_t* out,
   if (stride != 1 && stride != 2) return 3;
   if (batch < 1 || batch > 65535 || (batch > 1 && (dgrad || stats || addend || bnr))) return 6;
   ConvArgs a;
-  a.tpb = 1;
   a.batch = batch;
   a.bs_src = bs_src;
   a.bs_wt = bs_wt;

@@ -38,7 +38,6 @@ int conv1x1_policy();
 void conv1x1_set_bn(int bn);
 long long conv1x1_launches();
 int conv1x1_stream_bn(int KR, int Nout, int nE, int nM);
-void conv_set_fwd_tpb(int t);  // row tiles per workgroup of the forward convs with BN statistics
 void conv_set_prologue(const float* p);  // BN-apply prologue of the next conv forward (experiment)
 int conv1x1_stream_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, int M, int KR, int Nout, bool dgrad,
                           float* stats, const float* shift, const bf16_t* addend, const uint8_t* addend_mask,
