@@ -109,6 +109,9 @@ __device__ __forceinline__ void wait_vmcnt() {
 #ifndef PMD_CONV_ST_PASS
 #define PMD_CONV_ST_PASS 0
 #endif
+#ifndef PMD_F8_NB2_MINB4
+#define PMD_F8_NB2_MINB4 0  // 1: the 2-set single-stage fp8 dgrad under the PMD_F8_MINB cap too
+#endif
 #ifndef PMD_TIMING_NO_ATOMICS
 #define PMD_TIMING_NO_ATOMICS 0  // bit 0 / 1: drop the forward BN statistics / the dgrad fused-reduce atomics
                                  // (WRONG numerics; timing A/B only)
@@ -164,7 +167,8 @@ template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA, boo
           int WM = 2, int WN = 2, bool P8 = false, bool HALO = false, int NB = 2, bool F8 = false,
           int NST1 = 0, bool PRO = false>
 __global__ __launch_bounds__(64 * WM * WN,
-                             (F8 && NST1 && NB < 2) ? PMD_F8_MINB : (WM * WN == 4 ? PMD_CONV_MINB4 : 2))
+                             (F8 && NST1 && (NB < 2 || PMD_F8_NB2_MINB4)) ? PMD_F8_MINB
+                                                                          : (WM * WN == 4 ? PMD_CONV_MINB4 : 2))
     void conv_igemm_kernel(ConvArgs a) {
   constexpr int NW = WM * WN, NT = 64 * NW;
   static_assert(DMA || (BK == 64 && NST == 2 && NW == 4), "register staging: BK=64, 2 stages, 4 waves");
@@ -546,7 +550,7 @@ __global__ __launch_bounds__(64 * WM * WN,
 #ifndef PMD_F8_NJ
 #define PMD_F8_NJ 4
 #endif
-        constexpr int NJW = (NB < 2 && PMD_F8_MINB >= 4) ? 1 : PMD_F8_NJ;
+        constexpr int NJW = ((NB < 2 || PMD_F8_NB2_MINB4) && PMD_F8_MINB >= 4) ? 1 : PMD_F8_NJ;
         constexpr int NJ = NJW < NI ? NJW : NI;
         static_assert(NI % NJ == 0, "NJ divides NI");
 #pragma unroll
@@ -1049,7 +1053,11 @@ __global__ __launch_bounds__(64 * WM * WN,
 #ifndef PMD_EPI_G
 #define PMD_EPI_G 4
 #endif
-  constexpr int G = ITERS < PMD_EPI_G ? ITERS : PMD_EPI_G;
+#ifndef PMD_F8_NB2_G
+#define PMD_F8_NB2_G PMD_EPI_G  // rows in flight of the 2-set single-stage fp8 dgrad epilogue
+#endif
+  constexpr int GW = (F8 && NST1 && NB == 2) ? PMD_F8_NB2_G : PMD_EPI_G;
+  constexpr int G = ITERS < GW ? ITERS : GW;
   static_assert(ITERS % G == 0, "epilogue groups");
   const bool has_add = DGRAD && a.addend, has_amask = DGRAD && a.addend_mask;
   // Per thread the chunk column (cc, n) is fixed and the tile row advances by
