@@ -114,6 +114,14 @@ def syncbn_label(comm, sync_bn):
     return {"nccl": "rccl"}.get(comm.backend, comm.backend)
 
 
+def native_build_info():
+    """Provenance of the loaded extension (library digest and compile flags): a variant
+    build (e.g. the timing-only -DPMD_TIMING_NO_ATOMICS) is refused at import unless
+    PMD_ALLOW_VARIANT=1, and shows here when it was allowed."""
+    from pytorch_multiprocessing_distributed_amd.ops import native
+    return native.stamp_info()
+
+
 def bench_rank(rank, world, a):
     from pytorch_multiprocessing_distributed_amd import launch
     from pytorch_multiprocessing_distributed_amd.data.loader import SyntheticImageNet
@@ -289,6 +297,8 @@ def bench_rank(rank, world, a):
                        "sync_bn": a.sync_bn == "on" and (world > 1 or rehearsal),
                        "bucket_mb": a.bucket_mb, "hip_graph": bool(a.graph and world == 1),
                        "syncbn_comm": syncbn_label(comm, a.sync_bn),
+                       "syncbn_ordering": (comm.xgmi.ordering if comm is not None and comm.xgmi is not None
+                                           else None),
                        "grad_compress": a.grad_compress,
                        "grad_transport": model.transport,
                        "grad_buckets_mb": ([round(m, 2) for m in model.bucket_sizes_mb()]
@@ -296,6 +306,7 @@ def bench_rank(rank, world, a):
             "final_loss": round(final_loss, 4),
             "tune_source": tune_source,
             "kernel_choice_hash": choice_hash,
+            **native_build_info(),
             "host_enqueue_ms_per_step": round(1000.0 * host_dt / a.steps, 3),
             "host_ms_per_step_idle_device": round(host_iso_ms, 3),
         }

@@ -4,6 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export PMD_NO_AUTOBUILD=1
+export PMD_ALLOW_VARIANT=1   # the variants are the point here (ops/native.py refuses them otherwise)
 SO=pytorch_multiprocessing_distributed_amd/_C.cpython-310-x86_64-linux-gnu.so
 D=${AB_DIR:-abso}
 cp $SO $D/so_current_backup.so

@@ -191,12 +191,22 @@ int conv_fp8_fwd_launch(const uint8_t* x, const uint8_t* w, bf16_t* out, float* 
 constexpr int kXgmiMaxRanks = 16;
 constexpr int kXgmiChunk = 512;        // floats per block of the fused SyncBN kernel (small:
 constexpr int kXgmiMaxBlocks = 64;     // its slot collapse is latency-bound, so spread it out)
-constexpr int kXgmiArChunk = 2048;     // floats per block of the plain all-reduce
 constexpr int kXgmiCap = kXgmiChunk * kXgmiMaxBlocks;  // max floats per call
 constexpr int kXgmiFlagBytes = 4096;
+// Per-communicator control block passed to every exchange kernel.  Block b of EVERY kernel
+// owns region [b * kXgmiChunk, (b + 1) * kXgmiChunk) of each parity slot and epochs[b].
+struct XgmiCtl {
+  uint32_t* epochs;                 // [kXgmiMaxBlocks] per-block call counters (device)
+  uint32_t* err;                    // device error word
+  uint32_t* err_host;               // host-mapped error word (device view; nullable)
+  unsigned long long timeout_ticks; // spin deadline, wall-clock ticks
+  int order;                        // 0 light (completion-only), 1 strict (release/acquire fences)
+  int delay_where;                  // test-only skew: 0 off, 1 before publish, 2 before reading
+  unsigned long long delay_ticks;
+  int ar_region;                    // plain all-reduce floats per block: 0 = kXgmiChunk (test-only override)
+};
 int xgmi_allreduce_launch(float* const* data, uint32_t* const* flags, float* x, int n, int rank,
-                          int world, uint32_t* epochs, uint32_t* err, uint32_t* err_host,
-                          unsigned long long timeout_ticks, hipStream_t st);
+                          int world, const XgmiCtl& c, hipStream_t st);
 
 // SyncBN collapse + one-shot exchange + finalize (fwd) / global sums (bwd) in one kernel
 struct BnFinalizeOut {
@@ -228,6 +238,5 @@ struct XgmiBnArgs {
 // fused SyncBN kernel: channel pairs per block (1..kBnPairs); default kBnPairs
 void xgmi_set_bn_pairs(int pairs);
 int xgmi_bn_launch(float* const* data, uint32_t* const* flags, const XgmiBnArgs& args, int rank, int world,
-                   uint32_t* epochs, uint32_t* err, uint32_t* err_host, unsigned long long timeout_ticks,
-                   hipStream_t st);
+                   const XgmiCtl& c, hipStream_t st);
 }  // namespace pmd

@@ -29,46 +29,66 @@
 // check runs before any checkpoint is written: a poisoned state is never saved.
 #include "common.h"
 
-// Memory ordering of the exchange (PMD_XGMI_LIGHT, default 1).  Receive buffers and flags
-// live in UNCACHED memory (MTYPE UC, runtime/xgmi.cpp): stores to them bypass the L2s and
-// loads from them always reach memory, so publishing needs no cache maintenance, only
-// completion: the writer waits for its payload stores (s_waitcnt vmcnt(0)) before the flag
-// store, and the reader's spin reads the flag with plain (relaxed) system-scope loads and
-// reads the payload only after a load returned the epoch.  The C++ release / acquire forms
-// (__threadfence_system, release store, acquire loads) add an L2 write-back (buffer_wbl2)
-// per block and an L2 invalidate per spin iteration -- writing back the dirty conv output
-// lines of the XCD's L2 on every SyncBN call.  Measured at W = 1 (rehearsal, full R50 step):
-// PMD_XGMI_LIGHT=0 spends 24 us per call (98 calls, 2.4 ms per step) -- profiles/rehearsal_r04.txt.
-#ifndef PMD_XGMI_LIGHT
-#define PMD_XGMI_LIGHT 1
-#endif
+// Memory ordering of the exchange: a RUNTIME choice (XgmiCtl::order), picked at startup by
+// the stress self-test (parallel/xgmi.py: light first, strict if light fails, RCCL SyncBN if
+// both fail).  Receive buffers and flags live in uncached device memory (runtime/xgmi.cpp),
+// and EVERY payload and flag store is a system-scope store (sc0 sc1: write-through to
+// memory on the writer's side, whatever MTYPE the importing GPU's IPC mapping carries), every
+// payload / flag load a system-scope load (bypasses L1 and L2).
+//   kXgmiLight  (0): completion-only publish -- each storing wave waits for its payload stores
+//                    (s_waitcnt vmcnt(0)), a workgroup barrier, then ONE relaxed flag store per
+//                    peer; the reader polls relaxed and reads the payload after the match.
+//   kXgmiStrict (1): the same plus a system-scope RELEASE fence (L2 write-back) between the
+//                    barrier and the flag store (followed by an explicit vmcnt(0): the compiler
+//                    may drop the wait after the write-back, MI355X_MICROARCH "Compiler hazard"),
+//                    and ONE system-scope ACQUIRE fence (L1/L2 invalidate) after the poll
+//                    matched, before the workgroup barrier that releases the readers.
+// The old C++ release-store / acquire-load forms cost 24 us per call (an L2 write-back per
+// block and an invalidate per SPIN ITERATION; profiles/rehearsal_r04.txt); the strict form
+// pays one write-back per block and one invalidate per matched flag.
+constexpr int kXgmiLight = 0;
+constexpr int kXgmiStrict = 1;
 
 namespace pmd {
 
-// payload stores complete (acknowledged) before the flag store that publishes them
+template <int ORDER>
 __device__ __forceinline__ void xgmi_publish_fence() {
-  if constexpr (PMD_XGMI_LIGHT)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else
-    __threadfence_system();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's payload stores completed
 }
+template <int ORDER>
 __device__ __forceinline__ void xgmi_flag_store(uint32_t* f, uint32_t e) {
-  if constexpr (PMD_XGMI_LIGHT)
-    __hip_atomic_store(f, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  else
-    __hip_atomic_store(f, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if constexpr (ORDER == kXgmiStrict) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");      // system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __hip_atomic_store(f, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ uint32_t xgmi_flag_load(const uint32_t* f) {
-  if constexpr (PMD_XGMI_LIGHT)
-    return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  else
-    return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <int ORDER>
+__device__ __forceinline__ void xgmi_after_match() {
+  if constexpr (ORDER == kXgmiStrict) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");      // system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
 }
 
-// payload read of the receive buffer: a system-scope load (sc0 sc1: bypasses the CU's
-// vector L1 as well, which no acquire invalidates any more in the light protocol)
+// payload store / load: system scope (write-through store, L1+L2-bypassing load)
+__device__ __forceinline__ void xgmi_st(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ float xgmi_ld(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Test-only skew injection (XgmiCtl::delay_*): the calling rank idles `ticks` of the wall
+// clock at one point of the protocol -- 1: before publishing (a late rank), 2: after its
+// flags matched, before reading the payload (a slow reader: what a peer running ahead could
+// overwrite).  0 = off (the production value).
+__device__ __forceinline__ void xgmi_delay(unsigned long long ticks) {
+  const unsigned long long t0 = (unsigned long long)wall_clock64();
+  while ((unsigned long long)wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
 }
 
 struct XgmiPeers {
@@ -78,13 +98,12 @@ struct XgmiPeers {
 
 // Wait until the flag reaches epoch e; false (and both error words set) once
 // `ticks` of the constant wall clock have passed.
-__device__ __forceinline__ bool xgmi_wait_flag(const uint32_t* f, uint32_t e, unsigned long long ticks,
-                                               uint32_t* err, uint32_t* err_host) {
+__device__ __forceinline__ bool xgmi_wait_flag(const uint32_t* f, uint32_t e, const XgmiCtl& c) {
   const unsigned long long t0 = (unsigned long long)wall_clock64();
   while ((int)(xgmi_flag_load(f) - e) < 0) {
-    if ((unsigned long long)wall_clock64() - t0 > ticks) {
-      atomicOr(err, 1u);
-      if (err_host) __hip_atomic_store(err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if ((unsigned long long)wall_clock64() - t0 > c.timeout_ticks) {
+      atomicOr(c.err, 1u);
+      if (c.err_host) __hip_atomic_store(c.err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return false;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -92,61 +111,72 @@ __device__ __forceinline__ bool xgmi_wait_flag(const uint32_t* f, uint32_t e, un
   return true;
 }
 
-__global__ __launch_bounds__(256) void xgmi_allreduce_kernel(XgmiPeers peers, float* __restrict__ x,
-                                                            int n, int rank, int world,
-                                                            uint32_t* __restrict__ epochs,
-                                                            uint32_t* __restrict__ err,
-                                                            uint32_t* err_host,
-                                                            unsigned long long timeout_ticks) {
+// The exchange shared by both kernels, for block b of a call at epoch e: region
+// [b * kXgmiChunk, (b + 1) * kXgmiChunk) of parity slot (e & 1).  ONE block -> region map and
+// ONE per-block epoch counter for every kernel, so the "at most one call ahead" argument holds
+// for every region whichever kernels are interleaved: a rank that reached epoch e + 1 on block
+// b finished epoch e there, which needed every peer's epoch-e flag of block b, which each peer
+// raised only after its epoch e - 1 read of that region (stream order) -- so the parity slot it
+// now overwrites is no longer read by anyone.  (Round 4 gave the plain all-reduce 2048-float
+// regions, so its block 0 overlapped the fused kernel's blocks 1-3 under a different epoch.)
+//   push `len` floats from `src` (LDS or global) to slot [par][rank] of every peer, raise my
+//   flag, wait for every peer's flag; returns false on timeout.
+template <int ORDER>
+__device__ __forceinline__ bool xgmi_exchange(const XgmiPeers& peers, const float* src, int len, int extra_idx,
+                                              const float* extra, int rank, int world, int b, int region,
+                                              uint32_t e, const XgmiCtl& c, int* bad_sh) {
+  const int tid = threadIdx.x;
+  if (c.delay_where == 1 && c.delay_ticks) xgmi_delay(c.delay_ticks);
+  const size_t my_slot = ((size_t)(e & 1) * world + rank) * kXgmiCap + (size_t)region;
+  for (int r = 0; r < world; ++r) {
+    float* dst = peers.data[r] + my_slot;
+    for (int i = tid; i < len; i += 256) xgmi_st(dst + i, src[i]);
+    if (extra && tid == 0) xgmi_st(dst + extra_idx, *extra);
+  }
+  xgmi_publish_fence<ORDER>();
+  __syncthreads();
+  if (tid < world) xgmi_flag_store<ORDER>(peers.flags[tid] + rank * kXgmiMaxBlocks + b, e);
+  if (tid < world) {
+    const uint32_t* f = peers.flags[rank] + tid * kXgmiMaxBlocks + b;
+    if (!xgmi_wait_flag(f, e, c)) *bad_sh = 1;
+    xgmi_after_match<ORDER>();
+  }
+  if (c.delay_where == 2 && c.delay_ticks) xgmi_delay(c.delay_ticks);
+  __syncthreads();   // (the flag loads returned before any thread reads the payload)
+  return *bad_sh == 0;
+}
+
+template <int ORDER>
+__global__ __launch_bounds__(256) void xgmi_allreduce_kernel(XgmiPeers peers, float* __restrict__ x, int n,
+                                                            int rank, int world, XgmiCtl c) {
   __shared__ uint32_t e_sh;
   __shared__ int bad_sh;
-  const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x;
+  const int b = blockIdx.x, tid = threadIdx.x;
   if (tid == 0) {
-    e_sh = epochs[b] + 1;
-    epochs[b] = e_sh;
+    e_sh = c.epochs[b] + 1;
+    c.epochs[b] = e_sh;
     bad_sh = 0;
   }
   __syncthreads();
   const uint32_t e = e_sh;
-  const int p = e & 1;
-  const int lo = b * kXgmiArChunk;
-  const int len = min(kXgmiArChunk, n - lo);
-  // 1) push my chunk into slot [p][rank] of every rank's receive buffer
-  const size_t my_slot = ((size_t)p * world + rank) * kXgmiCap + lo;
-  const bool vec = ((len & 3) == 0) && ((reinterpret_cast<uintptr_t>(x + lo) & 15) == 0);
-  for (int r = 0; r < world; ++r) {
-    float* dst = peers.data[r] + my_slot;
-    if (vec) {
-      for (int i = tid; i < (len >> 2); i += 256)
-        reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(x + lo)[i];
-    } else {
-      for (int i = tid; i < len; i += 256) dst[i] = x[lo + i];
-    }
-  }
-  xgmi_publish_fence();
-  __syncthreads();
-  // 2) raise my flag (block b) in every rank's buffer
-  if (tid < world) xgmi_flag_store(peers.flags[tid] + rank * kXgmiMaxBlocks + b, e);
-  // 3) wait until every rank's chunk for epoch e has landed in MY buffer
-  if (tid < world) {
-    const uint32_t* f = peers.flags[rank] + tid * kXgmiMaxBlocks + b;
-    if (!xgmi_wait_flag(f, e, timeout_ticks, err, err_host)) bad_sh = 1;
-  }
-  __syncthreads();   // (the flag loads returned before any thread reads the payload below)
+  // c.ar_region: floats per block; kXgmiChunk in production.  The round-4 split map (2048) is
+  // kept ONLY as the negative control of the interleaving stress test (tests/test_xgmi_gpu.py)
+  const int chunk = c.ar_region > 0 ? c.ar_region : kXgmiChunk;
+  const int lo = b * chunk;
+  const int len = min(chunk, n - lo);
+  // 1-3) push my region to every rank, flag, wait for all W flags of my buffer
+  const bool ok = xgmi_exchange<ORDER>(peers, x + lo, len, 0, nullptr, rank, world, b, lo, e, c, &bad_sh);
   // 4) sum the W slots in rank order (identical on every rank); NaN on timeout
-  const float* mine = peers.data[rank] + (size_t)p * world * kXgmiCap + lo;
-  const bool bad = bad_sh != 0;
+  const float* mine = peers.data[rank] + (size_t)(e & 1) * world * kXgmiCap + lo;
   for (int i = tid; i < len; i += 256) {
     float s = 0.f;
     for (int r = 0; r < world; ++r) s += xgmi_ld(mine + (size_t)r * kXgmiCap + i);
-    x[lo + i] = bad ? __builtin_nanf("") : s;
+    x[lo + i] = ok ? s : __builtin_nanf("");
   }
-  (void)nb;
 }
 
 int xgmi_allreduce_launch(float* const* data, uint32_t* const* flags, float* x, int n, int rank,
-                          int world, uint32_t* epochs, uint32_t* err, uint32_t* err_host,
-                          unsigned long long timeout_ticks, hipStream_t st) {
+                          int world, const XgmiCtl& c, hipStream_t st) {
   if (world < 1 || world > kXgmiMaxRanks || n < 0 || n > kXgmiCap) return 1;
   if (n == 0) return 0;
   XgmiPeers p{};
@@ -154,9 +184,13 @@ int xgmi_allreduce_launch(float* const* data, uint32_t* const* flags, float* x, 
     p.data[r] = data[r];
     p.flags[r] = flags[r];
   }
-  const int nb = (n + kXgmiArChunk - 1) / kXgmiArChunk;
-  hipLaunchKernelGGL(xgmi_allreduce_kernel, dim3(nb), dim3(256), 0, st, p, x, n, rank, world, epochs,
-                     err, err_host, timeout_ticks);
+  const int chunk = c.ar_region > 0 ? c.ar_region : kXgmiChunk;
+  if (chunk > kXgmiCap) return 1;
+  const int nb = (n + chunk - 1) / chunk;
+  if (c.order == kXgmiStrict)
+    hipLaunchKernelGGL(xgmi_allreduce_kernel<kXgmiStrict>, dim3(nb), dim3(256), 0, st, p, x, n, rank, world, c);
+  else
+    hipLaunchKernelGGL(xgmi_allreduce_kernel<kXgmiLight>, dim3(nb), dim3(256), 0, st, p, x, n, rank, world, c);
   return 0;
 }
 
@@ -171,7 +205,8 @@ namespace pmd {
 //      (s0, s1) pairs -- backward also adds the LOCAL sums into the gamma/beta
 //      gradient arena (DDP averages those later, like every other gradient);
 //   1-3) exchanges the pairs (+ the local element count) one-shot over xGMI
-//      exactly like xgmi_allreduce_kernel;
+//      through the same xgmi_exchange (same block -> region map, same epochs)
+//      as xgmi_allreduce_kernel;
 //   4) forward: BatchNorm finalize from the global sums (params [4][C],
 //      running stats, num_batches_tracked, global count); backward: writes the
 //      global (sum dz, sum dz*xhat) as [2][C] for bn_bwd_elemt.
@@ -179,18 +214,17 @@ constexpr int kBnPairs = (kXgmiChunk - 2) / 2;  // 255 channels per block; [2*kB
 static int g_bn_pairs = 64;  // one 64-channel collapse pass per block (see the kernel)
 void xgmi_set_bn_pairs(int pairs) { g_bn_pairs = pairs < 1 ? 1 : (pairs > kBnPairs ? kBnPairs : pairs); }
 
+template <int ORDER>
 __global__ __launch_bounds__(256) void xgmi_bn_kernel(XgmiPeers peers, XgmiBnArgs a, int rank, int world,
-                                                     uint32_t* __restrict__ epochs,
-                                                     uint32_t* __restrict__ err, uint32_t* err_host,
-                                                     unsigned long long timeout_ticks) {
+                                                     XgmiCtl ctl) {
   __shared__ float loc[kXgmiChunk];
   __shared__ float part[4][64][2];
   __shared__ uint32_t e_sh;
   __shared__ int bad_sh;
   const int b = blockIdx.x, tid = threadIdx.x;
   if (tid == 0) {
-    e_sh = epochs[b] + 1;
-    epochs[b] = e_sh;
+    e_sh = ctl.epochs[b] + 1;
+    ctl.epochs[b] = e_sh;
     bad_sh = 0;
   }
   const int P = a.CA + a.CB;
@@ -253,23 +287,10 @@ __global__ __launch_bounds__(256) void xgmi_bn_kernel(XgmiPeers peers, XgmiBnArg
   __syncthreads();
   const uint32_t e = e_sh;
   const int par = e & 1;
-  // 1) push pairs + count into slot [par][rank] of every rank's receive buffer
-  const size_t my_slot = ((size_t)par * world + rank) * kXgmiCap + (size_t)b * kXgmiChunk;
-  for (int r = 0; r < world; ++r) {
-    float* dst = peers.data[r] + my_slot;
-    for (int i = tid; i < 2 * np; i += 256) dst[i] = loc[i];
-    if (tid == 0) dst[2 * kBnPairs] = loc[2 * kBnPairs];
-  }
-  xgmi_publish_fence();
-  __syncthreads();
-  // 2) flag, 3) wait
-  if (tid < world) xgmi_flag_store(peers.flags[tid] + rank * kXgmiMaxBlocks + b, e);
-  if (tid < world) {
-    const uint32_t* f = peers.flags[rank] + tid * kXgmiMaxBlocks + b;
-    if (!xgmi_wait_flag(f, e, timeout_ticks, err, err_host)) bad_sh = 1;
-  }
-  __syncthreads();   // (the flag loads returned before any thread reads the payload below)
-  const bool bad = bad_sh != 0;
+  // 1-3) push pairs + count into slot [par][rank] of every rank's receive buffer, flag, wait
+  const bool ok = xgmi_exchange<ORDER>(peers, loc, 2 * np, 2 * kBnPairs, &loc[2 * kBnPairs], rank, world, b,
+                                       b * kXgmiChunk, e, ctl, &bad_sh);
+  const bool bad = !ok;
   // 4) global sums in rank order, then finalize / publish (NaN outputs on timeout)
   const float* mine = peers.data[rank] + (size_t)par * world * kXgmiCap + (size_t)b * kXgmiChunk;
   float cnt = 0.f;
@@ -325,8 +346,7 @@ __global__ __launch_bounds__(256) void xgmi_bn_kernel(XgmiPeers peers, XgmiBnArg
 }
 
 int xgmi_bn_launch(float* const* data, uint32_t* const* flags, const XgmiBnArgs& args, int rank, int world,
-                   uint32_t* epochs, uint32_t* err, uint32_t* err_host, unsigned long long timeout_ticks,
-                   hipStream_t st) {
+                   const XgmiCtl& c, hipStream_t st) {
   if (world < 1 || world > kXgmiMaxRanks) return 1;
   const int P = args.CA + args.CB;
   XgmiBnArgs a = args;
@@ -342,8 +362,10 @@ int xgmi_bn_launch(float* const* data, uint32_t* const* flags, const XgmiBnArgs&
     p.data[r] = data[r];
     p.flags[r] = flags[r];
   }
-  hipLaunchKernelGGL(xgmi_bn_kernel, dim3(nb), dim3(256), 0, st, p, a, rank, world, epochs, err,
-                     err_host, timeout_ticks);
+  if (c.order == kXgmiStrict)
+    hipLaunchKernelGGL(xgmi_bn_kernel<kXgmiStrict>, dim3(nb), dim3(256), 0, st, p, a, rank, world, c);
+  else
+    hipLaunchKernelGGL(xgmi_bn_kernel<kXgmiLight>, dim3(nb), dim3(256), 0, st, p, a, rank, world, c);
   return 0;
 }
 

@@ -4,13 +4,24 @@
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 
+#include <chrono>
 #include <cstring>
+#include <thread>
 
 namespace pmd {
 
 #define RCCL_OK(x)                                                                   \
   do {                                                                               \
     ncclResult_t r_ = (x);                                                           \
+    TORCH_CHECK(r_ == ncclSuccess, #x " failed: ", ncclGetErrorString(r_));           \
+  } while (0)
+// A non-blocking communicator (below) may answer ncclInProgress while it finishes work it
+// started in the background (the first collective's connection setup): poll its async state
+// until it settles, then check it
+#define RCCL_CALL(x)                                                                 \
+  do {                                                                               \
+    ncclResult_t r_ = (x);                                                           \
+    if (r_ == ncclInProgress) r_ = settle_();                                        \
     TORCH_CHECK(r_ == ncclSuccess, #x " failed: ", ncclGetErrorString(r_));           \
   } while (0)
 #define HIP_OK2(x)                                                                   \
@@ -40,7 +51,7 @@ std::string RcclComm::unique_id() {
 }
 
 RcclComm::RcclComm(const std::string& uid, int64_t rank, int64_t world, int64_t device, int64_t priority,
-                   int64_t stream)
+                   int64_t stream, double init_timeout_s)
     : rank_(rank), world_(world), device_(device) {
   TORCH_CHECK(uid.size() == NCCL_UNIQUE_ID_BYTES, "rccl: unique id must be ", NCCL_UNIQUE_ID_BYTES,
               " bytes");
@@ -48,7 +59,35 @@ RcclComm::RcclComm(const std::string& uid, int64_t rank, int64_t world, int64_t 
   c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, device));
   ncclUniqueId id;
   std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
-  RCCL_OK(ncclCommInitRank(&comm_, (int)world, id, (int)rank));
+  // NON-BLOCKING init bounded in wall time: a peer that never arrives (it failed before its
+  // own init) must not leave this rank stuck inside ncclCommInitRank -- on the deadline the
+  // half-built communicator is aborted and the constructor throws (parallel/rccl.py then
+  // agrees the failure with every rank and falls back to c10d)
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  ncclResult_t r = ncclCommInitRankConfig(&comm_, (int)world, id, (int)rank, &cfg);
+  if (r == ncclInProgress || r == ncclSuccess) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      ncclResult_t ae = ncclSuccess;
+      r = comm_ ? ncclCommGetAsyncError(comm_, &ae) : ncclInternalError;
+      if (r == ncclSuccess) r = ae;
+      if (r != ncclInProgress) break;
+      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (init_timeout_s > 0 && el > init_timeout_s) {
+        (void)ncclCommAbort(comm_);
+        comm_ = nullptr;
+        TORCH_CHECK(false, "rccl: ncclCommInitRank did not complete within ", init_timeout_s,
+                    " s (a peer rank never joined); communicator aborted");
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+  }
+  if (r != ncclSuccess) {
+    if (comm_) (void)ncclCommAbort(comm_);
+    comm_ = nullptr;
+    TORCH_CHECK(false, "rccl: ncclCommInitRankConfig failed: ", ncclGetErrorString(r));
+  }
   if (stream) {
     stream_ = reinterpret_cast<hipStream_t>(stream);
     owns_stream_ = false;
@@ -67,12 +106,34 @@ RcclComm::~RcclComm() {
       // already torn down by abort()
     } else {
       (void)hipStreamSynchronize(stream_);
+      // non-blocking communicator: finalize, let it settle (bounded), then destroy
+      if (ncclCommFinalize(comm_) == ncclInProgress) {
+        const auto t0 = std::chrono::steady_clock::now();
+        ncclResult_t ae = ncclInProgress;
+        while (ae == ncclInProgress &&
+               std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < 30.0) {
+          if (ncclCommGetAsyncError(comm_, &ae) != ncclSuccess) break;
+          std::this_thread::yield();
+        }
+      }
       (void)ncclCommDestroy(comm_);
     }
   }
   for (auto& e : ring_) (void)hipEventDestroy(e);
   if (in_ev_) (void)hipEventDestroy(in_ev_);
   if (stream_ && owns_stream_) (void)hipStreamDestroy(stream_);
+}
+
+ncclResult_t RcclComm::settle_() {
+  ncclResult_t ae = ncclInProgress;
+  const auto t0 = std::chrono::steady_clock::now();
+  while (ae == ncclInProgress) {
+    ncclResult_t r = ncclCommGetAsyncError(comm_, &ae);
+    if (r != ncclSuccess) return r;
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 600.0) return ncclInternalError;
+    if (ae == ncclInProgress) std::this_thread::yield();
+  }
+  return ae;
 }
 
 hipEvent_t RcclComm::next_event_() {
@@ -101,8 +162,8 @@ void RcclComm::all_reduce_record(const at::Tensor& t, int op, hipEvent_t done, h
   c10::DeviceGuard g(t.device());
   fence_in_();
   if (start) HIP_OK2(hipEventRecord(start, stream_));
-  RCCL_OK(ncclAllReduce(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), nccl_dtype(t.scalar_type()),
-                        op == 1 ? ncclAvg : ncclSum, comm_, stream_));
+  RCCL_CALL(ncclAllReduce(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), nccl_dtype(t.scalar_type()),
+                          op == 1 ? ncclAvg : ncclSum, comm_, stream_));
   HIP_OK2(hipEventRecord(done, stream_));
   calls_++;
 }
@@ -121,8 +182,8 @@ void RcclComm::broadcast_(const at::Tensor& t, int64_t root) {
               "rccl: contiguous tensor on this rank's device expected");
   c10::DeviceGuard g(t.device());
   fence_in_();
-  RCCL_OK(ncclBroadcast(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), nccl_dtype(t.scalar_type()),
-                        (int)root, comm_, stream_));
+  RCCL_CALL(ncclBroadcast(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), nccl_dtype(t.scalar_type()),
+                          (int)root, comm_, stream_));
   hipEvent_t done = next_event_();
   HIP_OK2(hipEventRecord(done, stream_));
   wait(done);
@@ -147,9 +208,9 @@ void register_rccl(pybind11::module& m) {
   namespace py = pybind11;
   py::class_<RcclComm>(m, "RcclComm")
       .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
-      .def(py::init<const std::string&, int64_t, int64_t, int64_t, int64_t, int64_t>(), py::arg("unique_id"),
-           py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("priority") = 0,
-           py::arg("stream") = 0)
+      .def(py::init<const std::string&, int64_t, int64_t, int64_t, int64_t, int64_t, double>(),
+           py::arg("unique_id"), py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("priority") = 0,
+           py::arg("stream") = 0, py::arg("init_timeout_s") = 300.0)
       .def("all_reduce_", &RcclComm::all_reduce_, py::arg("tensor"), py::arg("op") = 0)
       .def("broadcast_", &RcclComm::broadcast_, py::arg("tensor"), py::arg("root") = 0)
       .def("check", &RcclComm::check)

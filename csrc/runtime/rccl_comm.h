@@ -16,6 +16,9 @@
 //     stream waits on (no host blocking anywhere on the hot path).
 //   * abort(): ncclCommAbort, so a failing rank unblocks its peers; check()
 //     surfaces asynchronous RCCL errors.
+//   * the communicator is NON-BLOCKING (ncclConfig_t.blocking = 0) so that its init is
+//     bounded in wall time (a peer that failed before joining cannot hang this rank); calls
+//     that answer ncclInProgress are settled by polling ncclCommGetAsyncError.
 #pragma once
 #include <torch/extension.h>
 #include <hip/hip_runtime.h>
@@ -33,8 +36,9 @@ class RcclComm {
 
   // stream: an existing HIP stream handle to run the collectives on (the rank's step
   // streams are created up front, ops/functional.py init_step_streams), 0 = create one
+  // init_timeout_s: wall-time bound of the (non-blocking) ncclCommInitRankConfig; <= 0 = unbounded
   RcclComm(const std::string& uid, int64_t rank, int64_t world, int64_t device, int64_t priority,
-           int64_t stream = 0);
+           int64_t stream = 0, double init_timeout_s = 300.0);
   ~RcclComm();
   RcclComm(const RcclComm&) = delete;
   RcclComm& operator=(const RcclComm&) = delete;
@@ -66,6 +70,7 @@ class RcclComm {
  private:
   hipEvent_t next_event_();
   void fence_in_();
+  ncclResult_t settle_();   // wait out ncclInProgress of the non-blocking communicator
 
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;

@@ -54,6 +54,53 @@ class XgmiComm {
     set_timeout(timeout_s);
   }
 
+  // the control block every launch passes (epochs, error words, ordering, test-only skew)
+  XgmiCtl ctl() const {
+    XgmiCtl c{};
+    c.epochs = epochs_;
+    c.err = err_;
+    c.err_host = err_host_dev_;
+    c.timeout_ticks = timeout_ticks_;
+    c.order = order_;
+    c.delay_where = delay_where_;
+    c.delay_ticks = delay_ticks_;
+    c.ar_region = ar_region_;
+    return c;
+  }
+
+  // memory ordering of the exchange: 0 light (completion-only publish), 1 strict
+  // (system release fence before each flag, acquire fence after each match).  Every rank
+  // must use the same value; parallel/xgmi.py picks it with the stress self-test.
+  void set_order(int64_t order) {
+    TORCH_CHECK(order == 0 || order == 1, "xgmi: order must be 0 (light) or 1 (strict)");
+    order_ = (int)order;
+  }
+  int64_t order() const { return order_; }
+
+  // TEST-ONLY skew injection: every following call of THIS rank idles `seconds` at `where`
+  // (1 before publishing, 2 after the flags matched, before reading); where 0 = off.
+  void set_debug_delay(double seconds, int64_t where) {
+    TORCH_CHECK(where >= 0 && where <= 2 && seconds >= 0, "xgmi: bad debug delay");
+    delay_where_ = (int)where;
+    delay_ticks_ = static_cast<unsigned long long>(seconds * 1000.0 * wall_khz_);
+  }
+  // TEST-ONLY: floats per block of the plain all-reduce (0 = the shared map's kXgmiChunk);
+  // 2048 reproduces round 4's split map (the negative control of the interleaving test)
+  void set_ar_region(int64_t floats) {
+    TORCH_CHECK(floats == 0 || (floats >= 256 && floats <= kXgmiCap && floats % 256 == 0), "xgmi: bad region");
+    ar_region_ = (int)floats;
+  }
+
+  // clear both error words (host-synchronising; collective use only, after a failed self-test
+  // whose peers have all finished: the epochs stay aligned, every rank ran every call)
+  void reset_error() {
+    c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, device_));
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemset(err_, 0, sizeof(uint32_t)));
+    __atomic_store_n(err_host_, 0u, __ATOMIC_RELEASE);
+    HIP_OK(hipDeviceSynchronize());
+  }
+
   void set_timeout(double timeout_s) {
     TORCH_CHECK(timeout_s > 0, "xgmi: timeout must be positive");
     timeout_s_ = timeout_s;
@@ -110,8 +157,7 @@ class XgmiComm {
     }
     c10::DeviceGuard g(x.device());
     const int rc = xgmi_allreduce_launch(data, flags, x.data_ptr<float>(), static_cast<int>(x.numel()),
-                                         rank_, world_, epochs_, err_, err_host_dev_, timeout_ticks_,
-                                         c10::hip::getCurrentHIPStream().stream());
+                                         rank_, world_, ctl(), c10::hip::getCurrentHIPStream().stream());
     TORCH_CHECK(rc == 0, "xgmi: launch rejected");
     calls_++;
     return x;
@@ -190,8 +236,7 @@ class XgmiComm {
       data[r] = reinterpret_cast<float*>(static_cast<char*>(peers_[r]) + kXgmiFlagBytes);
     }
     c10::DeviceGuard g(slots_a.device());
-    const int rc = xgmi_bn_launch(data, flags, a, rank_, world_, epochs_, err_, err_host_dev_,
-                                  timeout_ticks_, c10::hip::getCurrentHIPStream().stream());
+    const int rc = xgmi_bn_launch(data, flags, a, rank_, world_, ctl(), c10::hip::getCurrentHIPStream().stream());
     TORCH_CHECK(rc == 0, "xgmi bn: launch rejected (", rc, ")");
     calls_++;
   }
@@ -267,6 +312,10 @@ class XgmiComm {
   unsigned long long timeout_ticks_ = 0;
   double timeout_s_ = 0.0;
   int64_t wall_khz_ = 100000;
+  int order_ = 0;
+  int delay_where_ = 0;
+  unsigned long long delay_ticks_ = 0;
+  int ar_region_ = 0;
   bool opened_ = false;
   int64_t calls_ = 0;
   struct Site {
@@ -293,6 +342,11 @@ void register_xgmi(pybind11::module& m) {
       .def("check", &XgmiComm::check)
       .def("failed", &XgmiComm::failed)
       .def("set_timeout", &XgmiComm::set_timeout, py::arg("timeout_s"))
+      .def("set_order", &XgmiComm::set_order, py::arg("order"))
+      .def_property_readonly("order", &XgmiComm::order)
+      .def("set_debug_delay", &XgmiComm::set_debug_delay, py::arg("seconds"), py::arg("where"))
+      .def("set_ar_region", &XgmiComm::set_ar_region, py::arg("floats"))
+      .def("reset_error", &XgmiComm::reset_error)
       .def_property_readonly("timeout", &XgmiComm::timeout)
       .def_property_readonly("wall_clock_khz", &XgmiComm::wall_clock_khz)
       .def_property_readonly("capacity", &XgmiComm::capacity)

@@ -193,8 +193,15 @@ def setup_syncbn(comm, sync_bn="on", transport="auto", on_gpu=True):
             raise ValueError("--syncbn_comm xgmi needs GPU ranks")
         try:
             x = comm.enable_xgmi()
-            if not x.self_test():
-                raise RuntimeError("xGMI all-reduce self-test mismatch")
+            # light -> strict memory ordering, picked by the interleaving stress self-test;
+            # PMD_XGMI_ORDER=light|strict pins one (still stress-tested)
+            pinned = os.environ.get("PMD_XGMI_ORDER", "")
+            if pinned:
+                x.set_ordering(pinned)
+                if not (x.self_test() and x.stress_test()):
+                    raise RuntimeError(f"xGMI stress self-test failed with the pinned {pinned} ordering")
+            else:
+                x.select_ordering()
         except Exception as e:  # noqa: BLE001
             if transport == "xgmi":
                 raise

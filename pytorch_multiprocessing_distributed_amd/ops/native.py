@@ -8,6 +8,14 @@ the sources in the tree.  A stale or unstamped library is rebuilt (printing
 progress), or -- with ``PMD_NO_AUTOBUILD=1`` -- refused with an ImportError:
 old kernels never run silently.  A missing or broken build raises loudly -- GPU
 code paths never fall back to PyTorch silently.
+
+Build VARIANTS are refused too: the stamp also records the compile flags, and a
+library built with extra macros (``PMD_EXTRA_CFLAGS``, e.g. the timing-only
+``-DPMD_TIMING_NO_ATOMICS`` that zeroes every BN statistic) or a non-default
+optimisation level is rebuilt with the production flags -- or, with
+``PMD_NO_AUTOBUILD=1``, refused -- unless ``PMD_ALLOW_VARIANT=1`` says the
+variant is wanted (A/B scripts, ``bench/ab_so.sh``).  ``stamp_info()`` is what
+``bench.py`` records in its JSON line (library digest, flags).
 """
 from __future__ import annotations
 
@@ -27,19 +35,54 @@ def _build_module():
     return _b
 
 
+PRODUCTION_OPT = ["-O3"]
+
+
+def variant_reason(st) -> str:
+    """Why the stamped library is not the production build ('' when it is)."""
+    if st is None:
+        return ""
+    extra = str(st.get("extra_cflags", "")).strip()
+    if extra:
+        return f"built with extra flags {extra!r}"
+    if st.get("opt", PRODUCTION_OPT) != PRODUCTION_OPT:
+        return f"built with {st.get('opt')} instead of {PRODUCTION_OPT}"
+    return ""
+
+
 def _ensure_built():
-    """Rebuild unless the library's stamp matches the sources in the tree."""
+    """Rebuild unless the library's stamp matches the sources in the tree AND records the
+    production flags (or the variant is explicitly allowed)."""
     _b = _build_module()
+    allow_variant = os.environ.get("PMD_ALLOW_VARIANT") == "1"
+    if not allow_variant and os.environ.get("PMD_EXTRA_CFLAGS", "").strip():
+        raise ImportError("PMD_EXTRA_CFLAGS is set: a variant build of the extension needs "
+                          "PMD_ALLOW_VARIANT=1 (variants are A/B or timing-only builds)")
     st = _b.read_stamp()
+    variant = "" if allow_variant else variant_reason(st)
     fresh = (os.path.exists(_b.target_path()) and st is not None
-             and st.get("sources") == _b.source_digest())
+             and st.get("sources") == _b.source_digest() and not variant)
     if fresh:
         return
     if os.environ.get("PMD_NO_AUTOBUILD") == "1":
-        why = "no build stamp" if st is None else "sources changed since the build"
-        raise ImportError(f"stale gfx950 extension {_b.target_path()} ({why}); "
+        why = ("no build stamp" if st is None else
+               f"variant library: {variant} (set PMD_ALLOW_VARIANT=1 to use it)" if variant else
+               "sources changed since the build")
+        raise ImportError(f"refusing gfx950 extension {_b.target_path()} ({why}); "
                           "run `python csrc/build.py` (PMD_NO_AUTOBUILD=1 forbids rebuilding here)")
-    _b.build(verbose=True)
+    if variant:
+        print(f"[pmd] rebuilding the extension with the production flags ({variant})", flush=True)
+    _b.build(verbose=True, force=bool(variant))
+
+
+def stamp_info() -> dict:
+    """Provenance of the loaded library for benchmark records."""
+    _b = _build_module()
+    st = _b.read_stamp() or {}
+    if os.environ.get("PMD_EXT_DIR"):
+        return {"lib_digest": None, "extra_cflags": None, "opt": None, "ext_dir": os.environ["PMD_EXT_DIR"]}
+    return {"lib_digest": (st.get("library") or "")[:16] or None,
+            "extra_cflags": st.get("extra_cflags", ""), "opt": " ".join(st.get("opt", []))}
 
 
 def _load():

@@ -139,14 +139,12 @@ def resolve_transport(comm, module, reducer="native", transport="auto", verbose=
     c, err = None, ""
     try:
         from ..ops.functional import STREAM_PRIO, comm_stream_handle
+        # collective and all-or-nothing: raises on EVERY rank when any rank failed, before
+        # any native collective runs, so the self-test below runs on all or none
         c = rccl.create(comm.group, priority=STREAM_PRIO, stream=comm_stream_handle())
     except Exception as e:  # noqa: BLE001
         err = str(e)
     ok = rccl.self_test(c, comm.group) if c is not None else False
-    if c is None:
-        # agree with the ranks that did run the self-test (they all-reduce a flag)
-        flag = torch.tensor([0], device=torch.device("cuda", torch.cuda.current_device()))
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=comm.group)
     if not ok:
         if c is not None:
             c.abort()

@@ -12,6 +12,7 @@ all-reduces there, fenced with HIP events (no host blocking).
 from __future__ import annotations
 
 import itertools
+import os
 import weakref
 
 import torch
@@ -58,21 +59,93 @@ def _store():
     return c10d._get_default_store()
 
 
-def create(group=None, priority: int = 0, store=None, stream: int = 0):
-    """Collective over ``group`` (every rank calls it).  Returns ``_C.RcclComm``.
-    ``stream``: HIP handle of an existing stream to run on (0: the communicator creates one)."""
+def _agree(ok: bool, group=None) -> bool:
+    """MIN of a 0/1 flag over the process group (c10d: gloo or ProcessGroupNCCL -- never a
+    native communicator), so every rank takes the same branch."""
+    if not dist.is_initialized():
+        return ok
+    dev = (torch.device("cuda", torch.cuda.current_device())
+           if dist.get_backend(group) == "nccl" else torch.device("cpu"))
+    flag = torch.tensor([1 if ok else 0], device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    return bool(flag.item() == 1)
+
+
+def _fault_here(stage: str) -> bool:
+    """Fault injection for tests: PMD_FAULT_RCCL_CREATE=<rank>[:<stage>] makes that rank fail
+    its communicator creation at ``stage`` ("uid" = before the unique-id exchange, "init" =
+    right before ncclCommInitRank; default "init")."""
+    spec = os.environ.get("PMD_FAULT_RCCL_CREATE", "")
+    if not spec:
+        return False
+    r, _, st = spec.partition(":")
+    return int(r) == dist.get_rank() and (st or "init") == stage
+
+
+def create(group=None, priority: int = 0, store=None, stream: int = 0, init_timeout_s: float | None = None,
+           factory=None, uid_fn=None):
+    """Collective over ``group`` (every rank calls it).  Returns ``_C.RcclComm``, or raises
+    the SAME RuntimeError on every rank: no rank ever enters a native collective
+    that a peer will not join.
+
+      1. rank 0 publishes the unique id -- or the reason it could not make one -- under a
+         fresh store key; every rank reads it (bounded by the store timeout);
+      2. every rank agrees (c10d MIN) that it holds a valid id before ANY rank calls
+         ncclCommInitRank -- a rank that failed so far skips the init, and so do its peers;
+      3. the init itself is non-blocking and bounded (``init_timeout_s``, env
+         ``PMD_RCCL_INIT_TIMEOUT``, default 300 s), so a peer failing INSIDE its init cannot
+         hang this rank;
+      4. every rank agrees that its communicator exists before anything uses it; on any
+         failure each rank aborts its own communicator and raises.
+
+    ``factory(uid, rank, world, device, priority, stream, timeout)`` / ``uid_fn()``: test
+    doubles for the native constructor / ncclGetUniqueId (tests/test_readiness_cpu.py)."""
     from ..ops.native import C
     if not dist.is_initialized():
         raise RuntimeError("torch.distributed must be initialised first (it hosts the TCPStore)")
+    factory = factory or C.RcclComm
+    uid_fn = uid_fn or C.RcclComm.unique_id
+    if init_timeout_s is None:
+        init_timeout_s = float(os.environ.get("PMD_RCCL_INIT_TIMEOUT", "300"))
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     store = store if store is not None else _store()
     key = f"pmd_rccl_uid_{next(_SEQ)}"
+    err = ""
     if rank == 0:
-        store.set(key, C.RcclComm.unique_id())
-    uid = store.get(key)                      # blocks until rank 0 published it
-    dev = torch.cuda.current_device()
-    comm = C.RcclComm(bytes(uid), rank, world, dev, priority, stream)
+        try:
+            if _fault_here("uid"):
+                raise RuntimeError("injected unique-id failure (PMD_FAULT_RCCL_CREATE)")
+            store.set(key, b"OK:" + bytes(uid_fn()))
+        except Exception as e:  # noqa: BLE001
+            err = f"rank 0: ncclGetUniqueId: {e}"
+            store.set(key, b"ERR:" + err.encode()[:200])
+    uid = None
+    try:
+        v = bytes(store.get(key))                    # blocks until rank 0 published (store timeout)
+        if v.startswith(b"OK:"):
+            uid = v[3:]
+        else:
+            err = err or v[4:].decode(errors="replace")
+    except Exception as e:  # noqa: BLE001
+        err = err or f"rank {rank}: unique id not received: {e}"
+    if uid is not None and _fault_here("init"):
+        err, uid = f"rank {rank}: injected init failure (PMD_FAULT_RCCL_CREATE)", None
+    if not _agree(uid is not None and not err, group):
+        raise RuntimeError(f"native RCCL communicator not created: {err or 'a peer rank failed before init'}")
+    comm = None
+    try:
+        dev = torch.cuda.current_device() if torch.cuda.is_available() else 0
+        comm = factory(uid, rank, world, dev, priority, stream, init_timeout_s)
+    except Exception as e:  # noqa: BLE001
+        err = f"rank {rank}: {e}"
+    if not _agree(comm is not None, group):
+        if comm is not None:
+            try:
+                comm.abort()
+            except Exception:  # noqa: BLE001
+                pass
+        raise RuntimeError(f"native RCCL communicator init failed: {err or 'on a peer rank'}")
     return register(comm)
 
 

@@ -217,3 +217,71 @@ def test_last_bucket_is_capped(last_mb):
     dp2 = DataParallel(build_model("resnet50", num_classes=1000, stem="imagenet"), None,
                        last_bucket_mb=None)
     assert dp2.bucket_sizes_mb()[-1] > last_mb
+
+
+class _FactoryComm:
+    def __init__(self, uid, rank):
+        self.uid, self.rank, self.aborted = uid, rank, 0
+
+    def abort(self):
+        self.aborted += 1
+
+
+def _create_worker(rank, world, port, out, fault, peer_init_fails):
+    import datetime
+    import time
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    if fault:
+        os.environ["PMD_FAULT_RCCL_CREATE"] = fault
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    made = []
+
+    def factory(uid, rk, w, dev, prio, stream, timeout):
+        # the native constructor's contract: a rank whose peer never completes the init
+        # gives up after `timeout` (non-blocking init + deadline) instead of hanging
+        if peer_init_fails and rk == 1:
+            raise RuntimeError("ncclCommInitRankConfig failed: injected")
+        if peer_init_fails:
+            time.sleep(min(timeout, 1.0))
+            raise RuntimeError("rccl: ncclCommInitRank did not complete (a peer rank never joined)")
+        c = _FactoryComm(uid, rk)
+        made.append(c)
+        return c
+
+    t0 = time.time()
+    res = {"rank": rank}
+    try:
+        c = rccl.create(factory=factory, uid_fn=lambda: b"u" * 128, init_timeout_s=1.0)
+        res.update(ok=True, uid=c.uid == b"u" * 128)
+    except RuntimeError as e:
+        res.update(ok=False, err=str(e))
+    res["secs"] = time.time() - t0
+    res["aborted"] = [c.aborted for c in made]
+    # the process group still works: nobody is stuck in a native collective
+    x = torch.ones(1)
+    dist.all_reduce(x)
+    res["after"] = float(x)
+    torch.save(res, f"{out}.{rank}")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fault,peer_init_fails", [("", False), ("1:init", False), ("0:uid", False),
+                                                   ("", True)])
+def test_rccl_create_is_all_or_nothing(tmp_path, fault, peer_init_fails):
+    """a communicator-creation failure on ONE rank must not leave its peers stuck in
+    ncclCommInitRank / the self-test.  Every rank agrees (c10d MIN) before the init and after
+    it, so either all ranks get a communicator or all raise the same error -- quickly."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "res")
+    mp.spawn(_create_worker, args=(2, _free_port(), out, fault, peer_init_fails), nprocs=2, join=True)
+    res = [torch.load(f"{out}.{r}", weights_only=False) for r in range(2)]
+    expect_ok = not fault and not peer_init_fails
+    for r in res:
+        assert r["ok"] is expect_ok, r
+        assert r["after"] == 2.0 and r["secs"] < 30, r
+        if expect_ok:
+            assert r["uid"]
+        else:
+            assert "not created" in r["err"] or "init failed" in r["err"], r

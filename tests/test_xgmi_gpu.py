@@ -168,3 +168,48 @@ def test_xgmi_fused_syncbn_statistics(tmp_path):
             print(f"fused SyncBN fwd kernel {k}: {v.item():.1f} us/call (2 ranks sharing 1 GPU)")
             continue
         assert (v < 1e-5).all(), (k, v)
+
+
+def _stress_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    from pytorch_multiprocessing_distributed_amd.parallel.xgmi import XgmiAllReduce
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    xg = XgmiAllReduce(timeout_s=20.0)
+    res = {}
+    # negative control FIRST (fresh epochs): round 4's split map -- the plain all-reduce's
+    # block 0 owning floats 0-2047 under epochs[0] while the fused kernel's blocks 1-3 own
+    # 512-2047 under epochs[1..3] -- with the slow rank reading late: must be caught
+    xg.set_ordering("light")
+    res["split_map_light"] = xg.stress_test(calls=240, ar_region=2048)
+    res["split_map_detail"] = dict(getattr(xg, "last_stress", {}))
+    for name in ("light", "strict"):
+        xg.set_ordering(name)
+        for delay in (50e-6, 0.0):
+            res[f"{name}_{delay}"] = xg.stress_test(calls=240, delay_s=delay)
+            res[f"{name}_{delay}_detail"] = dict(getattr(xg, "last_stress", {}))
+    res["selected"] = xg.select_ordering(verbose=False)
+    xg.check()
+    if rank == 1:      # the skewed (slow-reading) rank sees the corruption
+        torch.save({k: (v if not isinstance(v, dict) else str(v)) for k, v in res.items()}, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_xgmi_interleaved_plain_and_fused_calls_with_skewed_rank(tmp_path):
+    """>=200 back-to-back calls alternating the plain all-reduce and
+    the fused SyncBN kernel (both passes), no host sync, rank 1 delayed inside the kernel
+    (slow reader on the plain calls, late publisher on the fused ones), exact integer checks.
+    Passes under both memory orderings on the shared block -> region map; the round-4 split
+    map (negative control, test-only override) corrupts a slow reader's sum and must FAIL."""
+    out = str(tmp_path / "stress.pt")
+    mp.spawn(_stress_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    print({k: v for k, v in got.items()})
+    assert got["split_map_light"] is False, got["split_map_detail"]
+    for name in ("light", "strict"):
+        for delay in (5e-05, 0.0):
+            assert got[f"{name}_{delay}"] is True, (name, delay, got[f"{name}_{delay}_detail"])
+    assert got["selected"] == "light"
