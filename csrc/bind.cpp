@@ -1114,14 +1114,22 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("zero_", &zero_, "in-place zero of a contiguous GPU tensor (framework fill kernel)");
   m.def(
       "create_stream",
-      [](int64_t device, int64_t priority) {
+      [](int64_t device, int64_t priority, std::vector<int64_t> cu_mask) {
         c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, device));
         hipStream_t s = nullptr;
+        if (!cu_mask.empty()) {
+          // a stream restricted to a subset of the CUs (bit i of word i/32 = CU i); HIP gives
+          // it normal priority and a hardware queue of its own
+          std::vector<uint32_t> m(cu_mask.begin(), cu_mask.end());
+          const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)m.size(), m.data());
+          TORCH_CHECK(e == hipSuccess, "hipExtStreamCreateWithCUMask: ", hipGetErrorString(e));
+          return (int64_t) reinterpret_cast<uintptr_t>(s);
+        }
         const hipError_t e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, (int)priority);
         TORCH_CHECK(e == hipSuccess, "hipStreamCreateWithPriority: ", hipGetErrorString(e));
         return (int64_t) reinterpret_cast<uintptr_t>(s);
       },
-      py::arg("device"), py::arg("priority"),
+      py::arg("device"), py::arg("priority"), py::arg("cu_mask") = std::vector<int64_t>(),
       "a new non-blocking HIP stream (lives for the process; wrap with torch.cuda.ExternalStream): the "
       "step's streams are created up front so each gets its own hardware queue");
   m.def("sgd_", &sgd_);

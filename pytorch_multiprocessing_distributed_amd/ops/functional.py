@@ -349,13 +349,30 @@ def _wait_weight_images():
 _STEP_STREAMS: dict = {}
 
 
-def _new_stream(dev, prio=None):
+def _new_stream(dev, prio=None, cu_mask=None):
     # a NEW HIP stream: torch.cuda.Stream(priority=...) hands out streams of torch's fixed
     # per-priority pool (32 streams created together and spread round-robin over the hardware
     # queues, shared with whatever else -- gloo, c10d -- draws from the pool), so two of the
     # step's streams could land on one queue depending on the pool cursor
     from .native import C
-    return torch.cuda.ExternalStream(C.create_stream(dev.index, STREAM_PRIO if prio is None else prio), device=dev)
+    return torch.cuda.ExternalStream(C.create_stream(dev.index, STREAM_PRIO if prio is None else prio,
+                                                     list(cu_mask or [])), device=dev)
+
+
+def _side_cu_mask(dev):
+    """PMD_WGRAD_CUS=N (< the CU count): the weight-gradient stream runs on N CUs only --
+    CU i enabled iff i % 32 < N * 32 / n_cu (an even share of every 32-CU group) -- so the
+    main stream's latency-bound kernels always find free CUs.  Empty list: all CUs."""
+    n = int(os.environ.get("PMD_WGRAD_CUS", "0") or 0)
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    if n <= 0 or n >= ncu:
+        return []
+    keep = max(1, round(32 * n / ncu))
+    words = [0] * ((ncu + 31) // 32)
+    for i in range(ncu):
+        if i % 32 < keep:
+            words[i // 32] |= 1 << (i % 32)
+    return words
 
 
 def init_step_streams(dev):
@@ -370,7 +387,7 @@ def init_step_streams(dev):
     main = _new_stream(dev)
     main.wait_stream(torch.cuda.current_stream(dev))
     torch.cuda.set_stream(main)
-    side = _new_stream(dev, int(os.environ.get("PMD_WGRAD_PRIO", STREAM_PRIO)))
+    side = _new_stream(dev, int(os.environ.get("PMD_WGRAD_PRIO", STREAM_PRIO)), _side_cu_mask(dev))
     _WGRAD_STREAM["streams"][dev] = side
     comm = _new_stream(dev)
     _STEP_STREAMS[dev] = {"main": main, "wgrad": side, "comm": comm}
