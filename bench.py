@@ -30,10 +30,11 @@ sys.path.insert(0, ROOT)
 METRIC = ("images/sec (whole node) ResNet-50 224×224 bf16 at 1/2/4/8 MI355X; "
           "DDP scaling efficiency")
 # stock PyTorch-ROCm reference path (DDP+SyncBN+MIOpen, bench/comparator_torch.py),
-# recorded on one MI355X at per-GPU batch 256 (profiles/comparator_r01.log); reported
+# re-measured on one MI355X at per-GPU batch 256 in round 5, in the same process as a
+# 13,386 img/s run of ours (profiles/bench_r05_with_stock.jsonl; round 1: 6612.5); reported
 # as a RECORDED figure unless --with_stock measures it in the same run
-STOCK_IPS_PER_GPU_RECORDED = 6612.5
-STOCK_RECORDED_SOURCE = "profiles/comparator_r01.log (1x MI355X, round 1)"
+STOCK_IPS_PER_GPU_RECORDED = 6622.0
+STOCK_RECORDED_SOURCE = "profiles/bench_r05_with_stock.jsonl (1x MI355X, round 5, same lease as ours)"
 _MODEL_NAMES = {"resnet50": "ResNet-50", "resnet101": "ResNet-101", "resnet152": "ResNet-152",
                 "resnet34": "ResNet-34", "resnet18": "ResNet-18-ref", "res": "ResNet-18-ref"}
 
@@ -89,9 +90,6 @@ def parse():
     ap.add_argument("--host_profile", default="",
                     help="after the timed run: cProfile the host side of 10 more steps (rank 0) and "
                          "write the top functions by own time here")
-    ap.add_argument("--graph", action="store_true",
-                    help="capture the whole training step (fwd+bwd+SGD) in a HIP graph and replay it "
-                         "(single GPU); each replay is a full step on a freshly generated batch")
     return ap.parse_args()
 
 
@@ -168,7 +166,7 @@ def bench_rank(rank, world, a):
     data = SyntheticImageNet(a.batch, a.image, a.classes, steps=a.warmup + a.steps, device=dev,
                              dtype=torch.bfloat16, cpad=8, seed=rank)
     model.train()
-    # kernel choices fixed before anything runs (also before a graph capture)
+    # kernel choices fixed before anything runs
     from pytorch_multiprocessing_distributed_amd.ops import tuning
     if a.tune_table == "online":
         tune_source = "online"
@@ -187,34 +185,6 @@ def bench_rank(rank, world, a):
         opt.step()
         return loss
 
-    if a.graph and world == 1:
-        opt.graph_safe()
-        sx, sy = data.batch_at(0)
-
-        def static_step():
-            out = model(sx)
-            loss = OF.cross_entropy(out, sy)
-            opt.zero_grad()
-            loss.backward(OF.loss_seed(loss))
-            opt.step()
-            return loss
-
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for _ in range(max(a.warmup, 2)):
-                static_step()
-        torch.cuda.current_stream().wait_stream(side)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            static_loss = static_step()
-
-        def step(i):
-            x, y = data.batch_at(i)          # fresh on-device batch, copied into the graph inputs
-            sx.copy_(x)
-            sy.copy_(y)
-            graph.replay()
-            return static_loss
     for i in range(a.warmup):
         step(i)
         if i == 0 and comm is not None:
@@ -295,7 +265,7 @@ def bench_rank(rank, world, a):
                        "image_size": a.image, "per_gpu_batch": a.batch,
                        "parallelism": parallelism,
                        "sync_bn": a.sync_bn == "on" and (world > 1 or rehearsal),
-                       "bucket_mb": a.bucket_mb, "hip_graph": bool(a.graph and world == 1),
+                       "bucket_mb": a.bucket_mb,
                        "syncbn_comm": syncbn_label(comm, a.sync_bn),
                        "syncbn_ordering": (comm.xgmi.ordering if comm is not None and comm.xgmi is not None
                                            else None),

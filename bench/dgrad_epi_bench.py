@@ -62,16 +62,11 @@ def main():
     ap.add_argument("--tile", type=int, default=0, help="conv_set_tile policy (0 = autotuned)")
     ap.add_argument("--fp8", action="store_true",
                     help="also time the fp8 dgrad (e5m2 dY x e4m3 transposed weights) with the same epilogue")
-    ap.add_argument("--s1", type=int, default=0,
-                    help="streaming 1x1 kernel policy (kernels/conv1x1_stream.hip): 0 off, 1 on")
-    ap.add_argument("--s1bn", type=int, default=0, help="streaming kernel column tile (0 auto, 64, 128)")
     ap.add_argument("--impl", type=int, default=5,
                     help="conv_set_impl staging (0 = register staging, 1 = LDS-DMA BK=64, 5 = per shape)")
     a = ap.parse_args()
     _C.conv_set_tile(a.tile)
     _C.conv_set_impl(a.impl)
-    _C.conv1x1_set_policy(a.s1)
-    _C.conv1x1_set_bn(a.s1bn)
     dev = "cuda"
     N = a.batch
     tot_us = tot_ideal = 0.0

@@ -122,23 +122,6 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor wk, int64_t stride, int64_t pad, b
   return conv_fwd_impl(x, wk, stride, pad, want_stats, stats_buf, -1, -1, shift);
 }
 
-// BN-apply prologue experiment: y = conv(relu(x * p[2] + p[3])) for a 1x1 stride-1 conv,
-// x the PRE-BN activation, without materialising the BN output
-std::vector<Tensor> conv_fwd_pro(Tensor x, Tensor wk, Tensor p, bool want_stats, c10::optional<Tensor> stats_buf,
-                                 c10::optional<Tensor> shift) {
-  CHECK_DEV(p); CHECK_CONT(p);
-  TORCH_CHECK(p.scalar_type() == torch::kFloat32 && p.numel() == 4 * x.size(3), "p: fp32 [4][C]");
-  pmd::conv_set_prologue(p.data_ptr<float>());
-  try {
-    auto r = conv_fwd_impl(x, wk, 1, 0, want_stats, stats_buf, -1, -1, shift);
-    pmd::conv_set_prologue(nullptr);
-    return r;
-  } catch (...) {
-    pmd::conv_set_prologue(nullptr);
-    throw;
-  }
-}
-
 std::vector<Tensor> conv_fwd_hw(Tensor x, Tensor wk, int64_t stride, int64_t pad, int64_t out_h,
                                 int64_t out_w, bool want_stats, c10::optional<Tensor> stats_buf,
                                 c10::optional<Tensor> shift) {
@@ -1038,15 +1021,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "queue the split-K reductions of the following weight gradients (this thread)");
   m.def("wgrad_pending", &pmd::wgrad_pending);
   m.def("wgrad_flush", &wgrad_flush, "launch the queued split-K reductions as one grouped kernel");
-  m.def("conv1x1_set_policy", &pmd::conv1x1_set_policy,
-        "streaming 1x1 conv: 0 off, 1 data gradients, 2 data gradients + forwards");
-  m.def("conv1x1_policy", &pmd::conv1x1_policy);
-  m.def("conv1x1_launches", &pmd::conv1x1_launches);
   m.def("conv_fp8_fwd_set_impl", [](int64_t i) { g_fp8_fwd_impl = (int)i; },
         "fp8 forward conv kernel: 0 conv_fp8_fwd_kernel, 1 the implicit-GEMM kernel's fp8 path (default), -1 env");
-  m.def("conv1x1_stream_bn", &pmd::conv1x1_stream_bn,
-        "column tile the streaming 1x1 conv picks for (reduction, out channels, epilogue tensors, masks); 0 = ineligible");
-  m.def("conv1x1_set_bn", &pmd::conv1x1_set_bn, "streaming 1x1 conv column tile: 64 / 128, 0 = auto");
   m.def("conv_set_impl", &pmd::conv_set_impl, "conv staging/pipeline variant 0-4, 5 = per-shape default");
   m.def("conv_set_tile", &pmd::conv_set_tile,
         "conv fwd/dgrad tile policy: 0 auto, 1 128-row only, 2 256x128, 3 256x256 where legal");
@@ -1065,9 +1041,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   namespace py = pybind11;
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("wk"), py::arg("stride"), py::arg("pad"),
         py::arg("want_stats"), py::arg("stats_buf"), py::arg("shift") = py::none());
-  m.def("conv_fwd_pro", &conv_fwd_pro, py::arg("x"), py::arg("wk"), py::arg("p"), py::arg("want_stats") = true,
-        py::arg("stats_buf") = py::none(), py::arg("shift") = py::none(),
-        "1x1 conv forward of relu(x * p[2] + p[3]) (BN-apply prologue experiment)");
   m.def("conv_fwd_hw", &conv_fwd_hw, py::arg("x"), py::arg("wk"), py::arg("stride"), py::arg("pad"),
         py::arg("out_h"), py::arg("out_w"), py::arg("want_stats"), py::arg("stats_buf"),
         py::arg("shift") = py::none());

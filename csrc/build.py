@@ -114,13 +114,16 @@ def asan_runtime():
     return p if r.returncode == 0 and os.path.isabs(p) and os.path.exists(p) else None
 
 
-def build(force=False, jobs=None, debug=False, verbose=True, asan=False):
+def build(force=False, jobs=None, debug=False, verbose=True, asan=False, variant=None):
     """asan=True: the host C++ (binding layer + native runtime: reducer, RCCL/xGMI
     communicators, weight-image sets) instrumented with AddressSanitizer
     (-Xarch_host only: GPU code is never sanitised), device kernels reused, the
     library written to build/asan/ -- load it with PMD_EXT_DIR=build/asan and
     the ASan runtime preloaded (tests/test_asan_cpu.py)."""
-    os.makedirs(BUILD, exist_ok=True)
+    # variant="<name>": an A/B build with PMD_EXTRA_CFLAGS into build/variant_<name>/ and
+    # abso/so_<name>.so (bench/ab_so.sh), leaving the production objects, library and stamp alone
+    bdir = os.path.join(ROOT, "build", f"variant_{variant}") if variant else BUILD
+    os.makedirs(bdir, exist_ok=True)
     inc, lib, abi = _torch_paths()
     headers = glob.glob(os.path.join(CSRC, "kernels", "*.h"))
     opt = ["-O1", "-g"] if (debug or asan) else ["-O3"]
@@ -134,14 +137,14 @@ def build(force=False, jobs=None, debug=False, verbose=True, asan=False):
                *os.environ.get("PMD_EXTRA_CFLAGS", "").split()]
     stamps = []
     for src in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))):
-        obj = os.path.join(BUILD, os.path.basename(src) + ".o")   # shared by the ASan build
+        obj = os.path.join(bdir, os.path.basename(src) + ".o")   # shared by the ASan build
         objs.append(obj)
         cmd = (kcommon if asan else common) + ["-c", src, "-o", obj, f"-I{os.path.join(CSRC, 'kernels')}"]
         d = _digest([src, *headers], cmd)
         if force or _stale(d, obj):
             jobs_.append(cmd)
             stamps.append((obj, d))
-    hbuild = os.path.join(ROOT, "build", "csrc_asan") if asan else BUILD
+    hbuild = os.path.join(ROOT, "build", "csrc_asan") if asan else bdir
     os.makedirs(hbuild, exist_ok=True)
     # host TUs that include torch headers: the binding layer + native runtime
     # (reducer, comm bootstrap); they are host-only C++ compiled by hipcc
@@ -169,6 +172,9 @@ def build(force=False, jobs=None, debug=False, verbose=True, asan=False):
         for obj, d in stamps:          # only after every compile succeeded
             _stamp(obj, d)
     out = target_path()
+    if variant:
+        os.makedirs(os.path.join(ROOT, "abso"), exist_ok=True)
+        out = os.path.join(ROOT, "abso", f"so_{variant}.so")
     if asan:
         os.makedirs(ASAN_DIR, exist_ok=True)
         out = os.path.join(ASAN_DIR, os.path.basename(out))
@@ -187,7 +193,7 @@ def build(force=False, jobs=None, debug=False, verbose=True, asan=False):
         _stamp(out, lib_digest)
         if verbose:
             print(f"[pmd build] linked {out}", flush=True)
-    if not asan:
+    if not asan and not variant:
         st = read_stamp()
         want = {"sources": source_digest(), "library": lib_digest, "arch": ARCH,
                 "opt": opt, "extra_cflags": os.environ.get("PMD_EXTRA_CFLAGS", "")}
@@ -203,8 +209,10 @@ def main():
     ap.add_argument("--jobs", type=int, default=None)
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--asan", action="store_true", help="host-side AddressSanitizer build -> build/asan/")
+    ap.add_argument("--variant", default=None,
+                    help="A/B variant name: PMD_EXTRA_CFLAGS build -> abso/so_<name>.so (production untouched)")
     a = ap.parse_args()
-    build(force=a.force, jobs=a.jobs, debug=a.debug, asan=a.asan)
+    build(force=a.force, jobs=a.jobs, debug=a.debug, asan=a.asan, variant=a.variant)
 
 
 if __name__ == "__main__":

@@ -65,10 +65,6 @@ struct ConvArgs {
   // (byte pointers behind the bf16_t* fields); acc is scaled by 1 / (f8_sa * f8_sb)
   const float* f8_sa;
   const float* f8_sb;
-  // PRO (BN-apply prologue experiment, docs/ARCHITECTURE.md): src is the PRE-BN y of the
-  // producing conv and the A operand is relu(y * scale + shift) per input channel, with
-  // (scale, shift) rows 2 and 3 of this [4][Cs] BN parameter block
-  const float* pro_p;
 };
 typedef __attribute__((ext_vector_type(8))) int i32x8_c;
 
@@ -165,7 +161,7 @@ __device__ __forceinline__ int swz(int row) {
 // bound by that L2->LDS gather traffic); only the weight tiles stream per K-tile.
 template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA, bool MF32 = false,
           int WM = 2, int WN = 2, bool P8 = false, bool HALO = false, int NB = 2, bool F8 = false,
-          int NST1 = 0, bool PRO = false>
+          int NST1 = 0>
 __global__ __launch_bounds__(64 * WM * WN,
                              (F8 && NST1 && (NB < 2 || PMD_F8_NB2_MINB4)) ? PMD_F8_MINB
                                                                           : (WM * WN == 4 ? PMD_CONV_MINB4 : 2))
@@ -232,14 +228,9 @@ __global__ __launch_bounds__(64 * WM * WN,
   constexpr int SMEM0 = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
   constexpr int SMEM = SMEM0 > SMEM_PART ? SMEM0 : SMEM_PART;
   static_assert(SMEM + (STATS ? WM * 2 * BN * 4 : 0) <= 160 * 1024, "exceeds the 160 KiB LDS of a CU");
-  // PRO: the BN scale / shift of every input channel (1x1: channel = reduction index)
-  static_assert(!PRO || (DMA && !DGRAD && !MF32 && !P8 && !HALO && !F8 && !NST1), "PRO: plain 1x1 forward");
-  constexpr int PRO_MAXC = 512;
   constexpr int SMEM_ST = STATS ? WM * 2 * BN * 4 : 0;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM + SMEM_ST + (PRO ? 2 * PRO_MAXC * 4 : 0)];
+  __shared__ __attribute__((aligned(16))) char smem[SMEM + SMEM_ST];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
-  float* const pro_s = reinterpret_cast<float*>(smem + SMEM + SMEM_ST);
-  float* const pro_b = pro_s + PRO_MAXC;
 
   if (blockIdx.z) {  // batched launch (no statistics / addend / fused reduce: launcher contract)
     a.src += blockIdx.z * a.bs_src;
@@ -288,13 +279,6 @@ __global__ __launch_bounds__(64 * WM * WN,
   const int n0 = (L % tilesN) * BN;
   if (HALO) Mp = m0 + min(BM, hw_out - halo_t * BM);  // rows of this image only
   if (m0 >= Mp) return;  // uniform per block, before any barrier
-  if constexpr (PRO) {
-    // published by the pipeline's first barrier (its s_waitcnt lgkmcnt(0) covers these writes)
-    for (int c = threadIdx.x; c < a.Cs; c += 64 * WM * WN) {
-      pro_s[c] = a.pro_p[2 * a.Cs + c];
-      pro_b[c] = a.pro_p[3 * a.Cs + c];
-    }
-  }
 
   // ---- per-thread A-row precompute
   // register staging: thread -> (row rsub + 32 i, chunk tid & 7)
@@ -623,24 +607,6 @@ __global__ __launch_bounds__(64 * WM * WN,
       for (int i = 0; i < MI; ++i) af[i] = frag(As, wm * (BM / WM) + i * 16 + frow, q);
 #pragma unroll
       for (int j = 0; j < NI; ++j) bfg[j] = frag(Bs, wn * (BN / WN) + j * 16 + frow, q);
-      if constexpr (PRO) {
-        // this lane's 8 reduction elements are input channels kt * BK + 8 q .. + 7
-        const int c0 = kt * BK + 8 * q;
-        const float4 s0 = *reinterpret_cast<const float4*>(pro_s + c0);
-        const float4 s1 = *reinterpret_cast<const float4*>(pro_s + c0 + 4);
-        const float4 b0 = *reinterpret_cast<const float4*>(pro_b + c0);
-        const float4 b1 = *reinterpret_cast<const float4*>(pro_b + c0 + 4);
-        const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-        const float sh[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-#pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          float v[8];
-          unpack8(__builtin_bit_cast(uint4, af[i]), v);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e], 0.f);   // == bn_apply's z
-          af[i] = __builtin_bit_cast(bf16x8, pack8(v));
-        }
-      }
       // PMD_CONV_SETPRIO (A/B knob): raise the wave's issue priority around the MFMA cluster
       // (cdna_hip_programming.md T5: keeps hipcc from moving MFMAs in among the loads)
       if constexpr (PMD_CONV_SETPRIO) __builtin_amdgcn_s_setprio(1);
@@ -1310,7 +1276,7 @@ static int conv_impl() {
 }
 
 template <int BM, int BN, int BK, int NST, bool DGRAD, bool STATS, bool DMA, bool MF32 = false,
-          int WM = 2, int WN = 2, bool P8 = false, bool HALO = false, bool PRO = false>
+          int WM = 2, int WN = 2, bool P8 = false, bool HALO = false>
 static void launch_k(const ConvArgs& a, hipStream_t st) {
   const bool ph2 = DGRAD && a.stride == 2;
   const int Mgrid = ph2 ? a.N * ((a.OH + 1) >> 1) * ((a.OW + 1) >> 1) : a.M;
@@ -1330,8 +1296,8 @@ static void launch_k(const ConvArgs& a, hipStream_t st) {
       hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, NST, DGRAD, STATS, DMA, MF32, WM, WN, P8, HALO, 0>), grid,
                          block, 0, st, a);
   } else {
-    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, NST, DGRAD, STATS, DMA, MF32, WM, WN, P8, HALO, 0, false, 0,
-                                          PRO>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, BK, NST, DGRAD, STATS, DMA, MF32, WM, WN, P8, HALO, 0>), grid,
+                       block, 0, st, a);
   }
 }
 
@@ -1666,11 +1632,6 @@ static void launch_sel(const ConvArgs& a, hipStream_t st) {
   }
 }
 
-// BN-apply prologue parameters of the NEXT conv_igemm_launch on this thread (experiment
-// API: conv_fwd_pro in bind.cpp sets it around one forward launch)
-static thread_local const float* g_pro_p = nullptr;
-void conv_set_prologue(const float* p) { g_pro_p = p; }
-
 static int conv_igemm_launch_b(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* stats, int N, int H,
                                int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
                                bool dgrad, const bf16_t* addend, const uint8_t* addend_mask,
@@ -1726,34 +1687,6 @@ static int conv_igemm_launch_b(const bf16_t* src, const bf16_t* wt, bf16_t* out,
   a.Kg = R * S * Cs;
   a.f8_sa = nullptr;
   a.f8_sb = nullptr;
-  a.pro_p = g_pro_p;
-  if (g_pro_p) {
-    // BN-apply prologue (experiment): plain 1x1 forward on the 128-row LDS-DMA tiles
-    if (dgrad || R != 1 || S != 1 || stride != 1 || pad != 0 || batch != 1 || Cs % 32 || Cs > 512) return 7;
-    if (Nout <= 64) {
-      if (stats) launch_k<128, 64, 32, 3, false, true, true, false, 2, 2, false, false, true>(a, st);
-      else launch_k<128, 64, 32, 3, false, false, true, false, 2, 2, false, false, true>(a, st);
-    } else {
-      if (stats) launch_k<128, 128, 32, 2, false, true, true, false, 2, 2, false, false, true>(a, st);
-      else launch_k<128, 128, 32, 2, false, false, true, false, 2, 2, false, false, true>(a, st);
-    }
-    return 0;
-  }
-  // short-reduction 1x1 stride-1 convolutions: the persistent streaming kernel
-  // (kernels/conv1x1_stream.hip) when the policy selects it for this pass
-  const int s1p = conv1x1_policy();
-  if (R == 1 && S == 1 && stride == 1 && pad == 0 && batch == 1 && (dgrad ? s1p >= 1 : s1p >= 2)) {
-    static int cus = 0;
-    if (!cus) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-        cus = 256;
-    }
-    if (conv1x1_stream_launch(src, wt, out, a.M, Cs, Nout, dgrad, stats, stats ? shift : nullptr, addend,
-                              a.addend_mask, bnr, st, cus) == 0)
-      return 0;
-  }
   if (dgrad) {
     if (stats) launch_sel<true, true>(a, st);
     else launch_sel<true, false>(a, st);

@@ -31,17 +31,6 @@ int winograd_filter_launch(const bf16_t* wk, bf16_t* U, int K, int Cp, bool flip
 int winograd_input_launch(const bf16_t* x, bf16_t* V, int N, int H, int W, int C, hipStream_t st);
 int winograd_output_launch(const bf16_t* M, bf16_t* y, float* stats, int N, int H, int W, int K,
                            hipStream_t st, const float* shift = nullptr);
-// Persistent streaming 1x1 (stride 1) conv for short reductions (kernels/conv1x1_stream.hip):
-// policy 0 off, 1 data gradients, 2 data gradients + forwards; bn: force 64 / 128 (0 auto)
-void conv1x1_set_policy(int p);
-int conv1x1_policy();
-void conv1x1_set_bn(int bn);
-long long conv1x1_launches();
-int conv1x1_stream_bn(int KR, int Nout, int nE, int nM);
-void conv_set_prologue(const float* p);  // BN-apply prologue of the next conv forward (experiment)
-int conv1x1_stream_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, int M, int KR, int Nout, bool dgrad,
-                          float* stats, const float* shift, const bf16_t* addend, const uint8_t* addend_mask,
-                          const BnReduceArgs* bnr, hipStream_t st, int cus);
 void conv_set_impl(int impl);
 void conv_wgrad_set_impl(int impl);
 void conv_set_tile(int t);

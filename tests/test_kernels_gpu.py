@@ -789,146 +789,6 @@ def test_tuning_table_roundtrip(tmp_path):
     assert _C.conv_autotune_entries() == 2 and torch.equal(y, y2)
 
 
-# ----------------------------------------------------------- streaming 1x1 conv
-# (N, H, C = dX channels / fwd output channels, K = dY channels / fwd input channels,
-#  addend, addend mask, fused BN-reduce sets)
-S1_CASES = [
-    (3, 7, 64, 64, True, False, 0),       # M = 147: ragged 16-row tiles, 64-row block tiles
-    (4, 28, 256, 64, True, True, 2),      # l1b2.conv1 shape class (2 BN sets + both masks)
-    (4, 28, 256, 64, True, True, 1),
-    (4, 28, 64, 256, False, False, 1),    # conv3 dgrad class (no addend)
-    (4, 28, 256, 128, True, False, 1),
-    (8, 14, 512, 128, True, True, 2),
-    (8, 14, 512, 256, True, False, 1),
-    (8, 14, 1024, 256, True, True, 1),
-    (2, 9, 128, 128, False, False, 0),    # plain dgrad, M = 162
-]
-
-
-def _s1_expect(KR, Nout, nE, nM, bn):
-    """1 when the streaming kernel has a plan for this problem under column tile bn (the
-    launcher's own planner, conv1x1_stream_bn), else 0 (the tiled kernel runs instead)."""
-    from pytorch_multiprocessing_distributed_amd.ops.native import C as _C
-    _C.conv1x1_set_bn(bn)
-    try:
-        return 1 if _C.conv1x1_stream_bn(KR, Nout, nE, nM) else 0
-    finally:
-        _C.conv1x1_set_bn(0)
-
-
-def _s1_run(fn, policy, bn):
-    from pytorch_multiprocessing_distributed_amd.ops.native import C as _C
-    _C.conv1x1_set_policy(policy)
-    _C.conv1x1_set_bn(bn)
-    try:
-        n0 = _C.conv1x1_launches()
-        r = fn()
-        torch.cuda.synchronize()
-        return r, _C.conv1x1_launches() - n0
-    finally:
-        _C.conv1x1_set_policy(0)
-        _C.conv1x1_set_bn(0)
-
-
-@pytest.mark.parametrize("bn", [0, 64, 128])
-@pytest.mark.parametrize("case", S1_CASES, ids=lambda c: "N%d_H%d_C%d_K%d_a%d%d_s%d" % c)
-def test_conv1x1_stream_dgrad(case, bn):
-    """The persistent streaming 1x1 dgrad (kernels/conv1x1_stream.hip) == the tiled
-    implicit-GEMM kernel with the same fused epilogue (addend + mask, BN-backward reduce
-    over 1-2 sets) and == the fp32 oracle; ragged M; every legal column tile."""
-    HP = _hp()
-    torch.manual_seed(11)
-    N, H, C, K, add, amask, nsets = case
-    dy = torch.randn(N, H, H, K, device=DEV).to(torch.bfloat16)
-    w = (torch.randn(K, C, 1, 1, device=DEV) / K ** 0.5).contiguous(memory_format=torch.channels_last)
-    wp = HP.conv_weight(w, torch.bfloat16, C, True)
-    xshape = (N, H, H, C)
-    addend = torch.randn(N, H, H, C, device=DEV).to(torch.bfloat16) if add else None
-    am = None
-    if amask:
-        _, am = HP.bn_apply(torch.randn(N, H, H, C, device=DEV).to(torch.bfloat16),
-                            torch.stack([torch.zeros(C, device=DEV), torch.ones(C, device=DEV),
-                                         torch.ones(C, device=DEV), torch.zeros(C, device=DEV)]).contiguous(),
-                            relu=True)
-    sets, mk = [], None
-    for _ in range(nsets):
-        yb = torch.randn(N, H, H, C, device=DEV).to(torch.bfloat16)
-        pb = torch.stack([torch.randn(C, device=DEV) * 0.1, torch.rand(C, device=DEV) + 0.5,
-                          torch.rand(C, device=DEV), torch.randn(C, device=DEV)]).contiguous()
-        sets.append((yb, pb))
-    if nsets:
-        _, mk = HP.bn_apply(sets[0][0], sets[0][1], relu=True)
-
-    def run():
-        if nsets:
-            dx, reds = HP.conv_dgrad(dy, wp, xshape, 1, 0, addend, bnred=(mk, sets), addend_mask=am)
-            return dx, [HP.stats_collapse(r).view(2, C) for r in reds]
-        return HP.conv_dgrad(dy, wp, xshape, 1, 0, addend, addend_mask=am), []
-    (dx_t, red_t), n_t = _s1_run(run, 0, 0)
-    (dx_s, red_s), n_s = _s1_run(run, 1, bn)
-    assert n_t == 0
-    want_n = _s1_expect(K, C, (1 if add else 0) + nsets, (1 if add and amask else 0) + (1 if nsets else 0), bn)
-    if bn == 0 or bn == 64:
-        assert want_n == 1, "every ResNet 1x1 dgrad class must have a streaming plan"
-    assert n_s == want_n, n_s
-    _close_norm(dx_s, dx_t, CONV_REL_L2)
-    _close(dx_s, dx_t, 2e-2)
-    # oracle: fp32 dgrad + gated addend, masked by the BN ReLU bits
-    dxr = TP.conv_dgrad(dy, TP.conv_weight(w, torch.bfloat16, C), xshape, 1, 0).float()
-    if add:
-        ga = addend.float()
-        if amask:
-            bits = (am.view(-1, 1).int() >> torch.arange(8, device=DEV).view(1, 8)) & 1
-            ga = ga * bits.view(ga.shape).float()
-        dxr = dxr + ga
-    if nsets:
-        bits = (mk.view(-1, 1).int() >> torch.arange(8, device=DEV).view(1, 8)) & 1
-        dxr = dxr * bits.view(dxr.shape).float()
-    _close_norm(dx_s, dxr, CONV_REL_L2)
-    # BN-backward reduce: the streaming kernel sums the STORED (bf16-rounded, masked) dz --
-    # exact against fp32 sums of its own output; the tiled kernel sums the fp32 values
-    # before rounding, so the two differ by the bf16 rounding of dz (a random ~2^-9 per
-    # term: ~2e-3 of a cancelling channel sum), which bounds their mutual check
-    for (yb, pb), a_, b_ in zip(sets, red_s, red_t):
-        dz = dx_s.float().reshape(-1, C)
-        ref = torch.stack([dz.sum(0), (dz * (yb.float().reshape(-1, C) - pb[0])).sum(0) * pb[1]])
-        scale = ref.abs().max().item()
-        torch.testing.assert_close(a_, ref, rtol=1e-4, atol=1e-4 * scale)
-        assert (b_ - ref).norm() / ref.norm() < 5e-3
-
-
-@pytest.mark.parametrize("bn", [0, 64, 128])
-@pytest.mark.parametrize("shape", [(3, 7, 64, 64), (4, 28, 64, 256), (4, 28, 256, 64), (8, 14, 1024, 256),
-                                   (4, 28, 512, 128), (2, 9, 128, 128)],
-                         ids=lambda s: "N%d_H%d_Cin%d_K%d" % s)
-def test_conv1x1_stream_fwd_stats(shape, bn):
-    """Streaming 1x1 forward with the BN-statistics epilogue (sums about a shift) ==
-    the tiled kernel and the fp32 oracle; statistics == the oracle's."""
-    HP = _hp()
-    torch.manual_seed(12)
-    N, H, Cin, K = shape
-    x = torch.randn(N, H, H, Cin, device=DEV).to(torch.bfloat16)
-    w = (torch.randn(K, Cin, 1, 1, device=DEV) / Cin ** 0.5).contiguous(memory_format=torch.channels_last)
-    wp = HP.conv_weight(w, torch.bfloat16, Cin, True)
-    shift = torch.randn(K, device=DEV) * 0.05
-
-    def run():
-        y, st = HP.conv_fwd(x, wp, 1, 0, shift)
-        return y, HP.stats_collapse(st).view(2, K)
-    (y_t, s_t), n_t = _s1_run(run, 0, 0)
-    (y_s, s_s), n_s = _s1_run(run, 2, bn)
-    assert n_t == 0 and n_s == _s1_expect(Cin, K, 0, 0, bn), n_s
-    if Cin <= 256 and bn != 128:
-        assert n_s == 1
-    _close_norm(y_s, y_t, CONV_REL_L2)
-    yr, _ = TP.conv_fwd(x, TP.conv_weight(w, torch.bfloat16, Cin), 1, 0, False)
-    _close_norm(y_s, yr, CONV_REL_L2)
-    d = y_s.float().reshape(-1, K) - shift
-    want = torch.stack([d.sum(0), (d * d).sum(0)])
-    torch.testing.assert_close(s_s, want, rtol=2e-3, atol=2e-3 * want.abs().max().item())
-    torch.testing.assert_close(s_s, s_t, rtol=2e-3, atol=2e-3 * want.abs().max().item())
-
-
 def test_wgrad_deferred_grouped_reduce_matches_immediate():
     """Deferred split-K reductions (wgrad_set_defer + ONE grouped wgrad_flush launch, as a
     block backward issues them on the side stream) == each weight gradient reducing on its
@@ -958,30 +818,3 @@ def test_wgrad_deferred_grouped_reduce_matches_immediate():
     torch.cuda.synchronize()
     for o, r in zip(outs, ref):
         assert torch.equal(o, r)
-
-
-@pytest.mark.parametrize("C,K,H", [(64, 256, 9), (128, 512, 7), (32, 64, 5)])
-def test_conv_fwd_bn_prologue(C, K, H):
-    """BN-apply prologue experiment (conv_igemm_kernel<..., PRO>): the 1x1 forward of
-    relu(y * scale + shift) formed on the A fragments == the conv of bn_apply's z, and ==
-    the fp32 oracle; statistics match; ragged M; a 64-column tile (K = 64)."""
-    from pytorch_multiprocessing_distributed_amd.ops.native import C as _C
-    HP = _hp()
-    torch.manual_seed(21)
-    N = 3
-    y = (torch.randn(N, H, H, C, device=DEV) * 2 + 0.5).to(torch.bfloat16)
-    p = torch.stack([torch.zeros(C, device=DEV), torch.ones(C, device=DEV),
-                     torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.5]).contiguous()
-    w = (torch.randn(K, C, 1, 1, device=DEV) / C ** 0.5).contiguous(memory_format=torch.channels_last)
-    wp = HP.conv_weight(w, torch.bfloat16, C, True)
-    shift = torch.randn(K, device=DEV) * 0.05
-    z, _ = HP.bn_apply(y, p, relu=True)
-    ref, st_ref = _C.conv_fwd(z, wp[0], 1, 0, True, None, shift)
-    out, st = _C.conv_fwd_pro(y, wp[0], p, True, None, shift)
-    _close_norm(out, ref, CONV_REL_L2)
-    zr = torch.relu(y.float() * p[2] + p[3]).to(torch.bfloat16)
-    assert torch.equal(z, zr)
-    oracle = (zr.float().reshape(-1, C) @ w.float().reshape(K, C).t()).reshape(out.shape)
-    _close_norm(out, oracle, CONV_REL_L2)
-    a_, b_ = HP.stats_collapse(st).view(2, K), HP.stats_collapse(st_ref).view(2, K)
-    torch.testing.assert_close(a_, b_, rtol=2e-3, atol=2e-3 * b_.abs().max().item())
