@@ -256,7 +256,7 @@ Tensor conv_dgrad(Tensor dy, Tensor wkt, int64_t H, int64_t W, int64_t stride, i
                   c10::optional<Tensor> bn_y0, c10::optional<Tensor> bn_p0,
                   c10::optional<Tensor> bn_red0, c10::optional<Tensor> bn_y1,
                   c10::optional<Tensor> bn_p1, c10::optional<Tensor> bn_red1,
-                  c10::optional<Tensor> addend_mask) {
+                  c10::optional<Tensor> addend_mask, c10::optional<Tensor> addend_bias) {
   CHECK_DEV(dy); CHECK_BF16(dy); CHECK_CONT(dy);
   CHECK_DEV(wkt); CHECK_BF16(wkt); CHECK_CONT(wkt);
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), K = dy.size(3);
@@ -284,12 +284,16 @@ Tensor conv_dgrad(Tensor dy, Tensor wkt, int64_t H, int64_t W, int64_t stride, i
   if (fused) {
     auto chk_set = [&](const c10::optional<Tensor>& y, const c10::optional<Tensor>& p,
                        const c10::optional<Tensor>& r, int t) {
-      TORCH_CHECK(y && y->defined() && p && p->defined() && r && r->defined(), "bn reduce set incomplete");
-      CHECK_BF16(*y); CHECK_CONT(*y); CHECK_F32(*p); CHECK_F32(*r); CHECK_CONT(*r); CHECK_CONT(*p);
-      TORCH_CHECK(y->sizes() == dx.sizes(), "bn reduce: y must match dx");
+      // y may be None: a sum-only reduce (row 1 = -mean * invstd * sum dz), see conv_igemm.hip
+      TORCH_CHECK(p && p->defined() && r && r->defined(), "bn reduce set incomplete");
+      CHECK_F32(*p); CHECK_F32(*r); CHECK_CONT(*r); CHECK_CONT(*p);
+      if (y && y->defined()) {
+        CHECK_BF16(*y); CHECK_CONT(*y);
+        TORCH_CHECK(y->sizes() == dx.sizes(), "bn reduce: y must match dx");
+      }
       TORCH_CHECK(p->numel() == 4 * Cp, "bn reduce: params must be [4, C]");
       TORCH_CHECK(r->numel() == pmd_slots() * 2 * Cp, "bn reduce: red must be [slots, 2, C]");
-      bnr.y[t] = bfp(*y);
+      bnr.y[t] = (y && y->defined()) ? bfp(*y) : nullptr;
       bnr.p[t] = p->data_ptr<float>();
       bnr.red[t] = r->data_ptr<float>();
     };
@@ -301,10 +305,19 @@ Tensor conv_dgrad(Tensor dy, Tensor wkt, int64_t H, int64_t W, int64_t stride, i
       bnr.mask = bn_mask->data_ptr<uint8_t>();
     }
   }
+  const float* abias = nullptr;
+  if (addend_bias && addend_bias->defined()) {
+    TORCH_CHECK(add, "addend_bias needs an addend");
+    CHECK_DEV(*addend_bias); CHECK_F32(*addend_bias); CHECK_CONT(*addend_bias);
+    TORCH_CHECK(addend_bias->numel() == Cp, "addend_bias must be fp32 [C]");
+    abias = addend_bias->data_ptr<float>();
+  }
   // the gathered operand is dy (spatial P x Q, K channels); output spatial is H x W
+  pmd::conv_set_addend_bias(abias);
   const int rc = pmd::conv_igemm_launch(bfp(dy), bfp(wkt), bfp_mut(dx), nullptr, N, P, Q, K, (int)H,
                                         (int)W, Cp, R, S, (int)stride, (int)pad, true, add, amask,
                                         fused ? &bnr : nullptr, cur_stream(), nullptr);
+  pmd::conv_set_addend_bias(nullptr);
   CHECK_RC(rc, "conv_dgrad");
   return dx;
 }
@@ -345,12 +358,16 @@ Tensor conv_dgrad_fp8(Tensor dyq, Tensor wtq, Tensor sdy, Tensor sw, int64_t H, 
   if (fused) {
     auto chk_set = [&](const c10::optional<Tensor>& y, const c10::optional<Tensor>& p,
                        const c10::optional<Tensor>& r, int t) {
-      TORCH_CHECK(y && y->defined() && p && p->defined() && r && r->defined(), "bn reduce set incomplete");
-      CHECK_BF16(*y); CHECK_CONT(*y); CHECK_F32(*p); CHECK_F32(*r); CHECK_CONT(*r); CHECK_CONT(*p);
-      TORCH_CHECK(y->sizes() == dx.sizes(), "bn reduce: y must match dx");
+      // y may be None: a sum-only reduce (row 1 = -mean * invstd * sum dz), see conv_igemm.hip
+      TORCH_CHECK(p && p->defined() && r && r->defined(), "bn reduce set incomplete");
+      CHECK_F32(*p); CHECK_F32(*r); CHECK_CONT(*r); CHECK_CONT(*p);
+      if (y && y->defined()) {
+        CHECK_BF16(*y); CHECK_CONT(*y);
+        TORCH_CHECK(y->sizes() == dx.sizes(), "bn reduce: y must match dx");
+      }
       TORCH_CHECK(p->numel() == 4 * Cp, "bn reduce: params must be [4, C]");
       TORCH_CHECK(r->numel() == pmd_slots() * 2 * Cp, "bn reduce: red must be [slots, 2, C]");
-      bnr.y[t] = bfp(*y);
+      bnr.y[t] = (y && y->defined()) ? bfp(*y) : nullptr;
       bnr.p[t] = p->data_ptr<float>();
       bnr.red[t] = r->data_ptr<float>();
     };
@@ -413,6 +430,75 @@ Tensor conv_wgrad(Tensor dy, Tensor x, int64_t R, int64_t S, int64_t stride, int
   CHECK_RC(rc, "conv_wgrad");
   keep_ws(ws);
   return dw;
+}
+
+// ---- linear-BN backward (kernels/bnlin.hip, ops/functional.py _bnlin_final)
+static void chk_wk(const Tensor& wk) {
+  CHECK_DEV(wk); CHECK_BF16(wk); CHECK_CONT(wk);
+  TORCH_CHECK(wk.dim() == 4 && wk.size(1) == 1 && wk.size(2) == 1, "bnlin: 1x1 weight image [K,1,1,Cp]");
+}
+static void chk_kc(const Tensor& t, int64_t K, int64_t C, const char* what) {
+  CHECK_DEV(t); CHECK_F32(t);
+  TORCH_CHECK(t.numel() == K * C && t.stride(-1) == 1 && (t.dim() < 2 || t.stride(0) == C), what,
+              ": fp32 [K][C] rows expected");
+}
+
+std::vector<Tensor> bnlin_coeff(Tensor red, c10::optional<Tensor> count, double count_h, Tensor gamma, Tensor params,
+                                Tensor wk, int64_t C) {
+  chk_wk(wk);
+  const int K = wk.size(0), Cp = wk.size(3);
+  CHECK_DEV(red); CHECK_F32(red); CHECK_CONT(red); CHECK_F32(gamma); CHECK_CONT(gamma);
+  CHECK_F32(params); CHECK_CONT(params);
+  TORCH_CHECK(red.numel() == 2 * K && gamma.numel() == K && params.numel() == 4 * K && C <= Cp,
+              "bnlin_coeff: shapes");
+  const float* cnt = nullptr;
+  if (count && count->defined()) { CHECK_F32(*count); cnt = count->data_ptr<float>(); }
+  c10::DeviceGuard g(wk.device());
+  Tensor gm = torch::empty({C, 1, 1, C}, wk.options());
+  Tensor bias = torch::empty({C}, wk.options().dtype(torch::kFloat32));
+  Tensor abc = torch::empty({3, K}, wk.options().dtype(torch::kFloat32));
+  CHECK_RC(pmd::bnlin_coeff_launch(red.data_ptr<float>(), cnt, (float)count_h, gamma.data_ptr<float>(),
+                                   params.data_ptr<float>(), bfp(wk), bfp_mut(gm), bias.data_ptr<float>(),
+                                   abc.data_ptr<float>(), K, (int)C, Cp, cur_stream()),
+           "bnlin_coeff");
+  return {gm, bias, abc};
+}
+
+Tensor bnlin_dimg(Tensor gamma, Tensor params, Tensor wk, int64_t C) {
+  chk_wk(wk);
+  const int K = wk.size(0), Cp = wk.size(3);
+  CHECK_F32(gamma); CHECK_CONT(gamma); CHECK_F32(params); CHECK_CONT(params);
+  TORCH_CHECK(gamma.numel() == K && params.numel() == 4 * K && C <= Cp, "bnlin_dimg: shapes");
+  c10::DeviceGuard g(wk.device());
+  Tensor wkt_a = torch::empty({C, 1, 1, K}, wk.options());
+  CHECK_RC(pmd::bnlin_dimg_launch(gamma.data_ptr<float>(), params.data_ptr<float>(), bfp(wk), bfp_mut(wkt_a), K,
+                                  (int)C, Cp, cur_stream()),
+           "bnlin_dimg");
+  return wkt_a;
+}
+
+Tensor colsum(Tensor x) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONT(x);
+  const int C = x.size(-1);
+  c10::DeviceGuard g(x.device());
+  Tensor out = pmd_zeros({C}, x.options().dtype(torch::kFloat32));
+  CHECK_RC(pmd::colsum_launch(bfp(x), out.data_ptr<float>(), x.numel() / C, C, cur_stream()), "colsum");
+  return out;
+}
+
+void bnlin_wgrad(Tensor out, Tensor abc, Tensor T, Tensor wk, Tensor gz, Tensor cs) {
+  chk_wk(wk);
+  const int K = wk.size(0), Cp = wk.size(3);
+  const int C = T.numel() / K;
+  chk_kc(T, K, C, "bnlin_wgrad T");
+  chk_kc(out, K, C, "bnlin_wgrad out");
+  chk_kc(gz, C, C, "bnlin_wgrad gz");
+  CHECK_F32(abc); CHECK_CONT(abc); CHECK_F32(cs); CHECK_CONT(cs);
+  TORCH_CHECK(abc.numel() == 3 * K && cs.numel() == C, "bnlin_wgrad: abc / colsum");
+  c10::DeviceGuard g(wk.device());
+  CHECK_RC(pmd::bnlin_wgrad_launch(out.data_ptr<float>(), abc.data_ptr<float>(), T.data_ptr<float>(), bfp(wk),
+                                   gz.data_ptr<float>(), cs.data_ptr<float>(), K, C, Cp, cur_stream()),
+           "bnlin_wgrad");
 }
 
 // FP8 weight gradient: dyq e5m2 [N,P,Q,K] (scale sdy) x xq e4m3 [N,H,W,C] (scale sx);
@@ -1055,7 +1141,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wkt"), py::arg("H"), py::arg("W"),
         py::arg("stride"), py::arg("pad"), py::arg("addend"), py::arg("bn_mask"), py::arg("bn_y0"),
         py::arg("bn_p0"), py::arg("bn_red0"), py::arg("bn_y1"), py::arg("bn_p1"), py::arg("bn_red1"),
-        py::arg("addend_mask"));
+        py::arg("addend_mask"), py::arg("addend_bias") = py::none());
+  m.def("bnlin_coeff", &bnlin_coeff, py::arg("red"), py::arg("count"), py::arg("count_h"), py::arg("gamma"),
+        py::arg("params"), py::arg("wk"), py::arg("C"),
+        "linear-BN backward coefficients -> [G image, bias, abc]");
+  m.def("bnlin_dimg", &bnlin_dimg, py::arg("gamma"), py::arg("params"), py::arg("wk"), py::arg("C"),
+        "linear-BN backward: the gamma*invstd-scaled transposed dgrad image [C,1,1,K]");
+  m.def("colsum", &colsum, "fp32 column sums of an NHWC bf16 activation");
+  m.def("bnlin_wgrad", &bnlin_wgrad, "linear-BN backward weight gradient combine (+= into out)");
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("R"), py::arg("S"), py::arg("stride"),
         py::arg("pad"), py::arg("out") = py::none());
   m.def("bn_finalize", &bn_finalize, py::arg("sums"), py::arg("count"), py::arg("gamma"), py::arg("beta"),

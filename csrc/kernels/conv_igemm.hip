@@ -44,6 +44,7 @@ struct ConvArgs {
   const float* shift;  // K = the BN statistics shift [Nout] (nullable: 0), see bn_moments
   const bf16_t* addend;  // optional [M][Nout] tensor added to the output (grad accumulation)
   const uint8_t* addend_mask;  // optional ReLU bitmask gating the addend (identity-path dz = dout*mask)
+  const float* addend_bias;    // optional fp32 [Nout] added with the addend (dgrad only)
   // optional fused BatchNorm-backward reduce over the (final, bf16) output tile
   // (dgrad of the conv that CONSUMED a BN+ReLU output): per channel n
   //   red[slot][0][n] += sum dz,  red[slot][1][n] += sum dz * (y - mean) * invstd
@@ -1026,6 +1027,15 @@ __global__ __launch_bounds__(64 * WM * WN,
   constexpr int G = ITERS < GW ? ITERS : GW;
   static_assert(ITERS % G == 0, "epilogue groups");
   const bool has_add = DGRAD && a.addend, has_amask = DGRAD && a.addend_mask;
+  // per-channel addend bias (the linear-BN backward's constant term, ops/functional.py
+  // _bnlin_backward): this thread's 8 output channels are fixed for the whole epilogue
+  float abias[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) abias[e] = 0.f;
+  if (DGRAD && a.addend_bias && n0 + (tid % (BN / 8)) * 8 < a.Nout) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) abias[e] = a.addend_bias[n0 + (tid % (BN / 8)) * 8 + e];
+  }
   // Per thread the chunk column (cc, n) is fixed and the tile row advances by
   // RSTEP per iteration, so for every layer but the strided dgrads the global
   // element offset is one base plus a uniform stride: no per-row integer
@@ -1081,7 +1091,7 @@ __global__ __launch_bounds__(64 * WM * WN,
         mb[g] = a.bn_mask ? a.bn_mask[off[g] >> 3] : 0xffu;
 #pragma unroll
         for (int t = 0; t < NBA; ++t)
-          if (t < nbn) yy[t][g] = ld16n<NT_EPI_Y>(a.bn_y[t] + off[g]);
+          if (t < nbn) yy[t][g] = a.bn_y[t] ? ld16n<NT_EPI_Y>(a.bn_y[t] + off[g]) : make_uint4(0, 0, 0, 0);
       }
     }
 #pragma unroll
@@ -1095,7 +1105,7 @@ __global__ __launch_bounds__(64 * WM * WN,
 #pragma unroll
         for (int e = 0; e < 8; ++e) ga[e] = ((am[g] >> e) & 1u) ? ga[e] : 0.f;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] += ga[e];
+        for (int e = 0; e < 8; ++e) f[e] += ga[e] + abias[e];
         o = pack8(f);
       }
       if (nbn) {
@@ -1632,6 +1642,11 @@ static void launch_sel(const ConvArgs& a, hipStream_t st) {
   }
 }
 
+// per-channel fp32 bias added with the addend by the NEXT dgrad launch on this thread
+// (conv_dgrad in bind.cpp sets it around one launch; the linear-BN backward's constant term)
+static thread_local const float* g_addend_bias = nullptr;
+void conv_set_addend_bias(const float* b) { g_addend_bias = b; }
+
 static int conv_igemm_launch_b(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* stats, int N, int H,
                                int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
                                bool dgrad, const bf16_t* addend, const uint8_t* addend_mask,
@@ -1653,6 +1668,7 @@ static int conv_igemm_launch_b(const bf16_t* src, const bf16_t* wt, bf16_t* out,
   a.shift = stats ? shift : nullptr;
   a.addend = addend;
   a.addend_mask = addend ? addend_mask : nullptr;
+  a.addend_bias = (dgrad && addend) ? g_addend_bias : nullptr;
   a.bn_mask = nullptr;
   for (int t = 0; t < 2; ++t) {
     a.bn_y[t] = nullptr;
@@ -1660,7 +1676,9 @@ static int conv_igemm_launch_b(const bf16_t* src, const bf16_t* wt, bf16_t* out,
     a.bn_red[t] = nullptr;
   }
   if (bnr) {
-    if (!dgrad || !bnr->y[0] || !bnr->p[0] || !bnr->red[0]) return 5;
+    // y[t] may be null: a sum-only reduce (row 1 gets -mean * invstd * sum dz; the linear-BN
+    // backward adds the y-dependent part from the weight gradient, ops/functional.py)
+    if (!dgrad || !bnr->p[0] || !bnr->red[0]) return 5;
     a.bn_mask = bnr->mask;
     for (int t = 0; t < 2; ++t) {
       a.bn_y[t] = bnr->y[t];

@@ -944,6 +944,19 @@ static void plan(const WgradArgs& a, const WgradCfg& cfg, int* splits_out, int* 
   // keep the partial workspace bounded (<= 96 MiB)
   const long long per = (long long)a.K * a.Kg * 4;
   while (splits > 1 && per * splits > (96ll << 20)) --splits;
+  // PMD_WGRAD_SLAB_FRAC=f (A/B knob, 0 = off): the split partials (written, then read back by
+  // the reduction: 2 x splits x K x Kg x 4 bytes) may cost at most f x the operand bytes
+  // M x (K + C) x 2 -- fewer, longer splits for the deep layers whose partial traffic
+  // rivals their operands (l3/l4: K x Kg up to 2.4M elements at M = 12,544-50,176)
+  static const double slab_frac = [] {
+    const char* e = getenv("PMD_WGRAD_SLAB_FRAC");
+    return e ? atof(e) : 0.0;
+  }();
+  if (slab_frac > 0.0) {
+    const double op = (double)a.M * (a.K + a.C) * 2.0;
+    const int cap = (int)(slab_frac * op / (2.0 * (double)per));
+    if (splits > (cap < 1 ? 1 : cap)) splits = cap < 1 ? 1 : cap;
+  }
   if (splits < 1) splits = 1;
   const int cps = (chunks + splits - 1) / splits;
   *cps_out = cps;

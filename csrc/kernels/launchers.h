@@ -31,6 +31,15 @@ int winograd_filter_launch(const bf16_t* wk, bf16_t* U, int K, int Cp, bool flip
 int winograd_input_launch(const bf16_t* x, bf16_t* V, int N, int H, int W, int C, hipStream_t st);
 int winograd_output_launch(const bf16_t* M, bf16_t* y, float* stats, int N, int H, int W, int K,
                            hipStream_t st, const float* shift = nullptr);
+// linear-BN backward helpers (kernels/bnlin.hip)
+int bnlin_coeff_launch(const float* red, const float* count, float count_h, const float* gamma, const float* params,
+                       const bf16_t* wk, bf16_t* g, float* bias, float* abc, int K, int C, int Cp, hipStream_t st);
+int bnlin_dimg_launch(const float* gamma, const float* params, const bf16_t* wk, bf16_t* wkt_a, int K, int C, int Cp,
+                      hipStream_t st);
+int colsum_launch(const bf16_t* x, float* out, long long M, int C, hipStream_t st);
+int bnlin_wgrad_launch(float* out, const float* abc, const float* T, const bf16_t* wk, const float* gz,
+                       const float* cs, int K, int C, int Cp, hipStream_t st);
+void conv_set_addend_bias(const float* b);  // fp32 [Nout] bias of the next dgrad's addend (this thread)
 void conv_set_impl(int impl);
 void conv_wgrad_set_impl(int impl);
 void conv_set_tile(int t);

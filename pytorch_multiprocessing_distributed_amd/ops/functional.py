@@ -460,6 +460,47 @@ class _WgradSide:
         self.ready.append(w)
         return None
 
+    def fork(self, fn, keep=()):
+        """``fn()`` on the side stream after everything issued so far on the main stream;
+        returns (its result, the event the main stream must wait on before using it; None
+        when it ran here)."""
+        if not self.on:
+            return fn(), None
+        self.side.wait_stream(self.main)
+        with torch.cuda.stream(self.side):
+            r = fn()
+        for t in keep:
+            if t is not None and t.is_cuda:
+                t.record_stream(self.side)
+        ev = torch.cuda.Event()
+        ev.record(self.side)
+        return r, ev
+
+    def run(self, w, fn, keep=()):
+        """Like :meth:`wgrad` for a weight gradient computed by ``fn(target)`` (target = the
+        arena view [K,R,S,C] fp32 it must ADD into); ``keep``: tensors made on the main stream
+        that ``fn`` reads.  Without an arena target (or the side stream) ``fn`` runs here on a
+        zeroed tensor, which is returned for autograd ([K,C,R,S] channels_last); else None."""
+        tgt = _grad_target(w)
+        if tgt is None:
+            out = torch.zeros(w.shape[0], w.shape[2], w.shape[3], w.shape[1], dtype=torch.float32,
+                              device=w.device)
+            fn(out)
+            return out.permute(0, 3, 1, 2)
+        if not self.on:
+            fn(tgt.permute(0, 2, 3, 1))
+            _ready(w)
+            return None
+        _claim(w)
+        self.side.wait_stream(self.main)
+        with torch.cuda.stream(self.side):
+            fn(tgt.permute(0, 2, 3, 1))
+        for t in keep:
+            if t is not None and t.is_cuda:
+                t.record_stream(self.side)
+        self.ready.append(w)
+        return None
+
     def join(self):
         """End of the block backward: the join is DEFERRED by one block -- the
         main stream waits for the PREVIOUS block's side work (whose wgrads have
@@ -539,6 +580,28 @@ def bn_stat_shift(bn):
 
 
 _BN_SHIFT = os.environ.get("PMD_BN_SHIFT", "1") != "0"
+# Linear-BN backward for a block's final BN (PMD_BNLIN: "auto" = the large 1x1 stride-1 conv3
+# outputs of the l1 / l2 stages, "all" = every eligible identity block, "0" = off): the BN
+# backward is folded through the 1x1 conv that produced its input (y = z W^T), so neither the
+# BN-backward elementwise pass nor the producer's statistics epilogue ever reads y, and dy is
+# never materialised -- see _bnlin_final.
+_BNLIN = os.environ.get("PMD_BNLIN", "auto")
+_BNLIN_MIN = int(os.environ.get("PMD_BNLIN_MIN", str(200704 * 512)))   # M * K of the BN input
+
+
+def _bnlin_eligible(conv_m, yf, x, training, fuse, shortcut, f8):
+    if _BNLIN == "0" or not (training and fuse) or shortcut is not None or f8 is not None:
+        return False
+    ks = conv_m.kernel_size if isinstance(conv_m.kernel_size, tuple) else (conv_m.kernel_size,) * 2
+    st = conv_m.stride if isinstance(conv_m.stride, tuple) else (conv_m.stride,) * 2
+    if ks != (1, 1) or st != (1, 1):
+        return False
+    return _BNLIN == "all" or yf.numel() >= _BNLIN_MIN
+
+
+# a BN site whose reduce a dgrad epilogue fused receives dz already gated by its ReLU mask:
+# the elementwise pass and the identity-path addend skip re-reading the mask (PMD_PREMASKED=0: re-read)
+_PREMASKED = os.environ.get("PMD_PREMASKED", "1") != "0"
 
 
 def _shift_of(bn):
@@ -654,6 +717,10 @@ def _bn_backward(P, dout, mask, relu, training, sync, count, y1, p1, bn1, y2=Non
     if pre is not None:
         r1 = pre[0]
         r2 = pre[1] if y2 is not None else None
+        # the dgrad that fused this reduce stored dz * mask (kernels/conv_igemm.hip epilogue):
+        # dout is already gated by the ReLU mask, so the elementwise pass skips the mask bytes
+        if _PREMASKED:
+            relu = False
     else:
         r1 = P.bn_bwd_reduce(dout, mask, y1, p1, relu)
         r2 = P.bn_bwd_reduce(dout, mask, y2, p2, relu) if y2 is not None else None
@@ -938,6 +1005,80 @@ def bn_relu_maxpool(y, stats, bn):
     return _StemPoolFn.apply((bn, bn.training, _pop_shift(stats)), y, stats, bn.weight, bn.bias)
 
 
+# ------------------------------------------------- linear-BN backward (final BN)
+def _bnlin_prep(P, bn, p, wpack, z):
+    """Forward-time part of the linear-BN backward (see _bnlin_final), on the weight-gradient
+    side stream while the forward continues: the diag(gamma * invstd)-scaled dgrad image of the
+    conv3 weights and the z statistics the weight gradient needs (z^T z, colsum z).  Returns
+    (dgrad pack, Gz, colsum, event or None)."""
+    c = z.shape[-1]
+    wk = wpack[0]
+
+    def work():
+        return (P.bnlin_dimg(bn.weight, p, wk, c), P.conv_wgrad(z, z, (c, 1, 1, c), 1, 0), P.colsum(z))
+    if not (z.is_cuda and _WGRAD_STREAM["on"] and not _state["force_torch"]):
+        return (*work(), None)
+    side = _wgrad_stream(z.device)
+    main = torch.cuda.current_stream(z.device)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        dpack, gz, cs = work()
+    z.record_stream(side)
+    p.record_stream(side)
+    for t in dpack:
+        if t is not None:
+            t.record_stream(main)
+    ev = torch.cuda.Event()
+    ev.record(side)
+    return dpack, gz, cs, ev
+
+
+def _bnlin_final(P, dz, pre, training, sync, count, z, wpack, conv_m, bn, p, rec_prev, side, put, prep):
+    """Backward of ``out = relu(BN(y) + x)`` with ``y = z W^T`` (a 1x1 stride-1 conv) that never
+    materialises ``dy`` (the BN passes are the step's bytes): no BN-backward
+    elementwise pass.  ``dz = dout * relu_mask`` arrives from the next block's dgrad together
+    with its fused statistics (slots ``pre[0]``: sum dz, sum dz*xhat).  With
+    dy = A dz + B y + Cc per channel k (A = gamma*invstd from the forward; B, Cc from the
+    global sums after the collapse / SyncBN exchange, which run exactly as at every site):
+
+      D      = dz (diag(A) W)       plain dgrad on the forward-prepared scaled image
+      dz_in  = D + z (W^T diag(B) W) + Cc W     one small GEMM of z (reduction = C) with D as
+                                                its addend, the bias and the previous BN's fused
+                                                reduce in its epilogue  (B y W = z W^T B W)
+      dW     = diag(A) T + diag(B) W (z^T z) + Cc (x) colsum(z),   T = dz^T z   (side stream:
+               T is the conv's own weight-gradient GEMM; z^T z, colsum z from the forward)
+
+    W is the bf16 compute image the forward used, so y = z W^T is the forward's product before
+    its bf16 rounding -- the one difference from the elementwise path.  Returns (dz_in, the
+    fused reduce of ``rec_prev``'s BN, [d_gamma, d_beta] for params not in the arena)."""
+    wk = wpack[0]
+    c = z.shape[-1]
+    dpack, gz, cs, ev = prep
+    T, _ = side.fork(lambda: P.conv_wgrad(dz, z, tuple(wk.shape), 1, 0), keep=(dz, z))
+    if ev is not None:
+        torch.cuda.current_stream(dz.device).wait_event(ev)
+    dmain = P.conv_dgrad(dz, dpack, tuple(z.shape), 1, 0)             # dz diag(A) W
+    state = {}
+
+    def lin(red, cnt):
+        gpack, bias, abc = P.bnlin_coeff(red, cnt, bn.weight, p, wk, c)
+        _hin, _wp, y_, p_, z_ = rec_prev
+        dx, red_ = P.conv_dgrad(z, gpack, tuple(z.shape), 1, 0, dmain, bnred=(z_, [(y_, p_)]),
+                                addend_bias=bias)
+        state["pre"] = _Pre(red_, _after_dgrad_event(dx, sync if training else None))
+        state["abc"] = abc
+        return dx
+
+    dx, _, _, g = _bn_backward(P, dz, None, False, training, sync, count, dz, p, bn,
+                               pre=pre, elemt_fn=lin)
+    abc = state["abc"]
+
+    def wgrad(out):
+        P.bnlin_wgrad_(out, abc, T, wk, gz, cs)
+    put(conv_m.weight, side.run(conv_m.weight, wgrad, keep=(abc, wk)))
+    return dx, state["pre"], g
+
+
 # ------------------------------------------------------------ residual block
 class _BnSite:
     """Hand-off between two consecutive residual blocks for the fused BN reduce:
@@ -1072,6 +1213,9 @@ class _ResidualBlockFn(torch.autograd.Function):
         fuse = _state["fuse_bnred"] and training
         ctx.in_site = getattr(x, "_pmd_bnsite", None) if fuse else None
         ctx.out_site = None
+        # linear-BN backward of the final BN (no elementwise pass, see _bnlin_final)
+        ctx.bnlin = _bnlin_eligible(fconv, yf, x, training, fuse, shortcut, f8) and h.shape[-1] == wpf[0].shape[-1]
+        ctx.bnlin_prep = _bnlin_prep(P, fbn, pf, wpf, h) if ctx.bnlin else None
         if fuse:
             ctx.out_site = _BnSite(omask, [(yf, pf)] + ([(ys, ps)] if shortcut is not None else []))
             out._pmd_bnsite = ctx.out_site
@@ -1151,12 +1295,16 @@ class _ResidualBlockFn(torch.autograd.Function):
         else:
             # the identity-path gradient dout * relu_mask is NOT materialised: the first
             # stage's dgrad epilogue adds dout gated by the mask bits
-            dyf, _, _, g = _bn_backward(P, dout, omask, True, training, sync, countf,
-                                        yf, pf, fbn, pre=pre,
-                                        q8=(gsite(nst, fbn), None))
-            dres = (dout, omask)
-        put(fbn.weight, g[0])
-        put(fbn.bias, g[1])
+            if not (ctx.bnlin and pre is not None):
+                dyf, _, _, g = _bn_backward(P, dout, omask, True, training, sync, countf,
+                                            yf, pf, fbn, pre=pre,
+                                            q8=(gsite(nst, fbn), None))
+            # dout pre-masked by the fused reduce (see _bn_backward): no addend mask either
+            dres = (dout, None if (pre is not None and _PREMASKED) else omask)
+        lin = shortcut is None and ctx.bnlin and pre is not None
+        if not lin:
+            put(fbn.weight, g[0])
+            put(fbn.bias, g[1])
         fuse = _state["fuse_bnred"] and training
 
         f8img = ctx.f8img
@@ -1181,12 +1329,20 @@ class _ResidualBlockFn(torch.autograd.Function):
             _hin, _wp, y_, p_, z_ = rec
             dx_, red_ = dgrad(dy_, wp_, conv_m_, shape, addend, bnred=(z_, [(y_, p_)]))
             return dx_, _Pre(red_, _after_dgrad_event(dx_, sync if training else None))
-        chk("dyf", dyf)
         side = _WgradSide(dout)
-        # --- final conv (its wgrad forks to the side stream first: it overlaps the dgrad)
-        put(fconv.weight, side.wgrad(P, dyf, hlast, wpf, fconv.stride, fconv.padding, fconv.weight,
-                                     qins[nst]))
-        dh, pre_k = dgrad_fused(dyf, wpf, fconv, tuple(hlast.shape), recs[-1])
+        if lin:
+            # linear-BN backward of the final BN through the 1x1 conv3 (no y, no dy)
+            dh, pre_k, g = _bnlin_final(P, dout, pre, training, sync, countf, hlast, wpf, fconv,
+                                        fbn, pf, recs[-1], side, put, ctx.bnlin_prep)
+            ctx.bnlin_prep = None
+            put(fbn.weight, g[0])
+            put(fbn.bias, g[1])
+        else:
+            chk("dyf", dyf)
+            # --- final conv (its wgrad forks to the side stream first: it overlaps the dgrad)
+            put(fconv.weight, side.wgrad(P, dyf, hlast, wpf, fconv.stride, fconv.padding, fconv.weight,
+                                         qins[nst]))
+            dh, pre_k = dgrad_fused(dyf, wpf, fconv, tuple(hlast.shape), recs[-1])
         chk("dh(final)", dh)
         dx = None
         # --- conv->BN->ReLU stages in reverse; the block-input gradient of the

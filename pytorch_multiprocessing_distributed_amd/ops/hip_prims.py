@@ -74,7 +74,7 @@ def conv_fwd(x, wpack, stride, pad, want_stats):
     return _C.conv_fwd(x, wpack[0], int(stride), int(pad), False, None)[0], None
 
 
-def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None, bnred=None, addend_mask=None):
+def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None, bnred=None, addend_mask=None, addend_bias=None):
     """dX (+ addend [* relu bitmask addend_mask]).  ``bnred = (mask, [(y, params)] or
     [(y1, p1), (y2, p2)])`` fuses the BN-backward reduce of dX into the epilogue
     and returns ``(dx, [slot buffers])`` (same contract as :func:`bn_bwd_reduce`)."""
@@ -82,13 +82,14 @@ def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None, bnred=None, addend_
         raise RuntimeError("dgrad image was not prepared (input did not require grad)")
     if bnred is None:
         return _C.conv_dgrad(dy, wpack[1], int(x_shape[1]), int(x_shape[2]), int(stride), int(pad),
-                             addend, None, None, None, None, None, None, None, addend_mask)
+                             addend, None, None, None, None, None, None, None, addend_mask, addend_bias)
     mask, sets = bnred
-    bufs = [_acquire(y.shape[-1], y.device) for y, _ in sets]
+    # a set's y may be None (sum-only reduce of the linear-BN backward): size from the params
+    bufs = [_acquire(p.shape[-1], dy.device) for _, p in sets]
     (y0, p0), (y1, p1) = sets[0], (sets[1] if len(sets) > 1 else (None, None))
     dx = _C.conv_dgrad(dy, wpack[1], int(x_shape[1]), int(x_shape[2]), int(stride), int(pad),
                        addend, mask, y0, p0, bufs[0], y1, p1, bufs[1] if len(bufs) > 1 else None,
-                       addend_mask)
+                       addend_mask, addend_bias)
     return dx, bufs
 
 
@@ -99,7 +100,7 @@ def conv_dgrad_fp8(dyq, sdy, wtq, sw, x_shape, stride, pad, addend=None, bnred=N
         return _C.conv_dgrad_fp8(dyq, wtq, sdy, sw, int(x_shape[1]), int(x_shape[2]), int(stride), int(pad),
                                  addend, addend_mask=addend_mask)
     mask, sets = bnred
-    bufs = [_acquire(y.shape[-1], y.device) for y, _ in sets]
+    bufs = [_acquire(p.shape[-1], dyq.device) for _, p in sets]
     (y0, p0), (y1, p1) = sets[0], (sets[1] if len(sets) > 1 else (None, None))
     dx = _C.conv_dgrad_fp8(dyq, wtq, sdy, sw, int(x_shape[1]), int(x_shape[2]), int(stride), int(pad),
                            addend, mask, y0, p0, bufs[0], y1, p1, bufs[1] if len(bufs) > 1 else None,
@@ -164,6 +165,25 @@ def bn_apply(y1, p1, res=None, y2=None, p2=None, relu=True, fp8=None, fp8_only=F
 def bn_bwd_reduce(dout, mask, y, p, relu):
     buf = _acquire(y.shape[-1], y.device)
     return _C.bn_bwd_reduce(dout, mask, y, p, bool(relu), buf)
+
+
+# ------------------------------------------------- linear-BN backward (torch_prims notes)
+def bnlin_coeff(red, count, gamma, p, wk, c):
+    cnt_t = count if torch.is_tensor(count) else None
+    r = _C.bnlin_coeff(red, cnt_t, 0.0 if cnt_t is not None else float(count), gamma.detach(), p, wk, int(c))
+    return (None, r[0]), r[1], r[2]          # G as a dgrad pack (the kernel reads wpack[1]), bias, abc
+
+
+def bnlin_dimg(gamma, p, wk, c):
+    return (wk, _C.bnlin_dimg(gamma.detach(), p, wk, int(c)))   # dgrad pack: (forward image, scaled image)
+
+
+def colsum(x):
+    return _C.colsum(x)
+
+
+def bnlin_wgrad_(out, abc, T, wk, gz, cs):
+    _C.bnlin_wgrad(out, abc, T, wk, gz, cs)
 
 
 def bn_bwd_elemt(dout, mask, y, p, gamma, red, count, relu, want_dzm=False, q8=None, q8_only=False):

@@ -59,7 +59,7 @@ def conv_fwd(x, wpack, stride, pad, want_stats):
     return y, stats
 
 
-def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None, bnred=None, addend_mask=None):
+def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None, bnred=None, addend_mask=None, addend_bias=None):
     """dX (+ addend).  With ``bnred = (mask, [(y, params), ...])`` also returns
     the BN-backward reduce of the result for each set (the fused form of
     ``bn_bwd_reduce(dx, mask, y, params, relu=mask is not None)``)."""
@@ -70,10 +70,14 @@ def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None, bnred=None, addend_
     dx = _nhwc(dx)
     if addend is not None:
         dx = dx + (_dzm(addend, addend_mask, True) if addend_mask is not None else _f(addend))
-    dx = dx.to(dy.dtype)
+        if addend_bias is not None:
+            dx = dx + _f(addend_bias)
     if bnred is None:
-        return dx
+        return dx.to(dy.dtype)
     mask, sets = bnred
+    # same contract as the gfx950 kernel: the output IS the BN site's dz, stored already
+    # gated by that site's ReLU mask (its consumers then skip the mask)
+    dx = (_dzm(dx, mask, True) if mask is not None else dx).to(dy.dtype)
     return dx, [bn_bwd_reduce(dx, mask, y, p, mask is not None) for y, p in sets]
 
 
@@ -169,11 +173,62 @@ def _dzm(dout, mask, relu):
 
 
 def bn_bwd_reduce(dout, mask, y, p, relu):
-    """-> fp32 [2, C]: (sum dzm, sum dzm*xhat), dzm = dout * relu_mask."""
-    c = y.shape[-1]
+    """-> fp32 [2, C]: (sum dzm, sum dzm*xhat), dzm = dout * relu_mask.  ``y=None``: the
+    sum-only form of the linear-BN backward, (sum dzm, -mean * invstd * sum dzm)."""
+    c = dout.shape[-1]
     d = _dzm(dout, mask, relu).reshape(-1, c)
+    if y is None:
+        s = d.sum(0)
+        return torch.stack([s, -(p[0] * p[1]) * s])
     xhat = (_f(y).reshape(-1, c) - p[0]) * p[1]
     return torch.stack([d.sum(0), (d * xhat).sum(0)])
+
+
+# ------------------------------------------------- linear-BN backward (1x1 conv -> BN)
+# y = z W^T (the 1x1 conv feeding the BN, W = its compute weight image), so dy never needs
+# to be formed (ops/functional.py _bnlin_final):
+#   dy = A dz + B y + Cc   =>   dz_in = dz (A W) + z (W^T B W) + Cc W     (dgrad, bias)
+#                               dW    = A T + B (W Gz) + Cc (x) colsum(z), T = dz^T z, Gz = z^T z
+def _w2(wk, c):
+    return _f(wk).reshape(wk.shape[0], -1)[:, :c]
+
+
+def bnlin_coeff(red, count, gamma, p, wk, c):
+    """Global (sum dz, sum dz*xhat) -> (G [c,1,1,c]: image of W^T diag(B) W (symmetric: the
+    dgrad image of the z G GEMM), bias [c] = Cc W (fp32), abc [3, K] fp32 = A, B, Cc)."""
+    cnt = _f(count) if torch.is_tensor(count) else float(count)
+    red = _f(red).reshape(2, -1)
+    inv, mean = p[1], p[0]
+    a = _f(gamma.detach()) * inv
+    mdy, mdyx = red[0] / cnt, red[1] / cnt
+    b = -a * inv * mdyx
+    cc = a * (mean * inv * mdyx - mdy)
+    w = _w2(wk, c)
+    g = (w.t() @ (b[:, None] * w)).reshape(c, 1, 1, c).to(wk.dtype)
+    return (g,), cc @ w, torch.stack([a, b, cc])      # G as a dgrad pack (this module reads wpack[0])
+
+
+def bnlin_dimg(gamma, p, wk, c):
+    """The dgrad weight pack of diag(gamma * invstd) W (forward quantities only)."""
+    w = _w2(wk, c)
+    a = _f(gamma.detach()) * p[1]
+    return ((a[:, None] * w).reshape(w.shape[0], 1, 1, c).to(wk.dtype),)   # this module's dgrad reads wpack[0]
+
+
+def colsum(x):
+    """fp32 [C] column sums of an NHWC activation."""
+    return _f(x).reshape(-1, x.shape[-1]).sum(0)
+
+
+def bnlin_wgrad_(out, abc, T, wk, gz, cs):
+    """out [K,1,1,C] (fp32, += ) = A T + B (W Gz) + Cc (x) colsum."""
+    k = T.shape[0]
+    t = _f(T).reshape(k, -1)
+    c = t.shape[1]
+    w = _w2(wk, c)
+    g = _f(gz).reshape(c, c)
+    dw = abc[0][:, None] * t + abc[1][:, None] * (w @ g) + abc[2][:, None] * _f(cs)[None, :]
+    out.add_(dw.reshape(out.shape).to(out.dtype))
 
 
 def bn_bwd_elemt(dout, mask, y, p, gamma, red, count, relu, want_dzm=False):
