@@ -66,6 +66,17 @@ struct ConvArgs {
   // (byte pointers behind the bf16_t* fields); acc is scaled by 1 / (f8_sa * f8_sb)
   const float* f8_sa;
   const float* f8_sb;
+  // BN-apply epilogue of a forward conv without statistics (the block-final BN folded into
+  // its conv3, ops/functional.py _bnfold): out = relu(bf16(acc) * ap_p[2][n] + ap_p[3][n]
+  // [+ ap_res]) and the ReLU bitmask ap_mask -- the math of bn_apply_kernel<1> on the tile
+  const float* ap_p;
+  const bf16_t* ap_res;
+  uint8_t* ap_mask;
+  // dot-only fused reduce (dgrad kernel, 1 set): the GEMM tile is a RECOMPUTED BN input y,
+  // bn_y[0] is dz, and only red[slot][1][n] += invstd[n] * sum dz * y is accumulated (zero
+  // mean, no sum row); out may be null (no store) -- the y part of sum dz * xhat that the
+  // sum-only reduce of the producing dgrad left out
+  int red_dot;
 };
 typedef __attribute__((ext_vector_type(8))) int i32x8_c;
 
@@ -999,7 +1010,7 @@ __global__ __launch_bounds__(64 * WM * WN,
         bsum[t][e] = bdot[t][e] = 0.f;
         bmean[t][e] = 0.f;
       }
-    if (nbn && n < a.Nout) {
+    if (nbn && n < a.Nout && !a.red_dot) {
 #pragma unroll
       for (int t = 0; t < NBA; ++t)
         if (t < nbn)
@@ -1036,6 +1047,24 @@ __global__ __launch_bounds__(64 * WM * WN,
 #pragma unroll
     for (int e = 0; e < 8; ++e) abias[e] = a.addend_bias[n0 + (tid % (BN / 8)) * 8 + e];
   }
+  // BN-apply epilogue (forward without statistics only: the statistics kernels keep their
+  // register budget): this thread's 8 channels' scale / shift, loaded once
+  constexpr bool CAN_APPLY = !DGRAD && !STATS && !MF32 && !F8;
+  const bool apply = CAN_APPLY && a.ap_p;
+  const bool ap_has_res = apply && a.ap_res;
+  float asc[CAN_APPLY ? 8 : 1], ash[CAN_APPLY ? 8 : 1];
+  if constexpr (CAN_APPLY) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) asc[e] = ash[e] = 0.f;
+    const int na = n0 + (tid % (BN / 8)) * 8;
+    if (apply && na < a.Nout) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        asc[e] = a.ap_p[2 * a.Nout + na + e];
+        ash[e] = a.ap_p[3 * a.Nout + na + e];
+      }
+    }
+  }
   // Per thread the chunk column (cc, n) is fixed and the tile row advances by
   // RSTEP per iteration, so for every layer but the strided dgrads the global
   // element offset is one base plus a uniform stride: no per-row integer
@@ -1057,7 +1086,9 @@ __global__ __launch_bounds__(64 * WM * WN,
   const size_t off0 = (size_t)(m0 + row0) * a.Nout + (n_ok ? n : 0);
   const size_t ostep = (size_t)a.Nout;
   // fully unrolled (A/B: +0.8% step over the rolled loop with per-row index
-  // math; an LDS lookup table expanding the ReLU mask bytes measured -2.7%)
+  // math; an LDS lookup table expanding the ReLU mask bytes measured -2.7%).
+  // Skipped by a statistics-only forward (out == nullptr: the stats are complete).
+  if (a.out || nbn)
 #pragma unroll
   for (int it0 = 0; it0 < ITERS; it0 += G) {
     size_t off[G];
@@ -1087,6 +1118,7 @@ __global__ __launch_bounds__(64 * WM * WN,
         ad[g] = ld16n<NT_EPI_A>(a.addend + off[g]);
         am[g] = has_amask ? a.addend_mask[off[g] >> 3] : 0xffu;
       }
+      if (ap_has_res && ok[g]) ad[g] = ld16n<NT_EPI_A>(a.ap_res + off[g]);
       if (nbn && ok[g]) {
         mb[g] = a.bn_mask ? a.bn_mask[off[g] >> 3] : 0xffu;
 #pragma unroll
@@ -1108,6 +1140,24 @@ __global__ __launch_bounds__(64 * WM * WN,
         for (int e = 0; e < 8; ++e) f[e] += ga[e] + abias[e];
         o = pack8(f);
       }
+      if constexpr (CAN_APPLY) {
+        if (apply) {
+          // bn_apply_kernel<1, relu> on the bf16-rounded tile value
+          float f[8], r[8];
+          unpack8(o, f);
+          if (ap_has_res) unpack8(ad[g], r);
+          uint32_t bits = 0;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float t = f[e] * asc[e] + ash[e];
+            if (ap_has_res) t += r[e];
+            bits |= (uint32_t)(t > 0.f) << e;
+            f[e] = fmaxf(t, 0.f);
+          }
+          o = pack8(f);
+          if (a.ap_mask) a.ap_mask[off[g] >> 3] = (uint8_t)bits;
+        }
+      }
       if (nbn) {
         // the output IS a BN site's dz; every consumer gates it with this same ReLU
         // mask (BN backward, identity-path addend), so store dzm = dz * mask (bit-exact
@@ -1120,10 +1170,12 @@ __global__ __launch_bounds__(64 * WM * WN,
       }
       // PMD_CONV_ST_PASS (A/B): 0 = both passes as PMD_NT_MASK says, 1 = forward outputs only,
       // 2 = data-gradient outputs only
-      if constexpr (PMD_CONV_ST_PASS == 0 || (PMD_CONV_ST_PASS == 1) == !DGRAD)
-        st16n<NT_CONV_ST>(a.out + off[g], o);
-      else
-        *reinterpret_cast<uint4*>(a.out + off[g]) = o;
+      if (a.out) {
+        if constexpr (PMD_CONV_ST_PASS == 0 || (PMD_CONV_ST_PASS == 1) == !DGRAD)
+          st16n<NT_CONV_ST>(a.out + off[g], o);
+        else
+          *reinterpret_cast<uint4*>(a.out + off[g]) = o;
+      }
       if (nbn) {
         float d[8];
         unpack8(o, d);
@@ -1168,7 +1220,7 @@ __global__ __launch_bounds__(64 * WM * WN,
         float acc2 = 0.f;
         for (int r = col; r < NT; r += CPR) acc2 += part[r * PSTR + k];
         const int n = n0 + col * 8 + (k & 7);
-        if (n < a.Nout && !(PMD_TIMING_NO_ATOMICS & 2))
+        if (n < a.Nout && !(PMD_TIMING_NO_ATOMICS & 2) && !(a.red_dot && k < 8))
           atomicAdd(a.bn_red[t] + ((size_t)((m0 / BM) % kStatSlots) * 2 + (k >> 3)) * a.Nout + n, acc2);
       }
       __syncthreads();
@@ -1603,8 +1655,17 @@ static void launch_sel(const ConvArgs& a, hipStream_t st) {
     int c = -1;
     {
       std::lock_guard<std::mutex> lk(g_tune_mu);
-      auto it = g_tune.find(k);
-      if (it != g_tune.end()) c = it->second;
+      if (!DGRAD && !STATS && a.ap_p) {
+        // BN-apply pass: the tile of the same shape's statistics pass (its tuning-table entry)
+        TuneKey ks = k;
+        ks.v[12] = 1;
+        auto it = g_tune.find(ks);
+        if (it != g_tune.end()) c = it->second;
+      }
+      if (c < 0) {
+        auto it = g_tune.find(k);
+        if (it != g_tune.end()) c = it->second;
+      }
     }
     if (c < 0) {
       hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -1646,6 +1707,17 @@ static void launch_sel(const ConvArgs& a, hipStream_t st) {
 // (conv_dgrad in bind.cpp sets it around one launch; the linear-BN backward's constant term)
 static thread_local const float* g_addend_bias = nullptr;
 void conv_set_addend_bias(const float* b) { g_addend_bias = b; }
+// BN-apply epilogue / dot-only reduce of the NEXT launch on this thread (see ConvArgs)
+static thread_local const float* g_ap_p = nullptr;
+static thread_local const bf16_t* g_ap_res = nullptr;
+static thread_local uint8_t* g_ap_mask = nullptr;
+static thread_local int g_red_dot = 0;
+void conv_set_fwd_apply(const float* p, const bf16_t* res, uint8_t* mask) {
+  g_ap_p = p;
+  g_ap_res = p ? res : nullptr;
+  g_ap_mask = p ? mask : nullptr;
+}
+void conv_set_red_dot(int on) { g_red_dot = on; }
 
 static int conv_igemm_launch_b(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* stats, int N, int H,
                                int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
@@ -1656,7 +1728,19 @@ static int conv_igemm_launch_b(const bf16_t* src, const bf16_t* wt, bf16_t* out,
   if (Nout % 8 != 0) return 2;
   if (stride != 1 && stride != 2) return 3;
   if (batch < 1 || batch > 65535 || (batch > 1 && (dgrad || stats || addend || bnr))) return 6;
-  ConvArgs a;
+  ConvArgs a{};
+  // thread-local epilogue extras of this one launch (conv_set_fwd_apply / conv_set_red_dot)
+  if (g_ap_p) {
+    if (dgrad || stats || batch > 1) return 7;   // the apply epilogue is a plain-forward mode
+    a.ap_p = g_ap_p;
+    a.ap_res = g_ap_res;
+    a.ap_mask = g_ap_mask;
+  }
+  if (g_red_dot) {
+    if (!dgrad || !bnr || bnr->red[1] || !bnr->y[0] || bnr->mask || addend) return 8;
+    a.red_dot = 1;
+  }
+  if (!out && !(stats || (bnr && a.red_dot))) return 9;   // no store only for stats / dot passes
   a.batch = batch;
   a.bs_src = bs_src;
   a.bs_wt = bs_wt;

@@ -599,6 +599,32 @@ def _bnlin_eligible(conv_m, yf, x, training, fuse, shortcut, f8):
     return _BNLIN == "all" or yf.numel() >= _BNLIN_MIN
 
 
+# BN fold (training forward of the identity blocks whose final BN takes the linear-BN backward):
+# conv3 runs twice -- statistics only (no output), then again with the BN-apply epilogue
+# (+ identity, ReLU, mask) -- so the conv3 output y is never written nor read back; the
+# backward recomputes the y part of sum dz * xhat from z (_bnfold_dot).  Opt-in (PMD_BNFOLD=1):
+# it removes 0.8 GB per l1 site but measured at parity (profiles/bnfold_r05.txt) -- the short-
+# reduction conv3 is latency-bound (79 us without its store vs 88 with it at l1), so the second
+# GEMM pass costs what the y round trip saved.
+_BNFOLD = os.environ.get("PMD_BNFOLD", "0") == "1"
+
+
+class _YShape:
+    """Shape / device stand-in of a BN input that is never materialised (BN fold)."""
+    __slots__ = ("shape", "device", "dtype")
+
+    def __init__(self, shape, device, dtype):
+        self.shape = torch.Size(shape)
+        self.device = device
+        self.dtype = dtype
+
+    def numel(self):
+        n = 1
+        for d in self.shape:
+            n *= d
+        return n
+
+
 # a BN site whose reduce a dgrad epilogue fused receives dz already gated by its ReLU mask:
 # the elementwise pass and the identity-path addend skip re-reading the mask (PMD_PREMASKED=0: re-read)
 _PREMASKED = os.environ.get("PMD_PREMASKED", "1") != "0"
@@ -1079,6 +1105,15 @@ def _bnlin_final(P, dz, pre, training, sync, count, z, wpack, conv_m, bn, p, rec
     return dx, state["pre"], g
 
 
+def _bnfold_dot(P, z, wpack, dz, p, pre, sync):
+    """BN fold, backward: the dgrad that produced ``dz`` took the sum-only reduce of the final BN
+    (its input y was never stored); add ``invstd * sum dz * y`` with y = z W^T recomputed into the
+    same slots (before their collapse / SyncBN exchange), and move the reduce's ready event."""
+    P.conv_bn_dot_(z, wpack, dz, p, pre[0])
+    if getattr(pre, "event", None) is not None:
+        pre.event = _after_dgrad_event(dz, sync)
+
+
 # ------------------------------------------------------------ residual block
 class _BnSite:
     """Hand-off between two consecutive residual blocks for the fused BN reduce:
@@ -1176,7 +1211,18 @@ class _ResidualBlockFn(torch.autograd.Function):
         fconv, fbn = final
         wpf = _conv_weight(P, fconv, x.dtype, h.shape[-1], True)
         hq_f = used_q(fconv, hq, h)
-        yf, stf = _conv_fwd_any(P, f8, h, hq_f, wpf, fconv, _stats_req(fbn, training))
+        fuse = _state["fuse_bnred"] and training
+        # BN fold: the final conv's output is never written (see _BNFOLD)
+        fold = (_BNFOLD and shortcut is None and h.shape[-1] == wpf[0].shape[-1]
+                and _bnlin_eligible(fconv, _YShape((*h.shape[:-1], wpf[0].shape[0]), h.device, h.dtype),
+                                    x, training, fuse, shortcut, f8))
+        if fold:
+            yf = None
+            stf = P.conv_fwd_stats(h, wpf, fconv.stride, fconv.padding, _stats_req(fbn, training))
+            yproxy = _YShape((*h.shape[:-1], wpf[0].shape[0]), h.device, h.dtype)
+        else:
+            yf, stf = _conv_fwd_any(P, f8, h, hq_f, wpf, fconv, _stats_req(fbn, training))
+            yproxy = yf
         qins.append(hq_f if f8w else None)
         # e4m3 copy of the block output only if its consumer -- the next block's first
         # conv, which has this block's first-conv kernel shape -- runs in fp8
@@ -1190,6 +1236,10 @@ class _ResidualBlockFn(torch.autograd.Function):
             qins.append(xq_s if f8w else None)
             pf, ps, countf = _bn_forward_params(P, yf, stf, fbn, training, sync, ys, sts, sbn)
             r = P.bn_apply(yf, pf, None, ys, ps, relu=True, **({"fp8": osite} if osite else {}))
+        elif fold:
+            wps = None
+            pf, _, countf = _bn_forward_params(P, yproxy, stf, fbn, training, sync)
+            r = P.conv_fwd_apply(h, wpf, fconv.stride, fconv.padding, pf, x)
         else:
             wps = None
             pf, _, countf = _bn_forward_params(P, yf, stf, fbn, training, sync)
@@ -1210,11 +1260,11 @@ class _ResidualBlockFn(torch.autograd.Function):
         # cross-block fusion: the NEXT block's first dgrad computes d(out) and can
         # reduce this block's final BN(s) in its epilogue.  The site carries what
         # it needs; the input's site (previous block) is remembered likewise.
-        fuse = _state["fuse_bnred"] and training
         ctx.in_site = getattr(x, "_pmd_bnsite", None) if fuse else None
         ctx.out_site = None
         # linear-BN backward of the final BN (no elementwise pass, see _bnlin_final)
-        ctx.bnlin = _bnlin_eligible(fconv, yf, x, training, fuse, shortcut, f8) and h.shape[-1] == wpf[0].shape[-1]
+        ctx.bnlin = fold or (_bnlin_eligible(fconv, yf, x, training, fuse, shortcut, f8)
+                             and h.shape[-1] == wpf[0].shape[-1])
         ctx.bnlin_prep = _bnlin_prep(P, fbn, pf, wpf, h) if ctx.bnlin else None
         if fuse:
             ctx.out_site = _BnSite(omask, [(yf, pf)] + ([(ys, ps)] if shortcut is not None else []))
@@ -1281,6 +1331,14 @@ class _ResidualBlockFn(torch.autograd.Function):
             return sc, am, only
         # reduce of the final BN(s), if the next block's dgrad already produced it
         pre = ctx.out_site.take(dout, P) if ctx.out_site is not None else None
+        if yf is None:
+            # BN fold: the final conv's output was never written
+            if pre is not None and ctx.bnlin:
+                # the next block's dgrad took the sum-only reduce; add the y part from z
+                _bnfold_dot(P, hlast, wpf, dout, pf, pre, sync if training else None)
+            else:
+                # no fused reduce reached this block (e.g. the network's last block): recompute y
+                yf = P.conv_fwd(hlast, wpf, fconv.stride, fconv.padding, False)[0]
         # --- final BN (+ projection BN) and the residual ReLU
         if shortcut is not None:
             sconv, sbn = shortcut
