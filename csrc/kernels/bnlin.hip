@@ -17,9 +17,11 @@ namespace pmd {
 
 // Coefficients from the global sums, then G = W^T diag(B) W and bias = Cc W.  Block c (one per
 // column of W; every block recomputes B, Cc for all K into LDS, block 0 also writes abc [3][K]):
-// wc[k] = B_k W[k][c] in LDS, then thread c' accumulates G[c][c'] = sum_k wc[k] W[k][c'] with
-// independent, coalesced loads of row k (no barrier inside the K loop -- the round-5 tiled
-// version waited one L2 round trip per 16-row chunk: 60 us per call); wave 0 reduces bias[c].
+// wc[k] = B_k W[k][c] in LDS, then G[c][q] = sum_k wc[k] W[k][q] with the K loop split over
+// S = 256 / C thread slices (C < 256) and 8 independent, coalesced row loads in flight per
+// thread (no barrier inside the K loop; this runs on the critical path of the backward,
+// where the one-slice loop was a chain of K / 4 dependent L2 round trips: 27 us per call),
+// slices combined in LDS; wave 0 reduces bias[c].
 constexpr int kLinMaxK = 2048;
 
 __global__ __launch_bounds__(256) void bnlin_coeff_kernel(const float* __restrict__ red, const float* __restrict__ count,
@@ -29,7 +31,8 @@ __global__ __launch_bounds__(256) void bnlin_coeff_kernel(const float* __restric
                                                          float* __restrict__ abc, int K, int C, int Cp) {
   extern __shared__ float lsm[];
   float* wc = lsm;          // [K]  B_k W[k][c]
-  float* cc = lsm + K;      // [K]  Cc_k
+  float* cc = lsm + K;      // [K]  Cc_k W[k][c]
+  float* part = lsm + 2 * K;  // [256] slice partials
   const int tid = threadIdx.x;
   const int c = blockIdx.x;
   const float inv_cnt = 1.f / (count ? count[0] : count_h);
@@ -48,30 +51,51 @@ __global__ __launch_bounds__(256) void bnlin_coeff_kernel(const float* __restric
     }
   }
   __syncthreads();
-  for (int q = tid; q < C; q += 256) {
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int k = 0;
-    for (; k + 4 <= K; k += 4) {
-      s0 += wc[k] * bf2f(wk[(size_t)k * Cp + q]);
-      s1 += wc[k + 1] * bf2f(wk[(size_t)(k + 1) * Cp + q]);
-      s2 += wc[k + 2] * bf2f(wk[(size_t)(k + 2) * Cp + q]);
-      s3 += wc[k + 3] * bf2f(wk[(size_t)(k + 3) * Cp + q]);
+  const int qn = C < 256 ? C : 256;               // threads per slice
+  const int S = C < 256 ? 256 / C : 1;            // K slices
+  const int q0 = tid % qn, sl = tid / qn;
+  const bool active = sl < S;
+  const int kb = (int)((long long)sl * K / S), ke = (int)((long long)(sl + 1) * K / S);
+  for (int q = q0; q < C; q += qn) {
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (active) {
+      int k = kb;
+      for (; k + 8 <= ke; k += 8) {
+        float w[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) w[u] = bf2f(wk[(size_t)(k + u) * Cp + q]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s[u] += wc[k + u] * w[u];
+      }
+      for (; k < ke; ++k) s[0] += wc[k] * bf2f(wk[(size_t)k * Cp + q]);
     }
-    for (; k < K; ++k) s0 += wc[k] * bf2f(wk[(size_t)k * Cp + q]);
-    g[(size_t)c * C + q] = f2bf((s0 + s1) + (s2 + s3));
+    const float t = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+    if (S == 1) {
+      g[(size_t)c * C + q] = f2bf(t);
+    } else {
+      part[tid] = t;   // tid = sl * qn + q (C < 256: one q per thread)
+    }
+  }
+  if (S > 1) {
+    __syncthreads();
+    if (tid < C) {
+      float t = 0.f;
+      for (int j = 0; j < S; ++j) t += part[j * qn + tid];
+      g[(size_t)c * C + tid] = f2bf(t);
+    }
   }
   if (tid < 64) {
-    float s = 0.f;
-    for (int k = tid; k < K; k += 64) s += cc[k];
-    s = wave_sum(s);
-    if (tid == 0) bias[c] = s;
+    float sb = 0.f;
+    for (int k = tid; k < K; k += 64) sb += cc[k];
+    sb = wave_sum(sb);
+    if (tid == 0) bias[c] = sb;
   }
 }
 
 int bnlin_coeff_launch(const float* red, const float* count, float count_h, const float* gamma, const float* params,
                        const bf16_t* wk, bf16_t* g, float* bias, float* abc, int K, int C, int Cp, hipStream_t st) {
   if (K < 1 || K > kLinMaxK || C < 1 || Cp < C) return 1;
-  hipLaunchKernelGGL(bnlin_coeff_kernel, dim3(C), dim3(256), sizeof(float) * 2 * (size_t)K, st, red, count, count_h,
+  hipLaunchKernelGGL(bnlin_coeff_kernel, dim3(C), dim3(256), sizeof(float) * (2 * (size_t)K + 256), st, red, count, count_h,
                      gamma, params, wk, g, bias, abc, K, C, Cp);
   return 0;
 }

@@ -884,6 +884,138 @@ __global__ __launch_bounds__(64 * WM * WN,
   }
 
   // ---- epilogue
+  constexpr int CPR = BN / 8;  // 16-B chunks per output row
+  // fused BN-backward reduce: each thread owns one 8-channel chunk column (NT % CPR == 0)
+  static_assert(NT % CPR == 0, "chunk column per thread");
+  // NB = the BN-input sets this instantiation handles (launch_k instantiates 0 / 1 / 2
+  // to the call's count): the per-set reduce state is the epilogue's register peak,
+  // so a one-set dgrad (the common case) carries half of it.  The invstd is applied
+  // once after the loop, loaded there, for the same reason.
+  constexpr int NBA = NB > 0 ? NB : 1;
+  const int nbn = (DGRAD && NB > 0 && a.bn_red[0]) ? (NB > 1 && a.bn_red[1] ? 2 : 1) : 0;
+  float bsum[NBA][8], bdot[NBA][8], bmean[NBA][8];
+  {
+    const int n = n0 + (tid % CPR) * 8;
+#pragma unroll
+    for (int t = 0; t < NBA; ++t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        bsum[t][e] = bdot[t][e] = 0.f;
+        bmean[t][e] = 0.f;
+      }
+    if (nbn && n < a.Nout && !a.red_dot) {
+#pragma unroll
+      for (int t = 0; t < NBA; ++t)
+        if (t < nbn)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bmean[t][e] = a.bn_p[t][n + e];
+    }
+  }
+  // Output rows in groups of G per thread: every global load of a group (addend,
+  // masks, BN inputs) is issued before the group's first store (the stores may
+  // alias nothing the group reads), so a thread has G x (1-3) HBM reads in
+  // flight instead of one dependent load->store chain per row.  Full-step A/B
+  // (bench/ab_so.sh): G=2 +0.6% over the serial loop, G=4 -3.6% with default-policy
+  // loads (the 4-deep register tile of activation chunks cost more than the extra
+  // latency hiding) -- but +0.5% once the epilogue operands stream non-temporal (round 3:
+  // 13,440 / 13,435 vs 13,348 / 13,386 img/s, profiles/ab_r03_nt_loads.txt).
+  constexpr int ITERS = BM * CPR / NT;
+  static_assert((BM * CPR) % NT == 0, "whole epilogue iterations");
+#ifndef PMD_EPI_G
+#define PMD_EPI_G 4
+#endif
+#ifndef PMD_F8_NB2_G
+#define PMD_F8_NB2_G PMD_EPI_G  // rows in flight of the 2-set single-stage fp8 dgrad epilogue
+#endif
+  constexpr int GW = (F8 && NST1 && NB == 2) ? PMD_F8_NB2_G : PMD_EPI_G;
+  constexpr int G = ITERS < GW ? ITERS : GW;
+  static_assert(ITERS % G == 0, "epilogue groups");
+  const bool has_add = DGRAD && a.addend, has_amask = DGRAD && a.addend_mask;
+  // per-channel addend bias (the linear-BN backward's constant term, ops/functional.py
+  // _bnlin_backward): this thread's 8 output channels are fixed for the whole epilogue
+  float abias[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) abias[e] = 0.f;
+  if (DGRAD && a.addend_bias && n0 + (tid % (BN / 8)) * 8 < a.Nout) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) abias[e] = a.addend_bias[n0 + (tid % (BN / 8)) * 8 + e];
+  }
+  // BN-apply epilogue (forward without statistics only: the statistics kernels keep their
+  // register budget): this thread's 8 channels' scale / shift, loaded once
+  constexpr bool CAN_APPLY = !DGRAD && !STATS && !MF32 && !F8;
+  const bool apply = CAN_APPLY && a.ap_p;
+  const bool ap_has_res = apply && a.ap_res;
+  float asc[CAN_APPLY ? 8 : 1], ash[CAN_APPLY ? 8 : 1];
+  if constexpr (CAN_APPLY) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) asc[e] = ash[e] = 0.f;
+    const int na = n0 + (tid % (BN / 8)) * 8;
+    if (apply && na < a.Nout) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        asc[e] = a.ap_p[2 * a.Nout + na + e];
+        ash[e] = a.ap_p[3 * a.Nout + na + e];
+      }
+    }
+  }
+  // Per thread the chunk column (cc, n) is fixed and the tile row advances by
+  // RSTEP per iteration, so for every layer but the strided dgrads the global
+  // element offset is one base plus a uniform stride: no per-row integer
+  // division / 64-bit multiply in the loop (they were ~1/3 of its VALU issue).
+  // EPI_RM: thread row group q reads rows (q >> 1) + 16 (q & 1) + 8 (it & 1) + 32 (it >> 1)
+  constexpr int RSTEP = NT / CPR;
+  static_assert(!EPI_RM || (RSTEP == 16 && ITERS % 2 == 0), "EPI_RM row order: 16 thread rows");
+  auto row_delta = [](int it) { return EPI_RM ? 8 * (it & 1) + 32 * (it >> 1) : it * RSTEP; };
+  // EPI_RM64 (8-chunk rows, 36-dword row skew): the 4 thread rows of a 32-lane read
+  // group take rows {0, 16, 24, 8} + (q >> 2), which puts both 16-lane halves of every
+  // ds_read_b128 group on 4 disjoint 16-dword bank ranges
+  const int qr = tid / CPR;
+  const int row0 = EPI_RM ? (qr >> 1) + 16 * (qr & 1)
+                          : EPI_RM64 ? (qr >> 2) + 8 * ((0x1320 >> (4 * (qr & 3))) & 0xF) : qr;
+  const int cc = tid % CPR;
+  const int n = n0 + cc * 8;
+  const bool n_ok = n < a.Nout;
+  const bool phased = DGRAD && a.stride == 2;
+  const size_t off0 = (size_t)(m0 + row0) * a.Nout + (n_ok ? n : 0);
+  const size_t ostep = (size_t)a.Nout;
+  // PMD_EPI_PF (dgrad): the first row group's global epilogue operands (addend, masks, BN
+  // inputs) are issued before the C tile is staged through LDS, so their latency overlaps
+  // the staging instead of following it.  Full-step A/B (bench/ab_so.sh, 2 rounds, one lease):
+  // 0: 13,469 / 13,468 img/s, 1: 13,538 / 13,561, 2: 13,540 / 13,563 (+0.6%, profiles/epi_pf_r05.txt)
+#ifndef PMD_EPI_PF
+#define PMD_EPI_PF 2
+#endif
+  // (1: every dgrad; 2: not the 4-wave 128-column tiles with <= 1 BN set, which it would cost
+  // their 4th wave per SIMD -- 125 -> 144 VGPRs)
+  constexpr bool PF = DGRAD && (PMD_EPI_PF == 1 || (PMD_EPI_PF == 2 && !(NW == 4 && BN == 128 && NB < 2)));
+  uint4 pf_ad[PF ? G : 1], pf_yy[NBA][PF ? G : 1];
+  uint32_t pf_am[PF ? G : 1], pf_mb[PF ? G : 1];
+  if constexpr (PF) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int row = row0 + row_delta(g);
+      const int m = m0 + row;
+      const bool okg = m < Mp && n_ok;
+      size_t o = off0 + (size_t)row_delta(g) * ostep;
+      if (phased) {
+        const int mm = okg ? m : 0;
+        const int nb = mm / ohw, rem = mm - nb * ohw;
+        const int hh = rem / OWp, ww = rem - hh * OWp;
+        o = (((size_t)nb * a.OH + 2 * hh + ph) * a.OW + 2 * ww + pw) * a.Nout + (n_ok ? n : 0);
+      }
+      if (!okg) o = 0;
+      if (has_add && okg) {
+        pf_ad[g] = ld16n<NT_EPI_A>(a.addend + o);
+        pf_am[g] = has_amask ? a.addend_mask[o >> 3] : 0xffu;
+      }
+      if (nbn && okg) {
+        pf_mb[g] = a.bn_mask ? a.bn_mask[o >> 3] : 0xffu;
+#pragma unroll
+        for (int t = 0; t < NBA; ++t)
+          if (t < nbn) pf_yy[t][g] = a.bn_y[t] ? ld16n<NT_EPI_Y>(a.bn_y[t] + o) : make_uint4(0, 0, 0, 0);
+      }
+    }
+  }
   bf16_t* Cs = lds;
   const int crow0 = wm * (BM / WM) + (lane >> 4) * 4;
   const int ccol0 = wn * (BN / WN) + (lane & 15);
@@ -991,100 +1123,6 @@ __global__ __launch_bounds__(64 * WM * WN,
       }
     }
   }
-  constexpr int CPR = BN / 8;  // 16-B chunks per output row
-  // fused BN-backward reduce: each thread owns one 8-channel chunk column (NT % CPR == 0)
-  static_assert(NT % CPR == 0, "chunk column per thread");
-  // NB = the BN-input sets this instantiation handles (launch_k instantiates 0 / 1 / 2
-  // to the call's count): the per-set reduce state is the epilogue's register peak,
-  // so a one-set dgrad (the common case) carries half of it.  The invstd is applied
-  // once after the loop, loaded there, for the same reason.
-  constexpr int NBA = NB > 0 ? NB : 1;
-  const int nbn = (DGRAD && NB > 0 && a.bn_red[0]) ? (NB > 1 && a.bn_red[1] ? 2 : 1) : 0;
-  float bsum[NBA][8], bdot[NBA][8], bmean[NBA][8];
-  {
-    const int n = n0 + (tid % CPR) * 8;
-#pragma unroll
-    for (int t = 0; t < NBA; ++t)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        bsum[t][e] = bdot[t][e] = 0.f;
-        bmean[t][e] = 0.f;
-      }
-    if (nbn && n < a.Nout && !a.red_dot) {
-#pragma unroll
-      for (int t = 0; t < NBA; ++t)
-        if (t < nbn)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) bmean[t][e] = a.bn_p[t][n + e];
-    }
-  }
-  // Output rows in groups of G per thread: every global load of a group (addend,
-  // masks, BN inputs) is issued before the group's first store (the stores may
-  // alias nothing the group reads), so a thread has G x (1-3) HBM reads in
-  // flight instead of one dependent load->store chain per row.  Full-step A/B
-  // (bench/ab_so.sh): G=2 +0.6% over the serial loop, G=4 -3.6% with default-policy
-  // loads (the 4-deep register tile of activation chunks cost more than the extra
-  // latency hiding) -- but +0.5% once the epilogue operands stream non-temporal (round 3:
-  // 13,440 / 13,435 vs 13,348 / 13,386 img/s, profiles/ab_r03_nt_loads.txt).
-  constexpr int ITERS = BM * CPR / NT;
-  static_assert((BM * CPR) % NT == 0, "whole epilogue iterations");
-#ifndef PMD_EPI_G
-#define PMD_EPI_G 4
-#endif
-#ifndef PMD_F8_NB2_G
-#define PMD_F8_NB2_G PMD_EPI_G  // rows in flight of the 2-set single-stage fp8 dgrad epilogue
-#endif
-  constexpr int GW = (F8 && NST1 && NB == 2) ? PMD_F8_NB2_G : PMD_EPI_G;
-  constexpr int G = ITERS < GW ? ITERS : GW;
-  static_assert(ITERS % G == 0, "epilogue groups");
-  const bool has_add = DGRAD && a.addend, has_amask = DGRAD && a.addend_mask;
-  // per-channel addend bias (the linear-BN backward's constant term, ops/functional.py
-  // _bnlin_backward): this thread's 8 output channels are fixed for the whole epilogue
-  float abias[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) abias[e] = 0.f;
-  if (DGRAD && a.addend_bias && n0 + (tid % (BN / 8)) * 8 < a.Nout) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) abias[e] = a.addend_bias[n0 + (tid % (BN / 8)) * 8 + e];
-  }
-  // BN-apply epilogue (forward without statistics only: the statistics kernels keep their
-  // register budget): this thread's 8 channels' scale / shift, loaded once
-  constexpr bool CAN_APPLY = !DGRAD && !STATS && !MF32 && !F8;
-  const bool apply = CAN_APPLY && a.ap_p;
-  const bool ap_has_res = apply && a.ap_res;
-  float asc[CAN_APPLY ? 8 : 1], ash[CAN_APPLY ? 8 : 1];
-  if constexpr (CAN_APPLY) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) asc[e] = ash[e] = 0.f;
-    const int na = n0 + (tid % (BN / 8)) * 8;
-    if (apply && na < a.Nout) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        asc[e] = a.ap_p[2 * a.Nout + na + e];
-        ash[e] = a.ap_p[3 * a.Nout + na + e];
-      }
-    }
-  }
-  // Per thread the chunk column (cc, n) is fixed and the tile row advances by
-  // RSTEP per iteration, so for every layer but the strided dgrads the global
-  // element offset is one base plus a uniform stride: no per-row integer
-  // division / 64-bit multiply in the loop (they were ~1/3 of its VALU issue).
-  // EPI_RM: thread row group q reads rows (q >> 1) + 16 (q & 1) + 8 (it & 1) + 32 (it >> 1)
-  constexpr int RSTEP = NT / CPR;
-  static_assert(!EPI_RM || (RSTEP == 16 && ITERS % 2 == 0), "EPI_RM row order: 16 thread rows");
-  auto row_delta = [](int it) { return EPI_RM ? 8 * (it & 1) + 32 * (it >> 1) : it * RSTEP; };
-  // EPI_RM64 (8-chunk rows, 36-dword row skew): the 4 thread rows of a 32-lane read
-  // group take rows {0, 16, 24, 8} + (q >> 2), which puts both 16-lane halves of every
-  // ds_read_b128 group on 4 disjoint 16-dword bank ranges
-  const int qr = tid / CPR;
-  const int row0 = EPI_RM ? (qr >> 1) + 16 * (qr & 1)
-                          : EPI_RM64 ? (qr >> 2) + 8 * ((0x1320 >> (4 * (qr & 3))) & 0xF) : qr;
-  const int cc = tid % CPR;
-  const int n = n0 + cc * 8;
-  const bool n_ok = n < a.Nout;
-  const bool phased = DGRAD && a.stride == 2;
-  const size_t off0 = (size_t)(m0 + row0) * a.Nout + (n_ok ? n : 0);
-  const size_t ostep = (size_t)a.Nout;
   // fully unrolled (A/B: +0.8% step over the rolled loop with per-row index
   // math; an LDS lookup table expanding the ReLU mask bytes measured -2.7%).
   // Skipped by a statistics-only forward (out == nullptr: the stats are complete).
@@ -1114,17 +1152,25 @@ __global__ __launch_bounds__(64 * WM * WN,
         const bool sw = EPI_RM ? ((it0 + g) & 1) != 0 : ((row >> 3) & 1) != 0;
         if (sw) v[g] = make_uint4(v[g].z, v[g].w, v[g].x, v[g].y);
       }
-      if (has_add && ok[g]) {
-        ad[g] = ld16n<NT_EPI_A>(a.addend + off[g]);
-        am[g] = has_amask ? a.addend_mask[off[g] >> 3] : 0xffu;
+      if (PF && it0 == 0) {
+        ad[g] = pf_ad[g];
+        am[g] = pf_am[g];
+        mb[g] = pf_mb[g];
+#pragma unroll
+        for (int t = 0; t < NBA; ++t) yy[t][g] = pf_yy[t][g];
+      } else {
+        if (has_add && ok[g]) {
+          ad[g] = ld16n<NT_EPI_A>(a.addend + off[g]);
+          am[g] = has_amask ? a.addend_mask[off[g] >> 3] : 0xffu;
+        }
+        if (nbn && ok[g]) {
+          mb[g] = a.bn_mask ? a.bn_mask[off[g] >> 3] : 0xffu;
+#pragma unroll
+          for (int t = 0; t < NBA; ++t)
+            if (t < nbn) yy[t][g] = a.bn_y[t] ? ld16n<NT_EPI_Y>(a.bn_y[t] + off[g]) : make_uint4(0, 0, 0, 0);
+        }
       }
       if (ap_has_res && ok[g]) ad[g] = ld16n<NT_EPI_A>(a.ap_res + off[g]);
-      if (nbn && ok[g]) {
-        mb[g] = a.bn_mask ? a.bn_mask[off[g] >> 3] : 0xffu;
-#pragma unroll
-        for (int t = 0; t < NBA; ++t)
-          if (t < nbn) yy[t][g] = a.bn_y[t] ? ld16n<NT_EPI_Y>(a.bn_y[t] + off[g]) : make_uint4(0, 0, 0, 0);
-      }
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
