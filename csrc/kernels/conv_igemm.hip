@@ -987,7 +987,9 @@ __global__ __launch_bounds__(64 * WM * WN,
 #endif
   // (1: every dgrad; 2: not the 4-wave 128-column tiles with <= 1 BN set, which it would cost
   // their 4th wave per SIMD -- 125 -> 144 VGPRs)
-  constexpr bool PF = DGRAD && (PMD_EPI_PF == 1 || (PMD_EPI_PF == 2 && !(NW == 4 && BN == 128 && NB < 2)));
+  // (the BN-apply forward's residual tile likewise)
+  constexpr bool PF = (DGRAD && (PMD_EPI_PF == 1 || (PMD_EPI_PF == 2 && !(NW == 4 && BN == 128 && NB < 2)))) ||
+                      (CAN_APPLY && PMD_EPI_PF != 0);
   uint4 pf_ad[PF ? G : 1], pf_yy[NBA][PF ? G : 1];
   uint32_t pf_am[PF ? G : 1], pf_mb[PF ? G : 1];
   if constexpr (PF) {
@@ -1008,6 +1010,7 @@ __global__ __launch_bounds__(64 * WM * WN,
         pf_ad[g] = ld16n<NT_EPI_A>(a.addend + o);
         pf_am[g] = has_amask ? a.addend_mask[o >> 3] : 0xffu;
       }
+      if (ap_has_res && okg) pf_ad[g] = ld16n<NT_EPI_A>(a.ap_res + o);
       if (nbn && okg) {
         pf_mb[g] = a.bn_mask ? a.bn_mask[o >> 3] : 0xffu;
 #pragma unroll
@@ -1169,8 +1172,8 @@ __global__ __launch_bounds__(64 * WM * WN,
           for (int t = 0; t < NBA; ++t)
             if (t < nbn) yy[t][g] = a.bn_y[t] ? ld16n<NT_EPI_Y>(a.bn_y[t] + off[g]) : make_uint4(0, 0, 0, 0);
         }
+        if (ap_has_res && ok[g]) ad[g] = ld16n<NT_EPI_A>(a.ap_res + off[g]);
       }
-      if (ap_has_res && ok[g]) ad[g] = ld16n<NT_EPI_A>(a.ap_res + off[g]);
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
