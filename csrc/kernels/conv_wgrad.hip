@@ -934,10 +934,23 @@ static bool wgrad_cfg_ok(int impl, const WgradArgs& a) {
   return true;
 }
 
+// PMD_WGRAD_BIG_MIN (A/B knob): the minimum split-K block count of the 8-wave tiles (256).  One
+// 8-wave 256x256 block per CU holds 128 KB of LDS for the whole kernel (~150 us at l3/l4), so no
+// main-stream conv block (>= 34 KB) fits next to it until it retires.
+static int big_min_blocks() {
+  static const int v = [] {
+    const char* e = getenv("PMD_WGRAD_BIG_MIN");
+    const int x = e ? atoi(e) : 0;
+    return x > 0 ? x : 256;
+  }();
+  return v;
+}
+
 static WgradCfg wgrad_cfg(int impl, const WgradArgs& a) {
   const int t = wgrad_target_blocks(a.R);
-  if (impl == 4) return {4, 256, 256, t / 4 > 256 ? t / 4 : 256};
-  if (impl == 5) return {5, 256, 128, t / 2 > 256 ? t / 2 : 256};
+  const int bm = big_min_blocks();
+  if (impl == 4) return {4, 256, 256, t / 4 > bm ? t / 4 : bm};
+  if (impl == 5) return {5, 256, 128, t / 2 > bm ? t / 2 : bm};
   return {impl, a.K == 64 ? 64 : 128, 128, t};
 }
 
@@ -1360,6 +1373,18 @@ int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, float* ws, i
       }
     }
     if (c >= 0) impl = c;
+    // A tuned choice is timed alone, but it runs next to the main stream: one 8-wave 256x256
+    // block per CU holds 128 KB of LDS for the whole kernel (~150 us at l3/l4), so no main-stream
+    // conv block (>= 34 KB) -- nor, with its VGPRs, a 5-us statistics collapse -- fits next to it
+    // until it retires.  Tuned 256x256 choices therefore run as the 128x128 tile (64 KB):
+    // +0.4% step (13,506 / 13,540 vs 13,460 / 13,467 img/s, profiles/wgrad_lds_r05.txt).
+    // PMD_WGRAD_MAP4 / _MAP5 / _MAP6 = impl: the variant a tuned 256x256 / 256x128 (96 KB) /
+    // halo (152 KB) choice runs as (defaults 1 / none / none; 0 = as tuned; the other two
+    // measured slower).  A forced variant (PMD_WGRAD_IMPL, conv_wgrad_set_impl) is never remapped.
+    static const int remap[3] = {[] { const char* e = getenv("PMD_WGRAD_MAP4"); return e ? atoi(e) : 1; }(),
+                                 [] { const char* e = getenv("PMD_WGRAD_MAP5"); return e ? atoi(e) : 0; }(),
+                                 [] { const char* e = getenv("PMD_WGRAD_MAP6"); return e ? atoi(e) : 0; }()};
+    if (impl >= 4 && impl <= 6 && remap[impl - 4] > 0 && wgrad_cfg_ok(remap[impl - 4], a)) impl = remap[impl - 4];
   }
   wgrad_run(impl, a, ws, st);
   return 0;
