@@ -213,7 +213,17 @@ __global__ __launch_bounds__(64 * WM * WN,
   constexpr int A_ELEMS = BM * LDR;
   constexpr int B_ELEMS = BN * LDR;
   constexpr int STAGE = A_ELEMS + B_ELEMS;
-  constexpr int LDC = BN + 8;
+  // PMD_EPI_X (SWAPC, 128-column tiles): the C tile staged UNPADDED (LDC = BN) with the 16-B
+  // chunk index XORed by the row's low 4 bits (+ the EPI_SW half swap), conflict-free for the
+  // ds_write_b64 groups and the ds_read_b128 row reads alike -- 32 KB instead of 34 KB, so the
+  // 128x128 dgrad (32 KB mainloop) fits a CU next to two 64 KB weight-gradient blocks of the
+  // side stream (160 KB) instead of waiting for one to retire.  Measured -0.3% on the step
+  // (13,428 / 13,484 vs 13,473 / 13,508 img/s, profiles/epi_x_r05.txt): A/B only, off
+#ifndef PMD_EPI_X
+#define PMD_EPI_X 0
+#endif
+  constexpr bool EPI_X = PMD_EPI_X && PMD_CONV_SWAPC && !STATS && !MF32 && BN == 128 && NT == 256;
+  constexpr int LDC = EPI_X ? BN : BN + 8;
   // epilogue C-staging layout (SWAPC only): EPI_SW = 8-B half swap in rows with bit 3
   // set (conflict-free ds_write_b64); EPI_RM = row order of the ds_read_b128 row reads
   // for 16-chunk rows read by 16 thread rows (BN = 128, 4 waves): the two 16-lane
@@ -223,7 +233,7 @@ __global__ __launch_bounds__(64 * WM * WN,
 #define PMD_EPI_SW 1
 #endif
   constexpr bool EPI_SW = PMD_EPI_SW && SWAPC;
-  constexpr bool EPI_RM = PMD_EPI_SW && SWAPC && BN == 128 && NT == 256;
+  constexpr bool EPI_RM = PMD_EPI_SW && SWAPC && BN == 128 && NT == 256 && !EPI_X;
   constexpr bool EPI_RM64 = PMD_EPI_SW >= 2 && SWAPC && BN == 64 && NT == 256;
   // HALO image: at most ceil(BM / W) + 3 input rows of W + 2 pixels (a tile spans
   // ceil(BM / W) + 1 rows, plus the two halo rows), 8 chunks each, rounded up to whole
@@ -1062,7 +1072,9 @@ __global__ __launch_bounds__(64 * WM * WN,
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const int row = wm * (BM / WM) + i * 16 + (lane & 15);
-        const int col = (wn * (BN / WN) + j * 16 + (lane >> 4) * 4) ^ (EPI_SW ? ((lane >> 1) & 4) : 0);
+        const int colw = wn * (BN / WN) + j * 16 + (lane >> 4) * 4;   // logical channel (4 per lane)
+        const int col = EPI_X ? ((((colw >> 3) ^ (row & 15)) << 3) | ((colw & 4) ^ (((row >> 3) & 1) << 2)))
+                              : colw ^ (EPI_SW ? ((lane >> 1) & 4) : 0);
         const uint32_t lo = (uint32_t)f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16);
         const uint32_t hi = (uint32_t)f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16);
         *reinterpret_cast<uint2*>(Cs + row * LDC + col) = make_uint2(lo, hi);
@@ -1149,7 +1161,7 @@ __global__ __launch_bounds__(64 * WM * WN,
         off[g] = (((size_t)nb * a.OH + 2 * hh + ph) * a.OW + 2 * ww + pw) * a.Nout + (n_ok ? n : 0);
       }
       if (!ok[g]) off[g] = 0;
-      v[g] = *reinterpret_cast<const uint4*>(Cs + row * LDC + cc * 8);
+      v[g] = *reinterpret_cast<const uint4*>(Cs + row * LDC + (EPI_X ? ((cc ^ (row & 15)) << 3) : cc * 8));
       if constexpr (EPI_SW) {
         // rows with bit 3 set hold their 8-B halves swapped (compile-time under EPI_RM)
         const bool sw = EPI_RM ? ((it0 + g) & 1) != 0 : ((row >> 3) & 1) != 0;
