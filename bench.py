@@ -304,7 +304,8 @@ def bench_rank(rank, world, a):
         torch.cuda.synchronize()
         if rank == 0:
             buf = io.StringIO()
-            pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(45)
+            pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(60)
+            pstats.Stats(pr, stream=buf).sort_stats("cumulative").print_stats(60)
             with open(a.host_profile, "w") as f:
                 f.write(f"# bench.py host profile, 10 steps, {a.model} batch {a.batch}, "
                         f"parallelism {parallelism}\n")
