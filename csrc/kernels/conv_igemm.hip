@@ -28,6 +28,7 @@
 #include "common.h"
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <map>
 #include <vector>
@@ -1708,6 +1709,46 @@ static int tune(const ConvArgs& a0, hipStream_t st) {
   return best;
 }
 
+// PMD_CONV_REMAP="d2:4,f0:1,..." (A/B knob): run a tuned choice of the data-gradient (d) /
+// forward (f) passes as another candidate -- the tuner times a conv alone, the step runs it
+// next to the side stream (the co-residency question of profiles/wgrad_lds_r05.txt)
+static int conv_remap(bool dgrad, int c) {
+  static int map[2][16];
+  static const bool init = [] {
+    for (int p = 0; p < 2; ++p)
+      for (int i = 0; i < 16; ++i) map[p][i] = i;
+    const char* e = getenv("PMD_CONV_REMAP");
+    while (e && *e) {
+      const int p = *e == 'd' ? 1 : 0;
+      int from = -1, to = -1;
+      if (sscanf(e + 1, "%d:%d", &from, &to) == 2 && from >= 0 && from < 16 && to >= 0 && to < 16)
+        map[p][from] = to;
+      e = strchr(e, ',');
+      if (e) ++e;
+    }
+    return true;
+  }();
+  (void)init;
+  return (c >= 0 && c < 16) ? map[dgrad ? 1 : 0][c] : c;
+}
+
+static int conv_halo_pref(bool dgrad) {
+  static int pref[2] = {0, 0};
+  static const bool init = [] {
+    const char* e = getenv("PMD_CONV_HALO");
+    while (e && *e) {
+      int v = 0;
+      if ((e[0] == 'f' || e[0] == 'd') && e[1] == ':' && sscanf(e + 2, "%d", &v) == 1 && (v == 11 || v == 12))
+        pref[e[0] == 'd' ? 1 : 0] = v;
+      e = strchr(e, ',');
+      if (e) ++e;
+    }
+    return true;
+  }();
+  (void)init;
+  return pref[dgrad ? 1 : 0];
+}
+
 template <bool DGRAD, bool STATS>
 static void launch_sel(const ConvArgs& a, hipStream_t st) {
   if (conv_impl() == 5 && conv_tile() == 0 && autotune_on()) {
@@ -1740,6 +1781,11 @@ static void launch_sel(const ConvArgs& a, hipStream_t st) {
       }
     }
     if (c >= 0) {
+      c = conv_remap(DGRAD, c);
+      // PMD_CONV_HALO="f:12,d:11" (A/B knob): the halo-image 3x3 kernel (candidate 11: 2-deep,
+      // 12: 3-deep weight ring) for every halo-eligible stride-1 3x3 forward (f) / dgrad (d)
+      const int hp = conv_halo_pref(DGRAD);
+      if (hp && halo_ok(a)) c = hp;
       launch_choice<DGRAD, STATS>(c, a, st);
       return;
     }
