@@ -861,7 +861,7 @@ void conv_wgrad_set_impl(int impl) { g_wgrad_impl = impl; }
 static int wgrad_impl() {
   if (g_wgrad_impl < 0) {
     const char* e = getenv("PMD_WGRAD_IMPL");
-    g_wgrad_impl = (e && e[0] >= '0' && e[0] <= '6') ? e[0] - '0' : 1;
+    g_wgrad_impl = (e && e[0] >= '0' && e[0] <= '7') ? e[0] - '0' : 1;
   }
   return g_wgrad_impl;
 }
@@ -1052,6 +1052,10 @@ static void wgrad_run(int impl, WgradArgs a, float* ws, hipStream_t st) {
       break;
     case 5:  // 8 waves, 256x128, DMA 64-row x2
       WG_LAUNCH((conv_wgrad_dma_kernel<256, 128, 64, 2, 4, 2>), grid, dim3(512), st, a);
+      break;
+    case 7:  // DMA, 32-row stages, 3-deep ring: 48 KB (co-resides with a main-stream conv block)
+      if (k64) WG_LAUNCH((conv_wgrad_dma_kernel<64, 128, 32, 3>), grid, dim3(256), st, a);
+      else WG_LAUNCH((conv_wgrad_dma_kernel<128, 128, 32, 3>), grid, dim3(256), st, a);
       break;
     default:  // 1: DMA, 64-row stages, 2-deep ring
       if (k64) WG_LAUNCH((conv_wgrad_dma_kernel<64, 128, 64, 2>), grid, dim3(256), st, a);
@@ -1381,10 +1385,16 @@ int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, float* ws, i
     // PMD_WGRAD_MAP4 / _MAP5 / _MAP6 = impl: the variant a tuned 256x256 / 256x128 (96 KB) /
     // halo (152 KB) choice runs as (defaults 1 / none / none; 0 = as tuned; the other two
     // measured slower).  A forced variant (PMD_WGRAD_IMPL, conv_wgrad_set_impl) is never remapped.
-    static const int remap[3] = {[] { const char* e = getenv("PMD_WGRAD_MAP4"); return e ? atoi(e) : 1; }(),
+    // PMD_WGRAD_MAP0 / _MAP1 likewise for the register-staged / 64-row DMA choices (7 = the
+    // 48 KB 32-row x3 DMA variant, A/B).
+    static const int remap[8] = {[] { const char* e = getenv("PMD_WGRAD_MAP0"); return e ? atoi(e) : 0; }(),
+                                 [] { const char* e = getenv("PMD_WGRAD_MAP1"); return e ? atoi(e) : 0; }(),
+                                 0, 0,
+                                 [] { const char* e = getenv("PMD_WGRAD_MAP4"); return e ? atoi(e) : 1; }(),
                                  [] { const char* e = getenv("PMD_WGRAD_MAP5"); return e ? atoi(e) : 0; }(),
-                                 [] { const char* e = getenv("PMD_WGRAD_MAP6"); return e ? atoi(e) : 0; }()};
-    if (impl >= 4 && impl <= 6 && remap[impl - 4] > 0 && wgrad_cfg_ok(remap[impl - 4], a)) impl = remap[impl - 4];
+                                 [] { const char* e = getenv("PMD_WGRAD_MAP6"); return e ? atoi(e) : 0; }(),
+                                 0};
+    if (impl >= 0 && impl < 8 && remap[impl] > 0 && wgrad_cfg_ok(remap[impl], a)) impl = remap[impl];
   }
   wgrad_run(impl, a, ws, st);
   return 0;

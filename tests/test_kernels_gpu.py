@@ -93,7 +93,7 @@ def test_conv_fwd_dgrad_wgrad(shape):
     _close(dw, dwr, 2e-3)
 
 
-@pytest.mark.parametrize("impl", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("impl", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("shape", R50_SHAPES + CIFAR_SHAPES, ids=lambda s: "C%d_H%d_K%d_R%d_s%d" % s)
 def test_wgrad_variants(shape, impl):
     """Every operand-staging variant of the split-K wgrad kernel (register
