@@ -31,7 +31,7 @@ class _NoWork:
         pass
 
 
-def _worker(rank, world, port, out, stats_comm="gloo", fault="none"):
+def _worker(rank, world, port, out, stats_comm="gloo", fault="none", model_name="res"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -74,8 +74,22 @@ def _worker(rank, world, port, out, stats_comm="gloo", fault="none"):
             orig_launch(self, b)
         DP.DataParallel._launch = launch
     torch.manual_seed(0 if rank == 0 else 77)     # rank 1 starts different: broadcast must fix it
-    model = build_model("res", num_classes=10, stem="cifar").cuda()
-    x, y = C.synth_images(64, 32, 32, 8, 3, 10, 7, 0)   # == test_model_oracle_gpu's batch
+    if model_name == "resnet50":
+        # bottleneck blocks with the linear-BN backward on EVERY identity block (PMD_BNLIN=all)
+        OF._BNLIN = "all"
+        lin_calls = {"n": 0}
+        orig_lin = OF._bnlin_final
+
+        def counted(*a, **k):
+            lin_calls["n"] += 1
+            return orig_lin(*a, **k)
+        OF._bnlin_final = counted
+        torch.manual_seed(0)
+        model = build_model("resnet50", num_classes=10, stem="imagenet").cuda()
+        x, y = C.synth_images(16, 64, 64, 8, 3, 10, 7, 0)
+    else:
+        model = build_model("res", num_classes=10, stem="cifar").cuda()
+        x, y = C.synth_images(64, 32, 32, 8, 3, 10, 7, 0)   # == test_model_oracle_gpu's batch
     per = x.shape[0] // world
     dp = DP.DataParallel(model, comm, bucket_mb=1.0, first_bucket_mb=0.25, reducer=reducer)
     dp.train()
@@ -93,6 +107,7 @@ def _worker(rank, world, port, out, stats_comm="gloo", fault="none"):
                     "buffers": {k: v.cpu() for k, v in dp.module.state_dict().items()
                                 if "running" in k or "num_batches" in k},
                     "loss": float(losses.item() / world),
+                    "lin_calls": lin_calls["n"] if model_name == "resnet50" else 0,
                     "nbuckets": len(dp.buckets)}, out)
     OF.set_bn_sync(None)
     dist.destroy_process_group()
@@ -157,3 +172,52 @@ def test_two_ranks_on_one_gpu_match_single_process_per_tensor(tmp_path, stats_co
         assert not bad, bad
     else:
         assert bad, f"negative control {fault} passed the per-tensor oracle"
+
+
+def _r50_single(monkeypatch):
+    """Single-process ResNet-50 step on the global batch (linear-BN backward everywhere):
+    gfx950 kernels and the fp32 torch-primitive oracle, same weights and batch."""
+    import copy
+    from pytorch_multiprocessing_distributed_amd.models import build_model
+    from pytorch_multiprocessing_distributed_amd.ops import functional as OF
+    from pytorch_multiprocessing_distributed_amd.ops.native import C
+    monkeypatch.setattr(OF, "_BNLIN", "all")
+    torch.manual_seed(0)
+    m0 = build_model("resnet50", num_classes=10, stem="imagenet").cuda()
+    x, y = C.synth_images(16, 64, 64, 8, 3, 10, 7, 0)
+    m0.train()
+    grads, loss = {}, {}
+    for k in ("hip", "f32"):
+        m = copy.deepcopy(m0)
+        OF.force_torch_prims(k == "f32")
+        try:
+            lo = OF.cross_entropy(m(x.float() if k == "f32" else x), y)
+            lo.backward()
+        finally:
+            OF.force_torch_prims(False)
+        torch.cuda.synchronize()
+        loss[k] = float(lo)
+        grads[k] = {n: p.grad.detach().float().cpu() for n, p in m.named_parameters()}
+    return loss, grads
+
+
+def test_two_ranks_resnet50_linear_bn_match_single_process(tmp_path, monkeypatch):
+    """The linear-BN backward under SyncBN: 2 ranks x 8 images of ResNet-50 (every identity
+    block's final BN back-propagated through its conv3, statistics over the xGMI kernel) == one
+    process on the global 16, per gradient tensor against the fp32 oracle (3x the single
+    process's own error, floored at half its median, + 1e-2)."""
+    out = str(tmp_path / "r0.pt")
+    mp.spawn(_worker, args=(2, _free_port(), out, "xgmi", "none", "resnet50"), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    assert got["lin_calls"] == 11      # every identity block whose output feeds a fused dgrad
+    loss, grads = _r50_single(monkeypatch)
+    e1 = {n: _rel(g, grads["f32"][n]) for n, g in grads["hip"].items()}
+    e2 = {n: _rel(g, grads["f32"][n]) for n, g in got["grads"].items()}
+    assert set(e1) == set(e2) and len(e2) == 161
+    floor = 0.5 * sorted(e1.values())[len(e1) // 2]
+    bad = [(n, round(e2[n], 4), round(e1[n], 4)) for n in e2 if e2[n] > 3.0 * max(e1[n], floor) + 1e-2]
+    # the loss, like every tensor: within 3x the single process's own error against fp32 (a
+    # batch of 16 64x64 images leaves l4's BN 64 values per channel: bf16 itself is ~3% off)
+    own = abs(loss["hip"] - loss["f32"])
+    assert abs(got["loss"] - loss["f32"]) <= 3.0 * own + 1e-2 * loss["f32"], (got["loss"], loss)
+    assert not bad, bad
