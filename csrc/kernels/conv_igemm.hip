@@ -432,6 +432,12 @@ __global__ __launch_bounds__(64 * WM * WN,
     }
   };
 
+  // tap -> (tap row, tap col) of the general loader: a shift when the (phase) filter width
+  // is a power of two (the 4x4 space-to-depth stem, 1x1, 2-tap phases) instead of a
+  // runtime integer division per chunk per K-tile (the stem conv's gather was VALU-bound)
+  const bool ns_pow2 = (ns & (ns - 1)) == 0;
+  const int log2ns = ns_pow2 ? __builtin_ctz(ns) : 0;
+  auto tap_row = [&](int tap) { return ns_pow2 ? (tap >> log2ns) : tap / ns; };
   auto load_tile = [&](int kt, int dbuf) {
 #pragma unroll
     for (int i = 0; i < PA; ++i) {
@@ -439,7 +445,7 @@ __global__ __launch_bounds__(64 * WM * WN,
       const bool kok = k0 < Kgp;
       const int tap = k0 >> a.log2Cs;
       const int c = k0 & (a.Cs - 1);
-      const int tr = tap / ns;
+      const int tr = tap_row(tap);
       const int r = r0 + rstep * tr;
       const int s = s0 + rstep * (tap - tr * ns);
       int ih, iw;
@@ -473,7 +479,7 @@ __global__ __launch_bounds__(64 * WM * WN,
       const int k0 = kt * BKE + bchunk(i) * CE;
       const bool kok = k0 < Kgp;
       const int tap = k0 >> a.log2Cs;
-      const int tr = tap / ns;
+      const int tr = tap_row(tap);
       const int r = r0 + rstep * tr;
       const int s = s0 + rstep * (tap - tr * ns);
       const int boff = ((r * a.S + s) << a.log2Cs) + (k0 & (a.Cs - 1));
