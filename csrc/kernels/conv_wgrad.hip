@@ -804,13 +804,7 @@ static bool halo_cfg(const WgradArgs& a, HaloArgs* h, int* nich) {
   // the halo must cover every tap of every band row: q + s - pad in [-pad, Q + S - 1 - pad)
   c.bands_img = (a.P + c.PB - 1) / c.PB;
   c.bands = a.N * c.bands_img;
-  // one 150 KB block per CU; PMD_WGRAD_HALO_BLOCKS (A/B knob): fewer, longer blocks, so the
-  // main stream's kernels keep CUs while this side-stream kernel runs
-  static const int target = [] {
-    const char* e = getenv("PMD_WGRAD_HALO_BLOCKS");
-    const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : 256;
-  }();
+  const int target = 256;  // one 150 KB block per CU
   const int blocks = c.bands < target ? c.bands : target;
   c.bpb = (c.bands + blocks - 1) / blocks;
   *h = c;
@@ -934,23 +928,10 @@ static bool wgrad_cfg_ok(int impl, const WgradArgs& a) {
   return true;
 }
 
-// PMD_WGRAD_BIG_MIN (A/B knob): the minimum split-K block count of the 8-wave tiles (256).  One
-// 8-wave 256x256 block per CU holds 128 KB of LDS for the whole kernel (~150 us at l3/l4), so no
-// main-stream conv block (>= 34 KB) fits next to it until it retires.
-static int big_min_blocks() {
-  static const int v = [] {
-    const char* e = getenv("PMD_WGRAD_BIG_MIN");
-    const int x = e ? atoi(e) : 0;
-    return x > 0 ? x : 256;
-  }();
-  return v;
-}
-
 static WgradCfg wgrad_cfg(int impl, const WgradArgs& a) {
   const int t = wgrad_target_blocks(a.R);
-  const int bm = big_min_blocks();
-  if (impl == 4) return {4, 256, 256, t / 4 > bm ? t / 4 : bm};
-  if (impl == 5) return {5, 256, 128, t / 2 > bm ? t / 2 : bm};
+  if (impl == 4) return {4, 256, 256, t / 4 > 256 ? t / 4 : 256};
+  if (impl == 5) return {5, 256, 128, t / 2 > 256 ? t / 2 : 256};
   return {impl, a.K == 64 ? 64 : 128, 128, t};
 }
 
@@ -984,30 +965,6 @@ static void plan(const WgradArgs& a, const WgradCfg& cfg, int* splits_out, int* 
 
 static void wgrad_reduce_launch(const WgradArgs& a, int splits, hipStream_t st);
 
-// PMD_WGRAD_LDS_PAD=bytes (A/B knob, 0 = off): extra dynamic LDS per weight-gradient block
-// (capped at what the CU has left), i.e. an occupancy cap on the side stream so the main
-// stream's convolution blocks (34-135 KB of LDS) can co-reside: two 64 KB wgrad blocks leave
-// 32 KB of a CU's 160 KB, and a main-stream dgrad block (34 KB) then waits for a wgrad block
-// to retire.
-static size_t wgrad_lds_pad(const void* kern) {
-  static const int pad = env_int("PMD_WGRAD_LDS_PAD", 0);
-  if (pad <= 0) return 0;
-  static std::map<const void*, size_t> cache;
-  static std::mutex mu;
-  std::lock_guard<std::mutex> lk(mu);
-  auto it = cache.find(kern);
-  if (it != cache.end()) return it->second;
-  hipFuncAttributes at{};
-  size_t r = 0;
-  if (hipFuncGetAttributes(&at, kern) == hipSuccess) {
-    const size_t room = 160 * 1024 > at.sharedSizeBytes ? 160 * 1024 - at.sharedSizeBytes : 0;
-    r = (size_t)pad < room ? (size_t)pad : room;
-  }
-  cache[kern] = r;
-  return r;
-}
-#define WG_LAUNCH(KERN, GRID, BLOCK, ST, ...) \
-  hipLaunchKernelGGL(KERN, GRID, BLOCK, wgrad_lds_pad(reinterpret_cast<const void*>(&KERN)), ST, __VA_ARGS__)
 
 // One full weight gradient with variant `impl`: split-K plan, kernel, split reduce.
 static void wgrad_run(int impl, WgradArgs a, float* ws, hipStream_t st) {
@@ -1018,9 +975,9 @@ static void wgrad_run(int impl, WgradArgs a, float* ws, hipStream_t st) {
       const int splits = halo_splits(h);
       a.ws = splits > 1 ? ws : nullptr;
       if (ni == 4)
-        WG_LAUNCH((conv_wgrad_halo_kernel<4, 1280>), dim3(splits), dim3(256), st, a, h);
+        hipLaunchKernelGGL((conv_wgrad_halo_kernel<4, 1280>), dim3(splits), dim3(256), 0, st, a, h);
       else
-        WG_LAUNCH((conv_wgrad_halo_kernel<9, 3072>), dim3(splits), dim3(256), st, a, h);
+        hipLaunchKernelGGL((conv_wgrad_halo_kernel<9, 3072>), dim3(splits), dim3(256), 0, st, a, h);
       if (splits > 1) wgrad_reduce_launch(a, splits, st);
       return;
     }
@@ -1036,30 +993,30 @@ static void wgrad_run(int impl, WgradArgs a, float* ws, hipStream_t st) {
   const bool k64 = a.K == 64;
   switch (impl) {
     case 0:
-      if (k64) WG_LAUNCH((conv_wgrad_kernel<64, 128>), grid, dim3(256), st, a);
-      else WG_LAUNCH((conv_wgrad_kernel<128, 128>), grid, dim3(256), st, a);
+      if (k64) hipLaunchKernelGGL((conv_wgrad_kernel<64, 128>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), grid, dim3(256), 0, st, a);
       break;
     case 2:  // DMA, 32-row stages, 4-deep ring
-      if (k64) WG_LAUNCH((conv_wgrad_dma_kernel<64, 128, 32, 4>), grid, dim3(256), st, a);
-      else WG_LAUNCH((conv_wgrad_dma_kernel<128, 128, 32, 4>), grid, dim3(256), st, a);
+      if (k64) hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 128, 32, 4>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 32, 4>), grid, dim3(256), 0, st, a);
       break;
     case 3:  // DMA, 64-row stages, 3-deep ring (1 block/CU at BM=128)
-      if (k64) WG_LAUNCH((conv_wgrad_dma_kernel<64, 128, 64, 3>), grid, dim3(256), st, a);
-      else WG_LAUNCH((conv_wgrad_dma_kernel<128, 128, 64, 3>), grid, dim3(256), st, a);
+      if (k64) hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 128, 64, 3>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 64, 3>), grid, dim3(256), 0, st, a);
       break;
     case 4:  // 8 waves, 256x256, DMA 64-row x2
-      WG_LAUNCH((conv_wgrad_dma_kernel<256, 256, 64, 2, 2, 4>), grid, dim3(512), st, a);
+      hipLaunchKernelGGL((conv_wgrad_dma_kernel<256, 256, 64, 2, 2, 4>), grid, dim3(512), 0, st, a);
       break;
     case 5:  // 8 waves, 256x128, DMA 64-row x2
-      WG_LAUNCH((conv_wgrad_dma_kernel<256, 128, 64, 2, 4, 2>), grid, dim3(512), st, a);
+      hipLaunchKernelGGL((conv_wgrad_dma_kernel<256, 128, 64, 2, 4, 2>), grid, dim3(512), 0, st, a);
       break;
     case 7:  // DMA, 32-row stages, 3-deep ring: 48 KB (co-resides with a main-stream conv block)
-      if (k64) WG_LAUNCH((conv_wgrad_dma_kernel<64, 128, 32, 3>), grid, dim3(256), st, a);
-      else WG_LAUNCH((conv_wgrad_dma_kernel<128, 128, 32, 3>), grid, dim3(256), st, a);
+      if (k64) hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 128, 32, 3>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 32, 3>), grid, dim3(256), 0, st, a);
       break;
     default:  // 1: DMA, 64-row stages, 2-deep ring
-      if (k64) WG_LAUNCH((conv_wgrad_dma_kernel<64, 128, 64, 2>), grid, dim3(256), st, a);
-      else WG_LAUNCH((conv_wgrad_dma_kernel<128, 128, 64, 2>), grid, dim3(256), st, a);
+      if (k64) hipLaunchKernelGGL((conv_wgrad_dma_kernel<64, 128, 64, 2>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad_dma_kernel<128, 128, 64, 2>), grid, dim3(256), 0, st, a);
       break;
   }
   if (splits > 1) wgrad_reduce_launch(a, splits, st);

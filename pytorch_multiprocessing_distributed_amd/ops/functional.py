@@ -82,18 +82,6 @@ class WeightImageSet:
         dgrad (:func:`_wait_weight_images`)."""
         if not need_bwd:
             self._c.refresh(1)
-        elif _WPREP_SIDE and _WGRAD_STREAM["on"] and self._dev.type == "cuda":
-            # every image on the side stream, next to the stem (which reads its own s2d
-            # image): the main stream waits only at the first lookup (_weight_images)
-            main = torch.cuda.current_stream(self._dev)
-            side = _wgrad_stream(self._dev)
-            side.wait_stream(main)               # after the previous step's optimizer update
-            with torch.cuda.stream(side):
-                self._c.refresh(3)
-            ev = torch.cuda.Event()
-            ev.record(side)
-            _state["wk_event"] = ev
-            _state["wkt_event"] = ev
         elif _SPLIT_WPREP and _WGRAD_STREAM["on"] and self._dev.type == "cuda":
             self._c.refresh(1)
             main = torch.cuda.current_stream(self._dev)
@@ -150,9 +138,6 @@ class Fp8WeightSet:
 def _weight_images(P, w, dtype, cin, want_t):
     wi = _state["wimg"]
     if wi is not None:
-        ev = _state.pop("wk_event", None)
-        if ev is not None:
-            torch.cuda.current_stream().wait_event(ev)
         r = wi.lookup(w, cin, want_t)
         if r is not None:
             return r
@@ -333,9 +318,6 @@ _WGRAD_STREAM = {"on": os.environ.get("PMD_WGRAD_STREAM", "1") != "0", "streams"
 # dgrad weight images refreshed on the side stream during the forward: PMD_SPLIT_WPREP=1
 # (measured step-neutral, 12,699 / 12,684 vs 12,704 / 12,712 img/s: off by default)
 _SPLIT_WPREP = os.environ.get("PMD_SPLIT_WPREP", "0") == "1"
-# PMD_WPREP_SIDE=1: forward AND dgrad images refreshed on the side stream, overlapping the
-# ImageNet stem (s2d input, stem conv, BN + pool), the main stream waiting at the first lookup
-_WPREP_SIDE = os.environ.get("PMD_WPREP_SIDE", "0") == "1"
 
 
 # Priority of the step's own HIP streams (default high, -1; PMD_STREAM_PRIO=0: normal).
