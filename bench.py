@@ -87,6 +87,9 @@ def parse():
     ap.add_argument("--timeline", action="store_true",
                     help="print the gradient-bucket launch/overlap timeline of the last step")
     ap.add_argument("--profile", default="", help="write a torch.profiler table here (rank 0)")
+    ap.add_argument("--step_mode", default="auto", choices=["auto", "two_stream", "one_stream", "graph"],
+                    help="GPU step schedule (engine/train.py resolve_step_mode): auto = two_stream for the "
+                         "224x224 headline, graph (W=1) / one_stream (W>1) for small images")
     ap.add_argument("--host_profile", default="",
                     help="after the timed run: cProfile the host side of 10 more steps (rank 0) and "
                          "write the top functions by own time here")
@@ -156,6 +159,9 @@ def bench_rank(rank, world, a):
     else:
         comm = get_comm()
     setup_syncbn(comm, a.sync_bn, a.syncbn_comm, True)
+    from pytorch_multiprocessing_distributed_amd.engine.train import GraphedStep, resolve_step_mode
+    step_mode = resolve_step_mode(a.step_mode, 2 if rehearsal else world, True, a.image, a.dtype)
+    OF.set_wgrad_stream(step_mode == "two_stream")
     model = DataParallel(model, comm, bucket_mb=a.bucket_mb, first_bucket_mb=a.first_bucket_mb,
                          compress=a.grad_compress, transport=a.comm if comm is not None else "c10d",
                          timeline=a.timeline, last_bucket_mb=a.last_bucket_mb)
@@ -176,8 +182,13 @@ def bench_rank(rank, world, a):
     else:
         tune_source, _ = tuning.load_default()
 
+    graphed = {}
+
     def step(i):
         x, y = data.batch_at(i)
+        g = graphed.get("g")
+        if g is not None:
+            return g(x, y)[1]               # the captured step, replayed on this batch
         out = model(x)
         loss = OF.cross_entropy(out, y)
         opt.zero_grad()
@@ -189,6 +200,11 @@ def bench_rank(rank, world, a):
         step(i)
         if i == 0 and comm is not None:
             tuning.sync(comm.group)         # every rank runs rank 0's kernel choices
+    if step_mode == "graph":
+        # captured after the eager warmup (kernel choices tuned, lazy state initialised) and
+        # before the timed region, whose every step is then one copy-in + one graph replay
+        x, y = data.batch_at(0)
+        graphed["g"] = GraphedStep(model, opt, x, y)
     if a.save_tune_table and rank == 0:
         tuning.save(a.save_tune_table)
     torch.cuda.synchronize()
@@ -265,7 +281,7 @@ def bench_rank(rank, world, a):
                        "image_size": a.image, "per_gpu_batch": a.batch,
                        "parallelism": parallelism,
                        "sync_bn": a.sync_bn == "on" and (world > 1 or rehearsal),
-                       "bucket_mb": a.bucket_mb,
+                       "bucket_mb": a.bucket_mb, "step_mode": step_mode,
                        "syncbn_comm": syncbn_label(comm, a.sync_bn),
                        "syncbn_ordering": (comm.xgmi.ordering if comm is not None and comm.xgmi is not None
                                            else None),

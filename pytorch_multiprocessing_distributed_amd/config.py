@@ -78,6 +78,13 @@ def build_parser():
                         "communicator (csrc/runtime/rccl_comm.cpp) when it can be the only in-step "
                         "communicator (SyncBN on the xGMI kernel or off) and its startup self-test "
                         "passes, else torch ProcessGroupNCCL (c10d); the choice is printed")
+    p.add_argument("--step_mode", default="auto", choices=["auto", "two_stream", "one_stream", "graph"],
+                   help="GPU step schedule: two_stream = weight gradients on a side HIP stream (the "
+                        "device-bound large steps, e.g. ImageNet bs256); one_stream = everything on one "
+                        "stream (host-bound small steps: fewer host-side forks/joins); graph = one "
+                        "stream, captured once as a HIP graph and replayed (single GPU, bf16); auto: "
+                        "graph for W=1 small steps, one_stream for W>1 small steps, two_stream otherwise "
+                        "(small = image <= 64, e.g. the reference's CIFAR-10 ResNet18)")
     p.add_argument("--last_bucket_mb", default=2.0, type=float,
                    help="cap of the LAST gradient bucket (earliest layers: its all-reduce is "
                         "launched at the end of backward, fully exposed)")

@@ -70,6 +70,66 @@ def _first_step_tuning(args, rank, comm):
 _SYNC_DEBUG = sync_debug_enabled()
 
 
+def resolve_step_mode(mode, world, on_gpu, image_size, dtype):
+    """The GPU step schedule (``--step_mode``).  A ResNet-50 step at 224x224 / batch 256 is
+    device-bound: weight gradients on a side stream overlap the data-gradient chain
+    (two_stream).  The reference's own CIFAR-10 ResNet18 step (32x32, batch 32 per GPU) is
+    host-bound: ~1 ms of GPU work behind ~2 ms of launches, where the side stream's per-block
+    fork/join events cost more than they overlap (one_stream: 1.40 vs 2.05 ms/step on one
+    MI355X) and a captured HIP graph of the whole step removes the launch path altogether
+    (graph: 0.99 ms/step, profiles/step_mode_r05.txt).  Graphs need one process (no
+    collectives inside the capture) and bf16 (fp8 delayed scaling updates on the host)."""
+    if not on_gpu:
+        return "two_stream"
+    if mode == "auto":
+        small = image_size is not None and image_size <= 64
+        if not small:
+            return "two_stream"
+        mode = "graph" if world == 1 else "one_stream"
+    if mode == "graph" and (world != 1 or dtype == "fp8" or _SYNC_DEBUG):
+        mode = "one_stream"
+    return mode
+
+
+class GraphedStep:
+    """The whole training step (forward, loss, backward, fused SGD) captured ONCE as a HIP graph
+    on the current stream and replayed for every later batch of the same shape: the inputs are
+    copied into the captured buffers, the learning rate is device-resident
+    (``FusedSGD.graph_safe``), and the BN running statistics, statistic slots and gradient
+    arena are updated in place by the replay exactly as by an eager step."""
+
+    def __init__(self, model, optimizer, inp, target):
+        optimizer.graph_safe()
+        self.opt = optimizer
+        self.sx = inp.detach().clone()
+        self.sy = target.detach().clone()
+        self.shape = (tuple(inp.shape), tuple(target.shape))
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=torch.cuda.current_stream()):
+            out = model(self.sx)
+            loss = OF.cross_entropy(out, self.sy)
+            optimizer.zero_grad()
+            loss.backward(OF.loss_seed(loss))
+            optimizer.step()
+        optimizer.steps -= 1            # the capture recorded the step, it did not run it
+        self.out, self.loss = out.detach(), loss.detach()
+
+    def fits(self, inp, target):
+        return (tuple(inp.shape), tuple(target.shape)) == self.shape
+
+    def __call__(self, inp, target):
+        self.sx.copy_(inp)
+        self.sy.copy_(target)
+        self.opt.sync_lr()
+        self.graph.replay()
+        self.opt.steps += 1
+        return self.out, self.loss
+
+
+_GRAPHS: dict = {}
+
+
 def train_epoch(loader, model, optimizer, epoch, logger, args, rank, dev, comm=None,
                 step_offset=0):
     batch_time = DeviceMeter()
@@ -81,17 +141,26 @@ def train_epoch(loader, model, optimizer, epoch, logger, args, rank, dev, comm=N
     end = time.time()
     t_epoch = time.time()
     images = 0
+    graphed = getattr(args, "step_mode_resolved", "two_stream") == "graph"
     for i, (inp, target) in enumerate(loader):
         data_time.update(time.time() - end)
         launch.maybe_inject_fault(rank, step_offset + i)
-        with region("fwd"):
-            output = model(inp)
-            loss = OF.cross_entropy(output, target)
-        optimizer.zero_grad()
-        with region("bwd"):
-            loss.backward(OF.loss_seed(loss))
-        with region("opt"):
-            optimizer.step()
+        g = _GRAPHS.get(id(model)) if graphed else None
+        if graphed and g is None and step_offset + i >= 2:
+            # steps 0-1 ran eagerly: kernel choices tuned, lazy state initialised
+            g = _GRAPHS[id(model)] = GraphedStep(model, optimizer, inp, target)
+        if g is not None and g.fits(inp, target):
+            with region("graph"):
+                output, loss = g(inp, target)
+        else:
+            with region("fwd"):
+                output = model(inp)
+                loss = OF.cross_entropy(output, target)
+            optimizer.zero_grad()
+            with region("bwd"):
+                loss.backward(OF.loss_seed(loss))
+            with region("opt"):
+                optimizer.step()
         if comm is not None:
             comm.raise_if_failed()      # xGMI SyncBN timeout of a finished step (no device sync)
         if _SYNC_DEBUG and dev.type == "cuda":
@@ -241,6 +310,11 @@ def _run(rank, world_size, args, dev):
     model = build_model(args.model, num_classes=args.num_classes, stem=args.stem).to(dev)
     comm = get_comm()
     setup_syncbn(comm, args.sync_bn, getattr(args, "syncbn_comm", "auto"), on_gpu)
+    args.step_mode_resolved = resolve_step_mode(getattr(args, "step_mode", "auto"), world_size, on_gpu,
+                                                args.image_size, args.dtype)
+    OF.set_wgrad_stream(args.step_mode_resolved == "two_stream")
+    if rank == 0 and on_gpu:
+        print(f"[pmd] step mode: {args.step_mode_resolved}", flush=True)
     model = DataParallel(model, comm, bucket_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb,
                          broadcast_buffers=args.broadcast_buffers,
                          reducer=getattr(args, "reducer", "native"),
