@@ -1320,9 +1320,11 @@ __global__ void conv_weight_prep_kernel(const float* __restrict__ w, bf16_t* __r
 // write); bit 1: dgrad images wkt.  The training step refreshes wk on the main
 // stream (the stem needs it at once) and wkt on the idle side stream during the
 // forward (the first dgrad is milliseconds later).
-__global__ void conv_weight_prep_grouped_kernel(const WeightPrepDesc* __restrict__ descs,
-                                                const int* __restrict__ block_start, int n, int mode) {
+__global__ __launch_bounds__(256) void conv_weight_prep_grouped_kernel(const WeightPrepDesc* __restrict__ descs,
+                                                                      const int* __restrict__ block_start, int n,
+                                                                      int mode) {
   __shared__ int e_sh;
+  __shared__ float tile[64][65];   // pass 2: one 64 (k) x 64 (c) slice of a tap, odd row pitch
   if (threadIdx.x == 0) {
     int e = 0;
     while (e + 1 < n && block_start[e + 1] <= (int)blockIdx.x) ++e;
@@ -1332,15 +1334,10 @@ __global__ void conv_weight_prep_grouped_kernel(const WeightPrepDesc* __restrict
   const WeightPrepDesc d = descs[e_sh];
   const int lb = blockIdx.x - block_start[e_sh];
   const int nb = block_start[e_sh + 1] - block_start[e_sh];
-  const int total = d.K * d.RS * d.Cp;
-  // pass 1: wk [K][RS][Cp] in its own order, 8 channels (16 B) per thread (Cp % 8 == 0);
-  // pass 2: wkt [Cp][RS][K] in ITS order -- coalesced writes, strided reads of the
-  // (L2-resident, <= 9 MB) fp32 weight instead of a scattered 2-byte write stream
-  const int total8 = total / 8;
-  const int w1 = (mode & 1) ? total8 : 0;
-  const int work = w1 + (((mode & 2) && d.wkt) ? total : 0);
-  for (int i = lb * blockDim.x + threadIdx.x; i < work; i += nb * blockDim.x) {
-    if (i < w1) {
+  // pass 1: wk [K][RS][Cp] in its own order, 8 channels (16 B) per thread (Cp % 8 == 0)
+  if (mode & 1) {
+    const int total8 = d.K * d.RS * d.Cp / 8;
+    for (int i = lb * blockDim.x + threadIdx.x; i < total8; i += nb * blockDim.x) {
       const int e0 = i * 8;
       const int c0 = e0 % d.Cp;
       const int krs = e0 / d.Cp;  // k * RS + rs
@@ -1361,12 +1358,32 @@ __global__ void conv_weight_prep_grouped_kernel(const WeightPrepDesc* __restrict
       o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
       o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
       *reinterpret_cast<uint4*>(d.wk + e0) = o;
-    } else {
-      const int j = i - w1;
-      const int k = j % d.K;
-      const int rs = (j / d.K) % d.RS;
-      const int c = j / (d.K * d.RS);
-      d.wkt[j] = f2bf(c < d.C ? d.w[((size_t)k * d.RS + rs) * d.C + c] : 0.f);
+    }
+  }
+  // pass 2: wkt [Cp][RS][K], the per-tap [K][C] -> [C][K] transpose through LDS in 64 x 64 tiles:
+  // reads along c and writes along k both coalesced (the element-per-thread version read one
+  // fp32 per 64-B line: 141 -> 61 us per step, profiles/weight_prep_tile_r05.txt; one walk
+  // writing both images in mode 3 measured slower, 70 us: fewer bytes but latency-bound)
+  if ((mode & 2) && d.wkt) {
+    const int kt = (d.K + 63) / 64, ct = (d.Cp + 63) / 64;
+    const int ntiles = d.RS * kt * ct;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 64 columns x 4 rows per pass
+    for (int t = lb; t < ntiles; t += nb) {
+      const int rs = t / (kt * ct);
+      const int rem = t - rs * kt * ct;
+      const int k0 = (rem / ct) * 64, c0 = (rem % ct) * 64;
+#pragma unroll 4
+      for (int r = ty; r < 64; r += 4) {
+        const int k = k0 + r, c = c0 + tx;
+        tile[r][tx] = (k < d.K && c < d.C) ? d.w[((size_t)k * d.RS + rs) * d.C + c] : 0.f;
+      }
+      __syncthreads();
+#pragma unroll 4
+      for (int r = ty; r < 64; r += 4) {
+        const int c = c0 + r, k = k0 + tx;
+        if (c < d.Cp && k < d.K) d.wkt[((size_t)c * d.RS + rs) * d.K + k] = f2bf(tile[tx][r]);
+      }
+      __syncthreads();
     }
   }
 }

@@ -90,11 +90,14 @@ __global__ void quant_weight_fp8_kernel(const float* __restrict__ w, uint8_t* __
 }
 
 // Grouped form: block b finds its descriptor in the block-start table (a few
-// dozen entries), then grid-strides inside that weight; amax goes to the
+// dozen entries), then walks 64 (k) x 64 (c) tiles of each tap of that weight:
+// q rows written along c, and the transposed image qt through LDS so its rows
+// are written along k too (not one byte per K-strided address); amax goes to the
 // weight's own slots (one atomicMax per block, every block of one weight).
-__global__ void quant_weight_fp8_grouped_kernel(const Fp8WeightDesc* __restrict__ descs,
-                                                const int* __restrict__ block_start, int n) {
+__global__ __launch_bounds__(256) void quant_weight_fp8_grouped_kernel(const Fp8WeightDesc* __restrict__ descs,
+                                                                       const int* __restrict__ block_start, int n) {
   __shared__ int e_sh;
+  __shared__ uint32_t tile[64][65];
   if (threadIdx.x == 0) {
     int e = 0;
     while (e + 1 < n && block_start[e + 1] <= (int)blockIdx.x) ++e;
@@ -106,17 +109,33 @@ __global__ void quant_weight_fp8_grouped_kernel(const Fp8WeightDesc* __restrict_
   const int nb = block_start[e_sh + 1] - block_start[e_sh];
   const float s = d.scale[0];
   float m = 0.f;
-  const int total = d.K * d.RS * d.Cp;
-  for (int i = lb * blockDim.x + threadIdx.x; i < total; i += nb * blockDim.x) {
-    const int c = i % d.Cp;
-    const int krs = i / d.Cp;
-    const float v = c < d.C ? d.w[(size_t)krs * d.C + c] : 0.f;
-    m = fmaxf(m, fabsf(v));
-    const uint8_t b = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(v * s), 0.f, 0, false) & 0xff);
-    d.q[i] = b;
+  const int kt = (d.K + 63) / 64, ct = (d.Cp + 63) / 64;
+  const int ntiles = d.RS * kt * ct;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int t = lb; t < ntiles; t += nb) {
+    const int rs = t / (kt * ct);
+    const int rem = t - rs * kt * ct;
+    const int k0 = (rem / ct) * 64, c0 = (rem % ct) * 64;
+#pragma unroll 4
+    for (int r = ty; r < 64; r += 4) {
+      const int k = k0 + r, c = c0 + tx;
+      if (k < d.K && c < d.Cp) {
+        const size_t krs = (size_t)k * d.RS + rs;
+        const float v = c < d.C ? d.w[krs * d.C + c] : 0.f;
+        m = fmaxf(m, fabsf(v));
+        const uint8_t b = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(sat_e4m3(v * s), 0.f, 0, false) & 0xff);
+        d.q[krs * d.Cp + c] = b;
+        tile[r][tx] = b;
+      }
+    }
     if (d.qt) {
-      const int k = krs / d.RS, rs = krs - k * d.RS;
-      d.qt[((size_t)c * d.RS + rs) * d.K + k] = b;
+      __syncthreads();
+#pragma unroll 4
+      for (int r = ty; r < 64; r += 4) {
+        const int c = c0 + r, k = k0 + tx;
+        if (c < d.Cp && k < d.K) d.qt[((size_t)c * d.RS + rs) * d.K + k] = (uint8_t)tile[tx][r];
+      }
+      __syncthreads();
     }
   }
   // block_amax_update picks slot blockIdx % kAmaxSlots of the weight's own site

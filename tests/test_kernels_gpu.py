@@ -818,3 +818,60 @@ def test_wgrad_deferred_grouped_reduce_matches_immediate():
     torch.cuda.synchronize()
     for o, r in zip(outs, ref):
         assert torch.equal(o, r)
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3])
+def test_grouped_weight_images_exact(mode):
+    """The grouped per-step weight-image refresh (runtime/weights.cpp -> the LDS-tiled
+    transpose of conv_weight_prep_grouped_kernel) reproduces both layouts exactly:
+    wk [K][R][S][Cp] and wkt [Cp][R][S][K], zero in the padded channels; shapes with K and C
+    off the 64-tile grid, 1x1 / 3x3 / 7x7 taps."""
+    from pytorch_multiprocessing_distributed_amd.ops.native import C
+    shapes = [(64, 3, 7, 8), (256, 64, 1, 64), (72, 40, 3, 48), (512, 512, 3, 512), (2048, 512, 1, 512),
+              (100, 130, 3, 136)]
+    g = torch.Generator(device="cpu").manual_seed(3)
+    ws = [torch.randn(k, c, r, r, generator=g).to(DEV).contiguous(memory_format=torch.channels_last)
+          for k, c, r, _ in shapes]
+    imgs = C.WeightImages(ws, [cp for *_, cp in shapes], [True] * len(shapes))
+    imgs.refresh(3)
+    torch.cuda.synchronize()
+    pre = [[t.clone() for t in imgs.get(i)] for i in range(len(shapes))]
+    for w in ws:
+        w.mul_(-0.5)
+    imgs.refresh(mode)
+    torch.cuda.synchronize()
+    for i, ((k, c, r, cp), w) in enumerate(zip(shapes, ws)):
+        ref = torch.zeros(k, r, r, cp, device=DEV, dtype=torch.bfloat16)
+        ref[..., :c] = w.permute(0, 2, 3, 1).to(torch.bfloat16)
+        wk, wkt = imgs.get(i)
+        want_wk = ref if mode & 1 else pre[i][0]
+        want_wkt = ref.permute(3, 1, 2, 0) if mode & 2 else pre[i][1]
+        assert torch.equal(wk, want_wk), f"wk mismatch at {shapes[i]}"
+        assert torch.equal(wkt, want_wkt), f"wkt mismatch at {shapes[i]}"
+
+
+def test_grouped_fp8_weight_images_exact():
+    """fp8 counterpart (quant_weight_fp8_grouped_kernel, tiled with an LDS transpose): e4m3 of
+    w * scale (saturated, round-to-nearest-even like torch's cast) in both layouts, zero
+    padded channels, and the weight's amax in its own slots."""
+    from pytorch_multiprocessing_distributed_amd.ops.native import C
+    shapes = [(256, 64, 1, 64), (72, 40, 3, 48), (512, 512, 3, 512), (100, 130, 3, 136), (64, 8, 7, 8)]
+    g = torch.Generator(device="cpu").manual_seed(5)
+    ws = [torch.randn(k, c, r, r, generator=g).to(DEV).contiguous(memory_format=torch.channels_last)
+          for k, c, r, _ in shapes]
+    scales = [torch.full((1,), 37.0 * (i + 1), device=DEV) for i in range(len(shapes))]
+    amaxes = [torch.zeros(64, device=DEV) for _ in shapes]
+    imgs = C.Fp8WeightImages(ws, [cp for *_, cp in shapes], scales, amaxes, [i % 2 == 0 for i in range(len(shapes))])
+    imgs.refresh()
+    torch.cuda.synchronize()
+    for i, ((k, c, r, cp), w) in enumerate(zip(shapes, ws)):
+        ref = torch.zeros(k, r, r, cp, device=DEV)
+        ref[..., :c] = w.permute(0, 2, 3, 1) * scales[i]
+        ref = ref.clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)
+        assert torch.equal(imgs.get(i), ref), f"q mismatch at {shapes[i]}"
+        qt = imgs.get_t(i)
+        if i % 2 == 0:
+            assert torch.equal(qt, ref.permute(3, 1, 2, 0)), f"qt mismatch at {shapes[i]}"
+        else:
+            assert qt is None
+        assert amaxes[i].max().item() == w.abs().max().item()
