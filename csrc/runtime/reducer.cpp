@@ -279,12 +279,14 @@ void register_xgmi(pybind11::module& m);
 void register_trace(pybind11::module& m);
 void register_weights(pybind11::module& m);
 void register_rccl(pybind11::module& m);
+void register_events(pybind11::module& m);
 
 void register_runtime(pybind11::module& m) {
   register_xgmi(m);
   register_trace(m);
   register_weights(m);
   register_rccl(m);
+  register_events(m);
   py::class_<Reducer>(m, "Reducer")
       .def(py::init<py::object, py::object, at::Tensor, std::vector<int64_t>, std::vector<int64_t>, bool, bool,
                     py::object, bool>(),

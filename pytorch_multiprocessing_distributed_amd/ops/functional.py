@@ -86,12 +86,10 @@ class WeightImageSet:
             self._c.refresh(1)
             main = torch.cuda.current_stream(self._dev)
             side = _wgrad_stream(self._dev)
-            side.wait_stream(main)               # after the previous step's optimizer update
+            _stream_wait(side, main)             # after the previous step's optimizer update
             with torch.cuda.stream(side):
                 self._c.refresh(2)
-            ev = torch.cuda.Event()
-            ev.record(side)
-            _state["wkt_event"] = ev
+            _state["wkt_event"] = _record_on(side)
         else:
             self._c.refresh(3)
         if self.fp8 is not None:
@@ -331,6 +329,62 @@ _SPLIT_WPREP = os.environ.get("PMD_SPLIT_WPREP", "0") == "1"
 STREAM_PRIO = 0 if os.environ.get("PMD_STREAM_PRIO", "1") == "0" else -1
 
 
+# Cross-stream fork / join points between the main and the weight-gradient stream (~60 per
+# ResNet-50 step).  torch.cuda.Event records a marker with a SYSTEM-scope release, which the
+# main stream pays between its two kernels (6.1 us per fork, bench/event_fence.py);
+# PMD_FORK_EVENTS=0/1/2 uses the native event ring (csrc/runtime/events.cpp) with the default /
+# no system fence (default: 3.5 us per fork, +0.35% on the ResNet-50 step,
+# profiles/fork_events_r05.txt) / a device-scope release instead -- both streams are on one
+# device, where the producing kernel's own release covers the consumer.  -1: torch events.
+# Host- and peer-visible sync points keep torch's events.
+_FORK_EV = int(os.environ.get("PMD_FORK_EVENTS", "1") or 1)
+_RINGS: dict = {}
+
+
+def _fork_ring(dev):
+    if _FORK_EV < 0 or torch.cuda.is_current_stream_capturing():
+        return None
+    r = _RINGS.get(dev)
+    if r is None:
+        from .native import C
+        r = _RINGS[dev] = C.StreamEvents(1024, _FORK_EV, dev.index)
+    return r
+
+
+def _stream_wait(waiter, producer):
+    """``waiter`` waits for everything issued so far on ``producer`` (same device)."""
+    ring = _fork_ring(producer.device)
+    if ring is None:
+        waiter.wait_stream(producer)
+    else:
+        ring.fork(producer.cuda_stream, waiter.cuda_stream)
+
+
+class _RingEvent:
+    __slots__ = ("ring", "slot")
+
+    def __init__(self, ring, stream):
+        self.ring = ring
+        self.slot = ring.record(stream.cuda_stream)
+
+
+def _record_on(stream):
+    """An event recorded on ``stream`` now (a ring slot, or a torch event)."""
+    ring = _fork_ring(stream.device)
+    if ring is None:
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        return ev
+    return _RingEvent(ring, stream)
+
+
+def _wait_on(stream, ev):
+    if isinstance(ev, _RingEvent):
+        ev.ring.wait(stream.cuda_stream, ev.slot)
+    else:
+        stream.wait_event(ev)
+
+
 def _wgrad_stream(dev):
     st = _WGRAD_STREAM["streams"].get(dev)
     if st is None:
@@ -343,7 +397,7 @@ def _wait_weight_images():
     images the forward queued on the side stream."""
     ev = _state.pop("wkt_event", None)
     if ev is not None:
-        torch.cuda.current_stream().wait_event(ev)
+        _wait_on(torch.cuda.current_stream(), ev)
 
 
 _STEP_STREAMS: dict = {}
@@ -438,7 +492,9 @@ class _WgradSide:
         if not self.on or _grad_target(w) is None:
             return _wgrad(P, dy, x, wpack, stride, pad, w, xq)
         _claim(w)
-        self.side.wait_stream(self.main)
+        # one fork per weight gradient, issued as soon as dY is final: batching two behind one
+        # fork saves a marker but delays the first, -0.5% / -1.1% for 2 / 3 (fork_events_r05)
+        _stream_wait(self.side, self.main)
         with torch.cuda.stream(self.side):
             tgt = _grad_target(w)
             if _WS_GROUP:
@@ -466,15 +522,13 @@ class _WgradSide:
         when it ran here)."""
         if not self.on:
             return fn(), None
-        self.side.wait_stream(self.main)
+        _stream_wait(self.side, self.main)
         with torch.cuda.stream(self.side):
             r = fn()
         for t in keep:
             if t is not None and t.is_cuda:
                 t.record_stream(self.side)
-        ev = torch.cuda.Event()
-        ev.record(self.side)
-        return r, ev
+        return r, _record_on(self.side)
 
     def run(self, w, fn, keep=()):
         """Like :meth:`wgrad` for a weight gradient computed by ``fn(target)`` (target = the
@@ -492,7 +546,7 @@ class _WgradSide:
             _ready(w)
             return None
         _claim(w)
-        self.side.wait_stream(self.main)
+        _stream_wait(self.side, self.main)
         with torch.cuda.stream(self.side):
             fn(tgt.permute(0, 2, 3, 1))
         for t in keep:
@@ -516,13 +570,12 @@ class _WgradSide:
                 self.C.wgrad_flush()        # the block's split reductions: one launch
             self.deferred = False
         if not _WGRAD_STREAM["defer"]:
-            self.main.wait_stream(self.side)
+            _stream_wait(self.main, self.side)
             for w in self.ready:
                 _ready(w)
             self.ready = []
             return
-        ev = torch.cuda.Event()
-        ev.record(self.side)
+        ev = _record_on(self.side)
         pend = _WGRAD_STREAM.get("pending")
         if pend is None:
             pend = _WGRAD_STREAM["pending"] = []
@@ -535,7 +588,7 @@ class _WgradSide:
 
 def _join_pending(pend):
     main, ev, ws = pend
-    main.wait_event(ev)
+    _wait_on(main, ev)
     for w in ws:
         _ready(w)
 
@@ -657,9 +710,7 @@ def _after_dgrad_event(t, sync):
     if sync is None or not t.is_cuda or not getattr(sync, "overlap_bn_bwd", False) \
             or getattr(sync, "xgmi", None) is None:
         return None
-    ev = torch.cuda.Event()
-    ev.record()
-    return ev
+    return _record_on(torch.cuda.current_stream(t.device))
 
 
 # ---------------------------------------------------------------- BN pieces
@@ -766,12 +817,10 @@ def _bn_backward(P, dout, mask, relu, training, sync, count, y1, p1, bn1, y2=Non
             # the weight-gradient kernel(s) issued since, and join before bn_bwd_elemt
             # (and before the gamma/beta grads are marked ready for the reducer)
             side = sync.side_stream()
-            side.wait_event(ev)
+            _wait_on(side, ev)
             with torch.cuda.stream(side):
                 sync.bn_stats_bwd(r1, r2, acc1, acc2, red[:2 * c1], red[2 * c1:] if c2 else None)
-            done = torch.cuda.Event()
-            done.record(side)
-            torch.cuda.current_stream().wait_event(done)
+            _wait_on(torch.cuda.current_stream(), _record_on(side))
         else:
             sync.bn_stats_bwd(r1, r2, acc1, acc2, red[:2 * c1], red[2 * c1:] if c2 else None)
         P._release(r1, r2)
@@ -1046,7 +1095,7 @@ def _bnlin_prep(P, bn, p, wpack, z):
         return (*work(), None)
     side = _wgrad_stream(z.device)
     main = torch.cuda.current_stream(z.device)
-    side.wait_stream(main)
+    _stream_wait(side, main)
     with torch.cuda.stream(side):
         dpack, gz, cs = work()
     z.record_stream(side)
@@ -1054,9 +1103,7 @@ def _bnlin_prep(P, bn, p, wpack, z):
     for t in dpack:
         if t is not None:
             t.record_stream(main)
-    ev = torch.cuda.Event()
-    ev.record(side)
-    return dpack, gz, cs, ev
+    return dpack, gz, cs, _record_on(side)
 
 
 def _bnlin_final(P, dz, pre, training, sync, count, z, wpack, conv_m, bn, p, rec_prev, side, put, prep):
@@ -1082,7 +1129,7 @@ def _bnlin_final(P, dz, pre, training, sync, count, z, wpack, conv_m, bn, p, rec
     dpack, gz, cs, ev = prep
     T, _ = side.fork(lambda: P.conv_wgrad(dz, z, tuple(wk.shape), 1, 0), keep=(dz, z))
     if ev is not None:
-        torch.cuda.current_stream(dz.device).wait_event(ev)
+        _wait_on(torch.cuda.current_stream(dz.device), ev)
     dmain = P.conv_dgrad(dz, dpack, tuple(z.shape), 1, 0)             # dz diag(A) W
     state = {}
 

@@ -47,6 +47,10 @@ def _worker(rank, world, port, out, stats_comm="gloo", fault="none", model_name=
         comm.enable_xgmi(timeout_s=20.0)     # SyncBN statistics over the one-shot IPC kernel
         comm.xgmi.select_ordering(verbose=False)
     OF.set_bn_sync(comm)
+    if fault == "overlap":
+        # not a fault: the backward statistics exchange on the side stream from the event after
+        # the dgrad that produced its slots (PMD_SYNCBN_OVERLAP=1; the hand-offs on the fork ring)
+        comm.overlap_bn_bwd = True
     if fault == "stats_half" and rank == 1:
         # negative control: ONE SyncBN statistics site (the 4th forward exchange) contributes
         # half its partial sums on rank 1 -- a wrong statistic at a single site
@@ -153,7 +157,7 @@ def _oracle_violations(got, ms, loss, grads):
 
 
 @pytest.mark.parametrize("stats_comm,fault", [("gloo", "none"), ("xgmi", "none"), ("xgmi", "stats_half"),
-                                              ("xgmi", "skip_bucket")])
+                                              ("xgmi", "skip_bucket"), ("xgmi", "overlap")])
 def test_two_ranks_on_one_gpu_match_single_process_per_tensor(tmp_path, stats_comm, fault):
     """2 ranks x batch 32 of ResNet-18-ref through the production W>1 path (SyncBN over the
     xGMI kernel at the stress-selected ordering, native reducer) == one process on the
@@ -168,7 +172,7 @@ def test_two_ranks_on_one_gpu_match_single_process_per_tensor(tmp_path, stats_co
     worst = sorted(((e2[n] / max(e1[n], 1e-6), n) for n in e2), reverse=True)[:5]
     print(f"[{stats_comm}/{fault}] buckets {got['nbuckets']}, worst e2/e1: "
           + ", ".join(f"{n} {r:.2f}" for r, n in worst))
-    if fault == "none":
+    if fault in ("none", "overlap"):
         assert not bad, bad
     else:
         assert bad, f"negative control {fault} passed the per-tensor oracle"
