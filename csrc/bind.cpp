@@ -912,9 +912,10 @@ std::vector<Tensor> xent_fwd(Tensor logits, Tensor target) {
   Tensor lse = torch::empty({N}, logits.options());
   Tensor correct = pmd_zeros({1}, logits.options().dtype(torch::kInt64));
   Tensor tg = target.contiguous();
-  pmd::xent_fwd_launch(logits.data_ptr<float>(), reinterpret_cast<const long long*>(tg.data_ptr<int64_t>()),
-                       loss.data_ptr<float>(), lse.data_ptr<float>(),
-                       reinterpret_cast<long long*>(correct.data_ptr<int64_t>()), N, V, cur_stream());
+  CHECK_RC(pmd::xent_fwd_launch(logits.data_ptr<float>(), reinterpret_cast<const long long*>(tg.data_ptr<int64_t>()),
+                                loss.data_ptr<float>(), lse.data_ptr<float>(),
+                                reinterpret_cast<long long*>(correct.data_ptr<int64_t>()), N, V, cur_stream()),
+           "xent_fwd");
   return {loss, lse, correct};
 }
 
@@ -1176,6 +1177,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fp8_fwd_set_impl", [](int64_t i) { g_fp8_fwd_impl = (int)i; },
         "fp8 forward conv kernel: 0 conv_fp8_fwd_kernel, 1 the implicit-GEMM kernel's fp8 path (default), -1 env");
   m.def("conv_set_impl", &pmd::conv_set_impl, "conv staging/pipeline variant 0-4, 5 = per-shape default");
+  m.def("det_stats_set", &pmd::det_stats_set,
+        "deterministic BN-statistics mode (test/debug): private per-block slots folded in a fixed order");
+  m.def("det_stats_on", &pmd::det_stats_on);
+  m.def("gpu_sleep", [](int64_t us) { CHECK_RC(pmd::gpu_sleep_launch((int)us, cur_stream()), "gpu_sleep"); },
+        "test utility: idle the current stream for `us` microseconds (<= 1 s)");
   m.def("conv_set_tile", &pmd::conv_set_tile,
         "conv fwd/dgrad tile policy: 0 auto, 1 128-row only, 2 256x128, 3 256x256 where legal");
   m.def("conv_set_big_pipe", &pmd::conv_set_big_pipe,

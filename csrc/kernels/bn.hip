@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
                                                             const bf16_t* __restrict__ y,
                                                             const float* __restrict__ params,
                                                             float* __restrict__ red, int M, int C,
-                                                            int CT8) {
+                                                            int CT8, int nslots) {
   __shared__ float part[256 * 17];
   const int C8 = C >> 3;
   const int tid = threadIdx.x;
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
     float a = 0.f;
     for (int rr = 0; rr < rpi; ++rr) a += part[(rr * CT8 + col) * 17 + k];
     const int c = (blockIdx.y * CT8 + col) * 8 + (k & 7);
-    float* slot = red + (size_t)(blockIdx.x % kStatSlots) * 2 * C;
+    float* slot = red + stat_slot(blockIdx.x, nslots) * 2 * C;
     atomicAdd(slot + (k < 8 ? 0 : C) + c, a);
   }
 }
@@ -500,12 +500,16 @@ int bn_bwd_reduce_launch(const bf16_t* dout, const uint8_t* mask, const bf16_t* 
   if (b > bmax) b = bmax;
   if (b < 1) b = 1;
   const dim3 grid((unsigned)b, (unsigned)ctiles);
+  DetStats det;
+  const int ns = det_begin(det, &red, nullptr, (int)b, 2 * C, st);
+  if (ns < 1) return 2;
   if (relu)
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<true>), grid, dim3(256), 0, st, dout, mask, y, params, red,
-                       M, C, CT8);
+                       M, C, CT8, ns);
   else
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<false>), grid, dim3(256), 0, st, dout, mask, y, params,
-                       red, M, C, CT8);
+                       red, M, C, CT8, ns);
+  det_end(det, st);
   return 0;
 }
 

@@ -19,6 +19,14 @@ constexpr int kWave = 64;  // CDNA wavefront
 // atomics on the same 2C addresses; stats_collapse sums the slots.
 constexpr int kStatSlots = 64;
 
+// Slot of a producer block's statistics partial: row block rb -> rb % nslots of the
+// [nslots][2][C] slot copies.  nslots = kStatSlots in production: several blocks' fp32 atomics
+// land in one slot, so the low bits of a sum depend on their order.  The deterministic mode
+// (kernels/det.hip) hands the launch one private slot per row block of a zeroed scratch: every
+// address then receives exactly one atomic (0 + v: exact), and det_fold sums the slots in a
+// fixed order, so two identical steps are bit-identical.
+__device__ __forceinline__ size_t stat_slot(int rb, int nslots) { return (size_t)(rb % nslots); }
+
 // amax of a quantised tensor (fp8 delayed scaling): kAmaxSlots copies per site,
 // one per (block % kAmaxSlots), so thousands of blocks do not serialise on one
 // address; the host-side update takes the max over the slots.

@@ -78,6 +78,9 @@ struct ConvArgs {
   // mean, no sum row); out may be null (no store) -- the y part of sum dz * xhat that the
   // sum-only reduce of the producing dgrad left out
   int red_dot;
+  // statistics slots of stats / bn_red: a block of row tile rb adds into slot rb % nslots
+  // (kStatSlots; the deterministic mode's private scratch slots: det_begin, kernels/det.hip)
+  int nslots = kStatSlots;
 };
 typedef __attribute__((ext_vector_type(8))) int i32x8_c;
 
@@ -1141,7 +1144,7 @@ __global__ __launch_bounds__(64 * WM * WN,
 #pragma unroll
         for (int w = 0; w < WM; ++w) v += st[(w * 2 + which) * BN + col];
         if constexpr (!(PMD_TIMING_NO_ATOMICS & 1))  // timing-only A/B knob: what the statistics atomics cost
-          atomicAdd(a.stats + ((size_t)((m0 / BM) % kStatSlots) * 2 + which) * a.Nout + n0 + col, v);
+          atomicAdd(a.stats + (stat_slot(blockIdx.y * tilesM + mt, a.nslots) * 2 + which) * a.Nout + n0 + col, v);
       }
     }
   }
@@ -1289,7 +1292,7 @@ __global__ __launch_bounds__(64 * WM * WN,
         for (int r = col; r < NT; r += CPR) acc2 += part[r * PSTR + k];
         const int n = n0 + col * 8 + (k & 7);
         if (n < a.Nout && !(PMD_TIMING_NO_ATOMICS & 2) && !(a.red_dot && k < 8))
-          atomicAdd(a.bn_red[t] + ((size_t)((m0 / BM) % kStatSlots) * 2 + (k >> 3)) * a.Nout + n, acc2);
+          atomicAdd(a.bn_red[t] + (stat_slot(blockIdx.y * tilesM + mt, a.nslots) * 2 + (k >> 3)) * a.Nout + n, acc2);
       }
       __syncthreads();
     }
@@ -1662,6 +1665,7 @@ int conv_autotune_import(const std::vector<int>& flat) {
 template <bool DGRAD, bool STATS>
 static int tune(const ConvArgs& a0, hipStream_t st) {
   ConvArgs a = a0;
+  a.nslots = kStatSlots;  // the scratch sums below have kStatSlots slots (deterministic mode too)
   // the fused BN-backward reduce is part of the cost being compared (it decides
   // the epilogue-bound dgrads), so the timing runs keep it, aimed at scratch sums
   static float* scratch_red = nullptr;
@@ -1849,6 +1853,14 @@ void conv_set_fwd_apply(const float* p, const bf16_t* res, uint8_t* mask) {
 }
 void conv_set_red_dot(int on) { g_red_dot = on; }
 
+// deterministic mode: an upper bound of the launch's row-tile count over every tile choice
+// (BM >= 64; stride-2 dgrads run 4 phase grids of Mgrid rows; HALO tiles never straddle images)
+static int det_slot_bound(const ConvArgs& a) {
+  const bool ph2 = a.stride == 2;
+  const long long Mgrid = ph2 ? (long long)a.N * ((a.OH + 1) >> 1) * ((a.OW + 1) >> 1) : a.M;
+  return (int)((ph2 ? 4 : 1) * ((Mgrid + 63) / 64) + a.N);
+}
+
 static int conv_igemm_launch_b(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* stats, int N, int H,
                                int W, int Cs, int OH, int OW, int Nout, int R, int S, int stride, int pad,
                                bool dgrad, const bf16_t* addend, const uint8_t* addend_mask,
@@ -1919,6 +1931,13 @@ static int conv_igemm_launch_b(const bf16_t* src, const bf16_t* wt, bf16_t* out,
   a.Kg = R * S * Cs;
   a.f8_sa = nullptr;
   a.f8_sb = nullptr;
+  DetStats det;
+  if (stats && a.bn_red[0] && det_stats_on()) return 10;  // one slot count per launch
+  if (stats || a.bn_red[0]) {
+    a.nslots = det_begin(det, stats ? &a.stats : &a.bn_red[0], stats ? nullptr : &a.bn_red[1],
+                         det_slot_bound(a), 2 * Nout, st);
+    if (a.nslots < 1) return 10;
+  }
   if (dgrad) {
     if (stats) launch_sel<true, true>(a, st);
     else launch_sel<true, false>(a, st);
@@ -1926,6 +1945,7 @@ static int conv_igemm_launch_b(const bf16_t* src, const bf16_t* wt, bf16_t* out,
     if (stats) launch_sel<false, true>(a, st);
     else launch_sel<false, false>(a, st);
   }
+  det_end(det, st);
   return 0;
 }
 
@@ -1981,6 +2001,11 @@ int conv_fwd_fp8_igemm_launch(const uint8_t* xq, const uint8_t* wq, bf16_t* out,
   a.f8_sa = sx;
   a.f8_sb = sw;
   const bool one = a.Kg <= 512;
+  DetStats det;
+  if (stats) {
+    a.nslots = det_begin(det, &a.stats, nullptr, det_slot_bound(a), 2 * Nout, st);
+    if (a.nslots < 1) return 10;
+  }
 #define F8F(BMV, BNV)                                              \
   do {                                                             \
     if (one) {                                                     \
@@ -1994,6 +2019,7 @@ int conv_fwd_fp8_igemm_launch(const uint8_t* xq, const uint8_t* wq, bf16_t* out,
   if (a.Nout <= 64) F8F(128, 64);
   else F8F(128, 128);
 #undef F8F
+  det_end(det, st);
   return 0;
 }
 
@@ -2031,6 +2057,11 @@ int conv_dgrad_fp8_launch(const uint8_t* dyq, const uint8_t* wtq, const float* s
   a.f8_sa = sdy;
   a.f8_sb = sw;
   const bool one = a.Kg <= 512;  // <= 4 K-tiles: the short-reduction, epilogue-bound dgrads
+  DetStats det;
+  if (a.bn_red[0]) {
+    a.nslots = det_begin(det, &a.bn_red[0], &a.bn_red[1], det_slot_bound(a), 2 * Nout, st);
+    if (a.nslots < 1) return 10;
+  }
   if (a.Nout <= 64) {
     if (one) launch_f8<128, 64, true>(a, st);
     else launch_f8<128, 64, false>(a, st);
@@ -2038,6 +2069,7 @@ int conv_dgrad_fp8_launch(const uint8_t* dyq, const uint8_t* wtq, const float* s
     if (one) launch_f8<128, 128, true>(a, st);
     else launch_f8<128, 128, false>(a, st);
   }
+  det_end(det, st);
   return 0;
 }
 

@@ -263,6 +263,7 @@ struct Fp8ConvArgs {
   const float* sx;     // device scalars: the per-tensor scales the operands were quantised with
   const float* sw;
   int N, H, W, Cs, log2Cs, OH, OW, Nout, R, S, stride, pad, M, Kg;
+  int nslots;          // statistics slot count (stat_slot, common.h)
 };
 
 template <int BM, int BN, bool STATS>
@@ -432,7 +433,7 @@ __global__ __launch_bounds__(256, 2) void conv_fp8_fwd_kernel(Fp8ConvArgs a) {
       const int which = c / BN, col = c % BN;
       if (n0 + col < a.Nout) {
         const float v = st[which * BN + col] + st[(2 + which) * BN + col];
-        atomicAdd(a.stats + ((size_t)((m0 / BM) % kStatSlots) * 2 + which) * a.Nout + n0 + col, v);
+        atomicAdd(a.stats + (stat_slot(m0 / BM, a.nslots) * 2 + which) * a.Nout + n0 + col, v);
       }
     }
   }
@@ -469,6 +470,9 @@ int conv_fp8_fwd_launch(const uint8_t* x, const uint8_t* w, bf16_t* out, float* 
   a.Kg = R * S * C;
   const int BN = K <= 64 ? 64 : 128;
   const int tiles = (int)((M + 127) / 128) * ((K + BN - 1) / BN);
+  DetStats det;
+  a.nslots = det_begin(det, &a.stats, nullptr, (int)((M + 127) / 128), 2 * K, st);
+  if (a.nslots < 1) return 10;
   if (BN == 64) {
     if (stats) hipLaunchKernelGGL((conv_fp8_fwd_kernel<128, 64, true>), dim3(tiles), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((conv_fp8_fwd_kernel<128, 64, false>), dim3(tiles), dim3(256), 0, st, a);
@@ -476,6 +480,7 @@ int conv_fp8_fwd_launch(const uint8_t* x, const uint8_t* w, bf16_t* out, float* 
     if (stats) hipLaunchKernelGGL((conv_fp8_fwd_kernel<128, 128, true>), dim3(tiles), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((conv_fp8_fwd_kernel<128, 128, false>), dim3(tiles), dim3(256), 0, st, a);
   }
+  det_end(det, st);
   return 0;
 }
 

@@ -16,6 +16,21 @@ struct BnReduceArgs {
   const float* p[2];
   float* red[2];
 };
+// Deterministic statistics mode (test / debug, kernels/det.hip): det_begin swaps up to two
+// slot-buffer pointers of one launch (*p0, *p1) for private per-row-block scratch slots and
+// returns the slot count the kernel must index modulo (kStatSlots when the mode is off or
+// there is nothing to swap; -1 on failure); det_end folds them, in a fixed order, into slot 0
+// of the real buffers after the launch.
+struct DetStats {
+  float* real[2] = {nullptr, nullptr};
+  float* scr = nullptr;
+  int nslots = 0, width = 0, n = 0;
+};
+bool det_stats_on();
+void det_stats_set(bool on);
+int det_begin(DetStats& d, float** p0, float** p1, int nslots_bound, int width, hipStream_t st);
+int det_end(DetStats& d, hipStream_t st);
+int gpu_sleep_launch(int us, hipStream_t st);  // test utility: idle the stream for us microseconds
 // stats (optional): BN statistic slots [kStatSlots][2][Nout] of (sum (y-K), sum (y-K)^2) with
 // K = shift[n] (nullable: 0) -- see bn_moments in common.h
 int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* stats, int N, int H,

@@ -137,7 +137,7 @@ __global__ __launch_bounds__(256) void xent_fwd_kernel(const float* __restrict__
                                                        float* __restrict__ loss,
                                                        float* __restrict__ lse_out,
                                                        long long* __restrict__ correct, int N,
-                                                       int V) {
+                                                       int V, int nslots) {
   __shared__ float smax[4];
   __shared__ int sidx[4];
   __shared__ float ssum[4];
@@ -183,7 +183,7 @@ __global__ __launch_bounds__(256) void xent_fwd_kernel(const float* __restrict__
     const float lse = m + __logf(tot);
     const long long t = target[row];
     lse_out[row] = lse;
-    atomicAdd(loss, (lse - x[t]) / N);
+    atomicAdd(loss + row % nslots, (lse - x[t]) / N);  // nslots: 1 (deterministic mode: N)
     if (correct && mi == (int)t) atomicAdd((unsigned long long*)correct, 1ull);
   }
 }
@@ -291,8 +291,13 @@ int avgpool_bwd_launch(const float* dout, bf16_t* dx, int N, int HW, int C, hipS
 }
 int xent_fwd_launch(const float* logits, const long long* target, float* loss, float* lse,
                     long long* correct, int N, int V, hipStream_t st) {
+  DetStats det;  // deterministic mode: one slot per row, summed in row order
+  int ns = det_begin(det, &loss, nullptr, N, 1, st);
+  if (ns < 1) return 1;
+  if (!det.n) ns = 1;
   hipLaunchKernelGGL(xent_fwd_kernel, dim3(N), dim3(256), 0, st, logits, target, loss, lse, correct, N,
-                     V);
+                     V, ns);
+  det_end(det, st);
   return 0;
 }
 int xent_bwd_launch(const float* logits, const long long* target, const float* lse, const float* gloss,

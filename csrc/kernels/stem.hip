@@ -140,7 +140,7 @@ __device__ __forceinline__ void stem_stage_pooled(const bf16_t* __restrict__ dou
 __global__ __launch_bounds__(256) void stem_pool_bwd_reduce_kernel(
     const bf16_t* __restrict__ dout, const uint8_t* __restrict__ arg, const bf16_t* __restrict__ y,
     const float* __restrict__ params, float* __restrict__ red, int N, int H, int W, int C, int P, int Q,
-    int log2C8) {
+    int log2C8, int nslots) {
   extern __shared__ __attribute__((aligned(16))) unsigned char stem_lds[];
   const int C8 = C >> 3;
   const int tid = threadIdx.x;
@@ -186,7 +186,7 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_reduce_kernel(
     const int col = e >> 4, k = e & 15;
     float a = 0.f;
     for (int r = col; r < 256; r += C8) a += part[r * 17 + k];
-    float* slot = red + (size_t)(blockIdx.x % kStatSlots) * 2 * C;
+    float* slot = red + stat_slot(blockIdx.x, nslots) * 2 * C;
     atomicAdd(slot + (k < 8 ? 0 : C) + col * 8 + (k & 7), a);
   }
 }
@@ -282,8 +282,12 @@ int stem_pool_bwd_reduce_launch(const bf16_t* dout, const uint8_t* arg, const bf
   if (C % 8 || l < 0 || (C / 8) > 256 || 2 * P < H || 2 * Q < W) return 1;
   const size_t lds = stem_bwd_lds(Q, C);
   if (lds > 64 * 1024) return 2;
+  DetStats det;
+  const int ns = det_begin(det, &red, nullptr, N * P, 2 * C, st);
+  if (ns < 1) return 3;
   hipLaunchKernelGGL(stem_pool_bwd_reduce_kernel, dim3(N * P), dim3(256), lds, st, dout, arg, y, params, red,
-                     N, H, W, C, P, Q, l);
+                     N, H, W, C, P, Q, l, ns);
+  det_end(det, st);
   return 0;
 }
 

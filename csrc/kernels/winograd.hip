@@ -129,7 +129,8 @@ __global__ __launch_bounds__(256) void winograd_output_kernel(const bf16_t* __re
                                                               bf16_t* __restrict__ y,
                                                               float* __restrict__ stats,
                                                               const float* __restrict__ shift, int N,
-                                                              int H, int W, int K, int TH, int TW) {
+                                                              int H, int W, int K, int TH, int TW,
+                                                              int nslots) {
   const int K8 = K >> 3;
   const long long T = (long long)N * TH * TW;
   const long long total = T * K8;
@@ -205,7 +206,7 @@ __global__ __launch_bounds__(256) void winograd_output_kernel(const bf16_t* __re
     const int col = q >> 4, j = q & 15;
     float acc = 0.f;
     for (int r = col; r < 256; r += K8) acc += part[r][j];
-    atomicAdd(stats + ((size_t)(blockIdx.x % kStatSlots) * 2 + (j >> 3)) * K + col * 8 + (j & 7), acc);
+    atomicAdd(stats + (stat_slot(blockIdx.x, nslots) * 2 + (j >> 3)) * K + col * 8 + (j & 7), acc);
   }
 }
 
@@ -236,8 +237,13 @@ int winograd_output_launch(const bf16_t* M, bf16_t* y, float* stats, int N, int 
   const int K8 = K >> 3;
   if (K % 8 || K8 > 256 || (K8 & (K8 - 1))) return 1;  // 256-thread blocks: stride % K8 == 0
   const int TH = (H + 1) / 2, TW = (W + 1) / 2;
-  hipLaunchKernelGGL(winograd_output_kernel, dim3(ew_blocks((long long)N * TH * TW * K8)), dim3(256), 0,
-                     st, M, y, stats, shift, N, H, W, K, TH, TW);
+  const int blocks = ew_blocks((long long)N * TH * TW * K8);
+  DetStats det;
+  const int ns = det_begin(det, &stats, nullptr, blocks, 2 * K, st);
+  if (ns < 1) return 2;
+  hipLaunchKernelGGL(winograd_output_kernel, dim3(blocks), dim3(256), 0, st, M, y, stats, shift, N, H, W, K,
+                     TH, TW, ns);
+  det_end(det, st);
   return 0;
 }
 

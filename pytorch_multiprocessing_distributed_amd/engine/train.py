@@ -127,7 +127,12 @@ class GraphedStep:
         return self.out, self.loss
 
 
-_GRAPHS: dict = {}
+def _graph_of(optimizer):
+    """The optimizer's captured step (GraphedStep), or None.  Held BY the optimizer -- the
+    object whose arenas, momentum and device LR the graph updates in place -- so a later model /
+    optimizer in the same process never replays another's graph, and the graph and its memory
+    pool are freed with them."""
+    return getattr(optimizer, "_pmd_graph", None)
 
 
 def train_epoch(loader, model, optimizer, epoch, logger, args, rank, dev, comm=None,
@@ -145,10 +150,10 @@ def train_epoch(loader, model, optimizer, epoch, logger, args, rank, dev, comm=N
     for i, (inp, target) in enumerate(loader):
         data_time.update(time.time() - end)
         launch.maybe_inject_fault(rank, step_offset + i)
-        g = _GRAPHS.get(id(model)) if graphed else None
+        g = _graph_of(optimizer) if graphed else None
         if graphed and g is None and step_offset + i >= 2:
             # steps 0-1 ran eagerly: kernel choices tuned, lazy state initialised
-            g = _GRAPHS[id(model)] = GraphedStep(model, optimizer, inp, target)
+            g = optimizer._pmd_graph = GraphedStep(model, optimizer, inp, target)
         if g is not None and g.fits(inp, target):
             with region("graph"):
                 output, loss = g(inp, target)

@@ -50,7 +50,25 @@ _state = {"bn_sync": None, "force_torch": os.environ.get("PMD_PRIMS", "") == "to
           "fused_site_misses": 0,
           "fused_stem": os.environ.get("PMD_FUSED_STEM", "1") != "0",
           "fp8": None,          # Fp8Scaling when the block convs run in fp8 (config 5)
-          "wimg": None}         # WeightImageSet of the running forward (grouped weight prep)
+          "wimg": None,         # WeightImageSet of the running forward (grouped weight prep)
+          "det": os.environ.get("PMD_DET_STATS", "0") == "1"}   # set_deterministic
+
+
+def set_deterministic(flag: bool):
+    """Deterministic BN-statistics mode (test / debug; kernels/det.hip): every statistics
+    producer adds into private per-row-block slots that are folded in a fixed order, the loss
+    sum likewise, and the linear-BN backward (LDS atomics) is off, so two identical steps --
+    or one step with its stream hand-offs on different event mechanisms, or a HIP-graph replay
+    and the eager step it captured -- give bit-identical gradients, parameters and statistics.
+    Slower (one extra fold launch per statistics producer); never on in production.
+    ``PMD_DET_STATS=1`` turns it on at import."""
+    _state["det"] = bool(flag)
+    from .native import C
+    C.det_stats_set(bool(flag))
+
+
+def deterministic() -> bool:
+    return _state.get("det", False)
 
 
 def set_bn_sync(comm):
@@ -360,6 +378,20 @@ def _stream_wait(waiter, producer):
         ring.fork(producer.cuda_stream, waiter.cuda_stream)
 
 
+# test hook (negative controls of the hand-off tests): the fork whose running count reaches 0 is
+# SKIPPED -- the side stream then runs without waiting for the main stream's producer
+_DROP_FORK = [-1]
+
+
+def _fork(side, main):
+    """The side stream forks from the main stream: it waits for everything issued on main."""
+    if _DROP_FORK[0] >= 0:
+        _DROP_FORK[0] -= 1
+        if _DROP_FORK[0] < 0:
+            return
+    _stream_wait(side, main)
+
+
 class _RingEvent:
     __slots__ = ("ring", "slot")
 
@@ -494,7 +526,7 @@ class _WgradSide:
         _claim(w)
         # one fork per weight gradient, issued as soon as dY is final: batching two behind one
         # fork saves a marker but delays the first, -0.5% / -1.1% for 2 / 3 (fork_events_r05)
-        _stream_wait(self.side, self.main)
+        _fork(self.side, self.main)
         with torch.cuda.stream(self.side):
             tgt = _grad_target(w)
             if _WS_GROUP:
@@ -522,7 +554,7 @@ class _WgradSide:
         when it ran here)."""
         if not self.on:
             return fn(), None
-        _stream_wait(self.side, self.main)
+        _fork(self.side, self.main)
         with torch.cuda.stream(self.side):
             r = fn()
         for t in keep:
@@ -546,7 +578,7 @@ class _WgradSide:
             _ready(w)
             return None
         _claim(w)
-        _stream_wait(self.side, self.main)
+        _fork(self.side, self.main)
         with torch.cuda.stream(self.side):
             fn(tgt.permute(0, 2, 3, 1))
         for t in keep:
@@ -643,7 +675,8 @@ _BNLIN_MIN = int(os.environ.get("PMD_BNLIN_MIN", str(200704 * 512)))   # M * K o
 
 
 def _bnlin_eligible(conv_m, yf, x, training, fuse, shortcut, f8):
-    if _BNLIN == "0" or not (training and fuse) or shortcut is not None or f8 is not None:
+    if (_BNLIN == "0" or not (training and fuse) or shortcut is not None or f8 is not None
+            or _state.get("det")):   # its reductions are LDS-atomic (not in the deterministic mode)
         return False
     ks = conv_m.kernel_size if isinstance(conv_m.kernel_size, tuple) else (conv_m.kernel_size,) * 2
     st = conv_m.stride if isinstance(conv_m.stride, tuple) else (conv_m.stride,) * 2

@@ -104,6 +104,8 @@ def _load():
 
 
 C = _load()
+if os.environ.get("PMD_DET_STATS", "0") == "1":   # deterministic statistics (ops/functional.py)
+    C.det_stats_set(True)
 
 
 def available() -> bool:

@@ -5,8 +5,12 @@ main <-> weight-gradient stream hand-offs (ops/functional.py PMD_FORK_EVENTS):
   fork -> the side stream reads it; the side stream writes -> join -> main reads, 200 rounds on
   double buffers (a stale line in any XCD's L2 would show as a wrong value);
 * the two-stream ResNet-18-ref backward with its fork / join points on the ring (no system
-  fence) gives the same parameter gradients as with torch's events, per tensor, up to the
-  backward's own run-to-run noise (the order of the statistics atomics)."""
+  fence) gives BIT-IDENTICAL parameter gradients, BN running statistics and losses to the same
+  backward on torch's events, in the deterministic statistics mode (ops/functional.py
+  set_deterministic: private per-block statistic slots folded in a fixed order), with and
+  without the main stream held back so the side stream really waits at every fork;
+* negative control: the same comparison with ONE fork dropped (the side stream reads dY before
+  the main stream has produced it) must fail."""
 import copy
 
 import pytest
@@ -56,49 +60,90 @@ def test_ring_handoffs_exact(mode, n):
     assert ring.query(slot)
 
 
-def test_two_stream_step_on_ring_matches_torch_events(monkeypatch):
-    """One backward per batch (no optimizer step, so no chaotic amplification), 3 batches, two
-    runs with torch's events and two on the ring: every parameter gradient of a ring run is
-    within 4x the torch-vs-torch spread of that tensor (floor: half the median spread) -- the
-    statistics atomics' order is the only nondeterminism; a stale hand-off would be O(1)."""
+def _grads(mode, m0, batches, lag_us=0, drop=-1):
+    """Per-tensor parameter gradients (+ running statistics, losses) of one backward per batch
+    (no optimizer step) on the two-stream schedule, the hand-offs on torch events (mode -1) or
+    the native ring (mode >= 0).  lag_us: the main stream idles that long before each
+    backward, so every fork is taken while the side stream's work is ahead of its producer;
+    drop >= 0: the fork with that index in each backward is skipped (negative control)."""
     from pytorch_multiprocessing_distributed_amd.engine.optim import FusedSGD
-    from pytorch_multiprocessing_distributed_amd.models import build_model
     from pytorch_multiprocessing_distributed_amd.ops import functional as OF
     from pytorch_multiprocessing_distributed_amd.ops.native import C
     from pytorch_multiprocessing_distributed_amd.parallel.dp import DataParallel
-    dev = torch.device("cuda", 0)
-    OF.init_step_streams(dev)
-    OF.set_wgrad_stream(True)
-    torch.manual_seed(0)
-    m0 = build_model("res", num_classes=10, stem="cifar").to(dev)
-    batches = [C.synth_images(32, 32, 32, 8, 3, 10, 11 + s, 0) for s in range(3)]
-    runs = {}
-    for name, mode in (("warm", -1), ("torch", -1), ("ring", 1), ("torch2", -1), ("ring2", 1)):
-        monkeypatch.setattr(OF, "_FORK_EV", mode)
-        OF._RINGS.clear()
-        m = DataParallel(copy.deepcopy(m0), None)
-        m.train()
-        opt = FusedSGD(m, lr=0.01, momentum=0.9, weight_decay=1e-4, nesterov=True)
-        grads = []
+    OF._FORK_EV = mode
+    OF._RINGS.clear()
+    m = DataParallel(copy.deepcopy(m0), None)
+    m.train()
+    opt = FusedSGD(m, lr=0.01, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    grads, losses = [], []
+    try:
         for x, y in batches:
             loss = OF.cross_entropy(m(x), y)
             opt.zero_grad()
+            if lag_us:
+                C.gpu_sleep(lag_us)
+            OF._DROP_FORK[0] = drop
             loss.backward(OF.loss_seed(loss))
+            OF._DROP_FORK[0] = -1
             torch.cuda.synchronize()
             g = opt.flat.grad_arena
             grads += [g[o:o + p.numel()].clone() for p, o in zip(opt.flat.params, opt.flat.offsets)]
+            losses.append(loss.detach().clone())
         if mode >= 0:
-            ring = OF._RINGS[dev]
+            ring = OF._RINGS[batches[0][0].device]
             assert ring.mode == mode and ring.records > 5 * len(batches)   # the step used the ring
-        runs[name] = grads
-    OF._RINGS.clear()
-    ref = runs["torch"]
-    noise = [_rel(a, b) for a, b in zip(runs["torch2"], ref)]
-    med = sorted(noise)[len(noise) // 2]
-    bad = []
-    for name in ("ring", "ring2"):
-        for i, (g, r) in enumerate(zip(runs[name], ref)):
-            err = _rel(g, r)
-            if err > 4 * max(noise[i], 0.5 * med) + 1e-4:
-                bad.append((name, i, err, noise[i]))
-    assert not bad, bad[:10]
+    finally:
+        OF._DROP_FORK[0] = -1
+        OF._RINGS.clear()
+    running = [v.clone() for k, v in m.module.state_dict().items() if "running" in k]
+    return grads, running, losses
+
+
+def _differences(a, b):
+    return [i for i, (x, y) in enumerate(zip(a, b)) if not torch.equal(x, y)]
+
+
+@pytest.fixture
+def det_two_stream(monkeypatch):
+    from pytorch_multiprocessing_distributed_amd.models import build_model
+    from pytorch_multiprocessing_distributed_amd.ops import functional as OF
+    from pytorch_multiprocessing_distributed_amd.ops.native import C
+    dev = torch.device("cuda", 0)
+    OF.init_step_streams(dev)
+    OF.set_wgrad_stream(True)
+    monkeypatch.setattr(OF, "_FORK_EV", OF._FORK_EV)
+    OF.set_deterministic(True)
+    try:
+        torch.manual_seed(0)
+        m0 = build_model("res", num_classes=10, stem="cifar").to(dev)
+        batches = [C.synth_images(32, 32, 32, 8, 3, 10, 11 + s, 0) for s in range(3)]
+        _grads(-1, m0, batches)            # tunes the kernel choices, sizes the scratch
+        yield m0, batches
+    finally:
+        OF.set_deterministic(False)
+
+
+@pytest.mark.parametrize("lag_us", [0, 20000])
+def test_two_stream_step_on_ring_is_bit_exact(det_two_stream, lag_us):
+    m0, batches = det_two_stream
+    ref = _grads(-1, m0, batches)
+    again = _grads(-1, m0, batches, lag_us)
+    # the deterministic mode itself: two torch-event runs agree bit for bit
+    for a, b in zip(ref, again):
+        assert not _differences(a, b), "deterministic mode is not deterministic"
+    for mode in (0, 1, 2):
+        got = _grads(mode, m0, batches, lag_us)
+        for what, a, b in zip(("grads", "running", "losses"), got, ref):
+            bad = _differences(a, b)
+            assert not bad, (mode, what, bad[:10])
+
+
+def test_dropped_fork_is_caught(det_two_stream):
+    """Negative control: the first fork of every backward skipped (its weight gradient reads dY
+    while the main stream is still held back) -- the bit-exact oracle must see it."""
+    m0, batches = det_two_stream
+    ref = _grads(-1, m0, batches)
+    got = _grads(1, m0, batches, lag_us=20000, drop=0)
+    assert _differences(got[0], ref[0]), "a dropped fork went unnoticed"
+    # the control breaks only the weight gradient it hands off: the main-stream state agrees
+    assert not _differences(got[1], ref[1])
