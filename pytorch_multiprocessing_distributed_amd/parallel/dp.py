@@ -137,11 +137,16 @@ def resolve_transport(comm, module, reducer="native", transport="auto", verbose=
         return "c10d", None
     from . import rccl
     c, err = None, ""
-    try:
+
+    def stream_spec():
         from ..ops.functional import STREAM_PRIO, comm_stream_handle
-        # collective and all-or-nothing: raises on EVERY rank when any rank failed, before
-        # any native collective runs (ADVICE r4), so the self-test below runs on all or none
-        c = rccl.create(comm.group, priority=STREAM_PRIO, stream=comm_stream_handle())
+        return STREAM_PRIO, comm_stream_handle()
+
+    try:
+        # collective and all-or-nothing: raises on EVERY rank when any rank failed -- also in
+        # resolving the stream, which happens inside the agreement -- before
+        # any native collective runs, so the self-test below runs on all or none
+        c = rccl.create(comm.group, stream_spec=stream_spec)
     except Exception as e:  # noqa: BLE001
         err = str(e)
     ok = rccl.self_test(c, comm.group) if c is not None else False

@@ -83,7 +83,7 @@ def _fault_here(stage: str) -> bool:
 
 
 def create(group=None, priority: int = 0, store=None, stream: int = 0, init_timeout_s: float | None = None,
-           factory=None, uid_fn=None):
+           factory=None, uid_fn=None, stream_spec=None):
     """Collective over ``group`` (every rank calls it).  Returns ``_C.RcclComm``, or raises
     the SAME RuntimeError on every rank: no rank ever enters a native collective
     that a peer will not join.
@@ -99,12 +99,12 @@ def create(group=None, priority: int = 0, store=None, stream: int = 0, init_time
          failure each rank aborts its own communicator and raises.
 
     ``factory(uid, rank, world, device, priority, stream, timeout)`` / ``uid_fn()``: test
-    doubles for the native constructor / ncclGetUniqueId (tests/test_readiness_cpu.py)."""
-    from ..ops.native import C
+    doubles for the native constructor / ncclGetUniqueId (tests/test_readiness_cpu.py).
+    ``stream_spec()`` -> (priority, stream handle): resolved HERE, inside the agreement
+    protocol, so a rank failing to produce them fails the creation on every rank
+    instead of skipping ``create`` while its peers wait in its first agreement."""
     if not dist.is_initialized():
         raise RuntimeError("torch.distributed must be initialised first (it hosts the TCPStore)")
-    factory = factory or C.RcclComm
-    uid_fn = uid_fn or C.RcclComm.unique_id
     if init_timeout_s is None:
         init_timeout_s = float(os.environ.get("PMD_RCCL_INIT_TIMEOUT", "300"))
     rank = dist.get_rank(group)
@@ -112,7 +112,18 @@ def create(group=None, priority: int = 0, store=None, stream: int = 0, init_time
     store = store if store is not None else _store()
     key = f"pmd_rccl_uid_{next(_SEQ)}"
     err = ""
-    if rank == 0:
+    try:
+        if factory is None or uid_fn is None:
+            from ..ops.native import C
+            factory = factory or C.RcclComm
+            uid_fn = uid_fn or C.RcclComm.unique_id
+        if stream_spec is not None:
+            priority, stream = stream_spec()
+    except Exception as e:  # noqa: BLE001 -- agreed on below, with every peer
+        err = f"rank {rank}: communicator prerequisites: {e}"
+    if rank == 0 and err:
+        store.set(key, b"ERR:" + err.encode()[:200])
+    elif rank == 0:
         try:
             if _fault_here("uid"):
                 raise RuntimeError("injected unique-id failure (PMD_FAULT_RCCL_CREATE)")

@@ -219,6 +219,12 @@ class XgmiAllReduce:
                           f"interleaved calls, rank {self.world_size - 1} skewed, exact)", flush=True)
                 return name
             tried.append(f"{name}: {getattr(self, 'last_stress', {})}")
+            # a failed attempt -- also a timed-out self_test, after which stress_test (the one
+            # that clears the error words) never ran -- must not leave the next ordering starting
+            # with the error word set: clear it on every rank together
+            torch.cuda.synchronize()
+            self._c.reset_error()
+            dist.barrier(group=self.group)
         raise RuntimeError("xGMI exchange failed its stress self-test under every ordering ("
                            + "; ".join(tried) + ")")
 

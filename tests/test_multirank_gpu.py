@@ -72,16 +72,16 @@ def _defer_worker(rank, world, port, out, defer):
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
     OF._WGRAD_STREAM["on"] = True
     OF._WGRAD_STREAM["defer"] = defer
+    OF.set_deterministic(True)          # bit-exact oracle (kernels/det.hip)
     comm = get_comm()
     comm.enable_xgmi(timeout_s=20.0)
     OF.set_bn_sync(comm)
     torch.manual_seed(0)
     model = build_model("resnet50", num_classes=10, stem="imagenet").cuda()
     dp = DataParallel(model, comm, bucket_mb=2.0, first_bucket_mb=0.5)
-    # BN in eval mode: training-mode BN at random init makes the gradient chaotic
-    # (tests/test_model_oracle_gpu.py: a 2^-9 input perturbation moves it ~100%),
-    # which would drown a schedule bug in fp32-atomic ordering noise.  The
-    # reducer, the bucket rebuild and the deferred side-stream wgrads run the same.
+    # BN in eval mode: the reducer, the bucket rebuild and the deferred side-stream wgrads
+    # run the same as in training; the deterministic statistics mode makes every run of
+    # the step bit-reproducible, so the schedules are compared exactly.
     dp.module.eval()
     # lr=0: the weights stay fixed, so every step's averaged gradients must agree
     # between the deferred and the per-block join (a race on the last bucket, or
@@ -124,19 +124,14 @@ def test_deferred_wgrad_buckets_fire_once_and_match(tmp_path):
             if it > 0:
                 assert len(order) == r["nb"], (tag, it, order)
 
-    def rel(x, y):
-        num = sum(((x[k] - y[k]) ** 2).sum() for k in x)
-        den = sum((y[k] ** 2).sum() for k in y)
-        return (num / den).sqrt().item()
-    # Same averaged gradients at every step with and without the deferred join.
-    # Two runs of the SAME schedule differ only by fp32-atomic summation order
-    # (split-K weight gradients): that run-to-run spread is the noise floor.  A
-    # double all-reduce (factor 2) or a torn bucket (O(1)) is far above it.
+    # The same averaged gradients, bit for bit, at every step: the same schedule twice
+    # (d1, d1b) and with / without the deferred join (d0).  A double all-reduce, a torn
+    # bucket or a gradient read before its side-stream producer finished cannot hide in it.
     for step in range(3):
-        floor = rel(res["d1b"]["grads"][step], res["d1"]["grads"][step])
-        diff = rel(res["d0"]["grads"][step], res["d1"]["grads"][step])
-        assert diff < 4 * floor + 5e-3, (step, diff, floor)
-        assert diff < 2e-2, (step, diff, floor)
+        for tag in ("d1b", "d0"):
+            a, b = res[tag]["grads"][step], res["d1"]["grads"][step]
+            bad = [k for k in b if not torch.equal(a[k], b[k])]
+            assert not bad, (tag, step, bad[:5])
 
 
 # ------------------------------------------------------------- native RCCL comm

@@ -233,7 +233,8 @@ def _create_worker(rank, world, port, out, fault, peer_init_fails):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    if fault:
+    spec_fails = fault.startswith("spec:")     # stream_spec() raising on that rank
+    if fault and not spec_fails:
         os.environ["PMD_FAULT_RCCL_CREATE"] = fault
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
     made = []
@@ -253,7 +254,12 @@ def _create_worker(rank, world, port, out, fault, peer_init_fails):
     t0 = time.time()
     res = {"rank": rank}
     try:
-        c = rccl.create(factory=factory, uid_fn=lambda: b"u" * 128, init_timeout_s=1.0)
+        def stream_spec():
+            if spec_fails and int(fault[5:]) == rank:
+                raise ImportError("injected: the step streams could not be resolved")
+            return 0, 0
+        c = rccl.create(factory=factory, uid_fn=lambda: b"u" * 128, init_timeout_s=1.0,
+                        stream_spec=stream_spec)
         res.update(ok=True, uid=c.uid == b"u" * 128)
     except RuntimeError as e:
         res.update(ok=False, err=str(e))
@@ -268,7 +274,7 @@ def _create_worker(rank, world, port, out, fault, peer_init_fails):
 
 
 @pytest.mark.parametrize("fault,peer_init_fails", [("", False), ("1:init", False), ("0:uid", False),
-                                                   ("", True)])
+                                                   ("", True), ("spec:1", False), ("spec:0", False)])
 def test_rccl_create_is_all_or_nothing(tmp_path, fault, peer_init_fails):
     """a communicator-creation failure on ONE rank must not leave its peers stuck in
     ncclCommInitRank / the self-test.  Every rank agrees (c10d MIN) before the init and after
