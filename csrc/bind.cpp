@@ -119,70 +119,6 @@ static std::vector<Tensor> conv_fwd_impl(Tensor x, Tensor wk, int64_t stride, in
   return {y};
 }
 
-// statistics-only forward (_bnfold, ops/functional.py): the BN sums of conv(x) about
-// `shift`, no output written -- the BN-apply pass (conv_fwd_apply) recomputes the tile
-Tensor conv_fwd_stats(Tensor x, Tensor wk, int64_t stride, int64_t pad, c10::optional<Tensor> stats_buf,
-                      c10::optional<Tensor> shift) {
-  return conv_fwd_impl(x, wk, stride, pad, true, stats_buf, -1, -1, shift, false)[0];
-}
-
-// forward with the BN-apply epilogue: out = relu(conv(x) * p[2] + p[3] [+ res]) and its
-// ReLU bitmask (uint8 per 8-channel chunk), i.e. bn_apply(conv(x), p, res) without the
-// conv output ever reaching memory
-std::vector<Tensor> conv_fwd_apply(Tensor x, Tensor wk, int64_t stride, int64_t pad, Tensor p,
-                                   c10::optional<Tensor> res) {
-  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONT(x);
-  CHECK_DEV(wk); CHECK_BF16(wk); CHECK_CONT(wk);
-  CHECK_DEV(p); CHECK_F32(p); CHECK_CONT(p);
-  TORCH_CHECK(x.dim() == 4 && wk.dim() == 4 && wk.size(3) == x.size(3), "x [N,H,W,C], wk [K,R,S,C]");
-  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
-  const int K = wk.size(0), R = wk.size(1), S = wk.size(2);
-  TORCH_CHECK(p.numel() == 4 * K, "BN params must be [4, K]");
-  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
-  c10::DeviceGuard g(x.device());
-  Tensor y = torch::empty({N, P, Q, K}, x.options());
-  Tensor mask = torch::empty({(int64_t)N * P * Q * K / 8}, x.options().dtype(torch::kUInt8));
-  const pmd::bf16_t* r = nullptr;
-  if (res && res->defined()) {
-    CHECK_DEV(*res); CHECK_BF16(*res); CHECK_CONT(*res);
-    TORCH_CHECK(res->sizes() == y.sizes(), "residual shape");
-    r = bfp(*res);
-  }
-  pmd::conv_set_fwd_apply(p.data_ptr<float>(), r, mask.data_ptr<uint8_t>());
-  const int rc = pmd::conv_igemm_launch(bfp(x), bfp(wk), bfp_mut(y), nullptr, N, H, W, C, P, Q, K, R, S,
-                                        (int)stride, (int)pad, false, nullptr, nullptr, nullptr, cur_stream(),
-                                        nullptr);
-  pmd::conv_set_fwd_apply(nullptr, nullptr, nullptr);
-  CHECK_RC(rc, "conv_fwd_apply");
-  return {y, mask};
-}
-
-// red[slot][1][n] += invstd[n] * sum_m dz[m][n] * y[m][n] with y = z W^T RECOMPUTED (1x1,
-// stride 1; wk = the forward image [K,1,1,C]) -- nothing stored.  Completes the sum-only
-// fused reduce of the dgrad that produced dz for a BN whose input was never written (_bnfold).
-void conv_bn_dot(Tensor z, Tensor wk, Tensor dz, Tensor p, Tensor red) {
-  CHECK_DEV(z); CHECK_BF16(z); CHECK_CONT(z);
-  CHECK_DEV(wk); CHECK_BF16(wk); CHECK_CONT(wk);
-  CHECK_DEV(dz); CHECK_BF16(dz); CHECK_CONT(dz);
-  CHECK_F32(p); CHECK_CONT(p); CHECK_F32(red); CHECK_CONT(red);
-  TORCH_CHECK(z.dim() == 4 && wk.dim() == 4 && wk.size(1) == 1 && wk.size(2) == 1 && wk.size(3) == z.size(3),
-              "conv_bn_dot: z [N,H,W,C], wk [K,1,1,C]");
-  const int N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3), K = wk.size(0);
-  TORCH_CHECK(dz.sizes() == torch::IntArrayRef({N, H, W, K}), "conv_bn_dot: dz must be [N,H,W,K]");
-  TORCH_CHECK(p.numel() == 4 * K && red.numel() == pmd_slots() * 2 * K, "conv_bn_dot: params [4,K], red [S,2,K]");
-  c10::DeviceGuard g(z.device());
-  pmd::BnReduceArgs bnr{};
-  bnr.y[0] = bfp(dz);
-  bnr.p[0] = p.data_ptr<float>();
-  bnr.red[0] = red.data_ptr<float>();
-  // the GEMM z W^T is the dgrad of a 1x1 conv whose dgrad image ([Nout = K][Kg = C]) is wk
-  pmd::conv_set_red_dot(1);
-  const int rc = pmd::conv_igemm_launch(bfp(z), bfp(wk), nullptr, nullptr, N, H, W, C, H, W, K, 1, 1, 1, 0,
-                                        true, nullptr, nullptr, &bnr, cur_stream(), nullptr);
-  pmd::conv_set_red_dot(0);
-  CHECK_RC(rc, "conv_bn_dot");
-}
-
 std::vector<Tensor> conv_fwd(Tensor x, Tensor wk, int64_t stride, int64_t pad, bool want_stats,
                              c10::optional<Tensor> stats_buf, c10::optional<Tensor> shift) {
   return conv_fwd_impl(x, wk, stride, pad, want_stats, stats_buf, -1, -1, shift);
@@ -1228,11 +1164,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("eval_mode"), py::arg("shift") = py::none());
   m.def("bn_apply", &bn_apply, py::arg("y1"), py::arg("p1"), py::arg("res"), py::arg("y2"), py::arg("p2"),
         py::arg("relu"), py::arg("want_mask"), py::arg("q8_scale"), py::arg("q8_amax"), py::arg("q8_only") = false);
-  m.def("conv_fwd_stats", &conv_fwd_stats, py::arg("x"), py::arg("wk"), py::arg("stride"), py::arg("pad"),
-        py::arg("stats_buf") = py::none(), py::arg("shift") = py::none());
-  m.def("conv_fwd_apply", &conv_fwd_apply, py::arg("x"), py::arg("wk"), py::arg("stride"), py::arg("pad"),
-        py::arg("p"), py::arg("res") = py::none());
-  m.def("conv_bn_dot", &conv_bn_dot);
   m.def("stats_collapse", &stats_collapse);
   m.def("stats_finalize_local", &stats_finalize_local, py::arg("slots"), py::arg("count"), py::arg("gamma"),
         py::arg("beta"), py::arg("eps"), py::arg("rm"), py::arg("rv"), py::arg("momentum"), py::arg("nbt"),

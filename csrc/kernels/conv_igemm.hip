@@ -67,17 +67,6 @@ struct ConvArgs {
   // (byte pointers behind the bf16_t* fields); acc is scaled by 1 / (f8_sa * f8_sb)
   const float* f8_sa;
   const float* f8_sb;
-  // BN-apply epilogue of a forward conv without statistics (the block-final BN folded into
-  // its conv3, ops/functional.py _bnfold): out = relu(bf16(acc) * ap_p[2][n] + ap_p[3][n]
-  // [+ ap_res]) and the ReLU bitmask ap_mask -- the math of bn_apply_kernel<1> on the tile
-  const float* ap_p;
-  const bf16_t* ap_res;
-  uint8_t* ap_mask;
-  // dot-only fused reduce (dgrad kernel, 1 set): the GEMM tile is a RECOMPUTED BN input y,
-  // bn_y[0] is dz, and only red[slot][1][n] += invstd[n] * sum dz * y is accumulated (zero
-  // mean, no sum row); out may be null (no store) -- the y part of sum dz * xhat that the
-  // sum-only reduce of the producing dgrad left out
-  int red_dot;
   // statistics slots of stats / bn_red: a block of row tile rb adds into slot rb % nslots
   // (kStatSlots; the deterministic mode's private scratch slots: det_begin, kernels/det.hip)
   int nslots = kStatSlots;
@@ -217,17 +206,9 @@ __global__ __launch_bounds__(64 * WM * WN,
   constexpr int A_ELEMS = BM * LDR;
   constexpr int B_ELEMS = BN * LDR;
   constexpr int STAGE = A_ELEMS + B_ELEMS;
-  // PMD_EPI_X (SWAPC, 128-column tiles): the C tile staged UNPADDED (LDC = BN) with the 16-B
-  // chunk index XORed by the row's low 4 bits (+ the EPI_SW half swap), conflict-free for the
-  // ds_write_b64 groups and the ds_read_b128 row reads alike -- 32 KB instead of 34 KB, so the
-  // 128x128 dgrad (32 KB mainloop) fits a CU next to two 64 KB weight-gradient blocks of the
-  // side stream (160 KB) instead of waiting for one to retire.  Measured -0.3% on the step
-  // (13,428 / 13,484 vs 13,473 / 13,508 img/s, profiles/epi_x_r05.txt): A/B only, off
-#ifndef PMD_EPI_X
-#define PMD_EPI_X 0
-#endif
-  constexpr bool EPI_X = PMD_EPI_X && PMD_CONV_SWAPC && !STATS && !MF32 && BN == 128 && NT == 256;
-  constexpr int LDC = EPI_X ? BN : BN + 8;
+  // C tile staged with 8 elements of row padding (an unpadded XOR-swizzled staging, 32 instead of
+  // 34 KB, measured -0.3% on the step: profiles/epi_x_r05.txt)
+  constexpr int LDC = BN + 8;
   // epilogue C-staging layout (SWAPC only): EPI_SW = 8-B half swap in rows with bit 3
   // set (conflict-free ds_write_b64); EPI_RM = row order of the ds_read_b128 row reads
   // for 16-chunk rows read by 16 thread rows (BN = 128, 4 waves): the two 16-lane
@@ -237,7 +218,7 @@ __global__ __launch_bounds__(64 * WM * WN,
 #define PMD_EPI_SW 1
 #endif
   constexpr bool EPI_SW = PMD_EPI_SW && SWAPC;
-  constexpr bool EPI_RM = PMD_EPI_SW && SWAPC && BN == 128 && NT == 256 && !EPI_X;
+  constexpr bool EPI_RM = PMD_EPI_SW && SWAPC && BN == 128 && NT == 256;
   constexpr bool EPI_RM64 = PMD_EPI_SW >= 2 && SWAPC && BN == 64 && NT == 256;
   // HALO image: at most ceil(BM / W) + 3 input rows of W + 2 pixels (a tile spans
   // ceil(BM / W) + 1 rows, plus the two halo rows), 8 chunks each, rounded up to whole
@@ -923,7 +904,7 @@ __global__ __launch_bounds__(64 * WM * WN,
         bsum[t][e] = bdot[t][e] = 0.f;
         bmean[t][e] = 0.f;
       }
-    if (nbn && n < a.Nout && !a.red_dot) {
+    if (nbn && n < a.Nout) {
 #pragma unroll
       for (int t = 0; t < NBA; ++t)
         if (t < nbn)
@@ -960,24 +941,6 @@ __global__ __launch_bounds__(64 * WM * WN,
 #pragma unroll
     for (int e = 0; e < 8; ++e) abias[e] = a.addend_bias[n0 + (tid % (BN / 8)) * 8 + e];
   }
-  // BN-apply epilogue (forward without statistics only: the statistics kernels keep their
-  // register budget): this thread's 8 channels' scale / shift, loaded once
-  constexpr bool CAN_APPLY = !DGRAD && !STATS && !MF32 && !F8;
-  const bool apply = CAN_APPLY && a.ap_p;
-  const bool ap_has_res = apply && a.ap_res;
-  float asc[CAN_APPLY ? 8 : 1], ash[CAN_APPLY ? 8 : 1];
-  if constexpr (CAN_APPLY) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) asc[e] = ash[e] = 0.f;
-    const int na = n0 + (tid % (BN / 8)) * 8;
-    if (apply && na < a.Nout) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        asc[e] = a.ap_p[2 * a.Nout + na + e];
-        ash[e] = a.ap_p[3 * a.Nout + na + e];
-      }
-    }
-  }
   // Per thread the chunk column (cc, n) is fixed and the tile row advances by
   // RSTEP per iteration, so for every layer but the strided dgrads the global
   // element offset is one base plus a uniform stride: no per-row integer
@@ -998,18 +961,12 @@ __global__ __launch_bounds__(64 * WM * WN,
   const bool phased = DGRAD && a.stride == 2;
   const size_t off0 = (size_t)(m0 + row0) * a.Nout + (n_ok ? n : 0);
   const size_t ostep = (size_t)a.Nout;
-  // PMD_EPI_PF (dgrad): the first row group's global epilogue operands (addend, masks, BN
+  // Prefetch (dgrad): the first row group's global epilogue operands (addend, masks, BN
   // inputs) are issued before the C tile is staged through LDS, so their latency overlaps
-  // the staging instead of following it.  Full-step A/B (bench/ab_so.sh, 2 rounds, one lease):
-  // 0: 13,469 / 13,468 img/s, 1: 13,538 / 13,561, 2: 13,540 / 13,563 (+0.6%, profiles/epi_pf_r05.txt)
-#ifndef PMD_EPI_PF
-#define PMD_EPI_PF 2
-#endif
-  // (1: every dgrad; 2: not the 4-wave 128-column tiles with <= 1 BN set, which it would cost
-  // their 4th wave per SIMD -- 125 -> 144 VGPRs)
-  // (the BN-apply forward's residual tile likewise)
-  constexpr bool PF = (DGRAD && (PMD_EPI_PF == 1 || (PMD_EPI_PF == 2 && !(NW == 4 && BN == 128 && NB < 2)))) ||
-                      (CAN_APPLY && PMD_EPI_PF != 0);
+  // the staging instead of following it: +0.6% on the full step (profiles/epi_pf_r05.txt).
+  // Not for the 4-wave 128-column tiles with <= 1 BN set, which it would cost their 4th
+  // wave per SIMD (125 -> 144 VGPRs).
+  constexpr bool PF = DGRAD && !(NW == 4 && BN == 128 && NB < 2);
   uint4 pf_ad[PF ? G : 1], pf_yy[NBA][PF ? G : 1];
   uint32_t pf_am[PF ? G : 1], pf_mb[PF ? G : 1];
   if constexpr (PF) {
@@ -1030,7 +987,6 @@ __global__ __launch_bounds__(64 * WM * WN,
         pf_ad[g] = ld16n<NT_EPI_A>(a.addend + o);
         pf_am[g] = has_amask ? a.addend_mask[o >> 3] : 0xffu;
       }
-      if (ap_has_res && okg) pf_ad[g] = ld16n<NT_EPI_A>(a.ap_res + o);
       if (nbn && okg) {
         pf_mb[g] = a.bn_mask ? a.bn_mask[o >> 3] : 0xffu;
 #pragma unroll
@@ -1083,8 +1039,7 @@ __global__ __launch_bounds__(64 * WM * WN,
       for (int j = 0; j < NI; ++j) {
         const int row = wm * (BM / WM) + i * 16 + (lane & 15);
         const int colw = wn * (BN / WN) + j * 16 + (lane >> 4) * 4;   // logical channel (4 per lane)
-        const int col = EPI_X ? ((((colw >> 3) ^ (row & 15)) << 3) | ((colw & 4) ^ (((row >> 3) & 1) << 2)))
-                              : colw ^ (EPI_SW ? ((lane >> 1) & 4) : 0);
+        const int col = colw ^ (EPI_SW ? ((lane >> 1) & 4) : 0);
         const uint32_t lo = (uint32_t)f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16);
         const uint32_t hi = (uint32_t)f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16);
         *reinterpret_cast<uint2*>(Cs + row * LDC + col) = make_uint2(lo, hi);
@@ -1171,7 +1126,7 @@ __global__ __launch_bounds__(64 * WM * WN,
         off[g] = (((size_t)nb * a.OH + 2 * hh + ph) * a.OW + 2 * ww + pw) * a.Nout + (n_ok ? n : 0);
       }
       if (!ok[g]) off[g] = 0;
-      v[g] = *reinterpret_cast<const uint4*>(Cs + row * LDC + (EPI_X ? ((cc ^ (row & 15)) << 3) : cc * 8));
+      v[g] = *reinterpret_cast<const uint4*>(Cs + row * LDC + cc * 8);
       if constexpr (EPI_SW) {
         // rows with bit 3 set hold their 8-B halves swapped (compile-time under EPI_RM)
         const bool sw = EPI_RM ? ((it0 + g) & 1) != 0 : ((row >> 3) & 1) != 0;
@@ -1194,7 +1149,6 @@ __global__ __launch_bounds__(64 * WM * WN,
           for (int t = 0; t < NBA; ++t)
             if (t < nbn) yy[t][g] = a.bn_y[t] ? ld16n<NT_EPI_Y>(a.bn_y[t] + off[g]) : make_uint4(0, 0, 0, 0);
         }
-        if (ap_has_res && ok[g]) ad[g] = ld16n<NT_EPI_A>(a.ap_res + off[g]);
       }
     }
 #pragma unroll
@@ -1210,24 +1164,6 @@ __global__ __launch_bounds__(64 * WM * WN,
 #pragma unroll
         for (int e = 0; e < 8; ++e) f[e] += ga[e] + abias[e];
         o = pack8(f);
-      }
-      if constexpr (CAN_APPLY) {
-        if (apply) {
-          // bn_apply_kernel<1, relu> on the bf16-rounded tile value
-          float f[8], r[8];
-          unpack8(o, f);
-          if (ap_has_res) unpack8(ad[g], r);
-          uint32_t bits = 0;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            float t = f[e] * asc[e] + ash[e];
-            if (ap_has_res) t += r[e];
-            bits |= (uint32_t)(t > 0.f) << e;
-            f[e] = fmaxf(t, 0.f);
-          }
-          o = pack8(f);
-          if (a.ap_mask) a.ap_mask[off[g] >> 3] = (uint8_t)bits;
-        }
       }
       if (nbn) {
         // the output IS a BN site's dz; every consumer gates it with this same ReLU
@@ -1291,7 +1227,7 @@ __global__ __launch_bounds__(64 * WM * WN,
         float acc2 = 0.f;
         for (int r = col; r < NT; r += CPR) acc2 += part[r * PSTR + k];
         const int n = n0 + col * 8 + (k & 7);
-        if (n < a.Nout && !(PMD_TIMING_NO_ATOMICS & 2) && !(a.red_dot && k < 8))
+        if (n < a.Nout && !(PMD_TIMING_NO_ATOMICS & 2))
           atomicAdd(a.bn_red[t] + (stat_slot(blockIdx.y * tilesM + mt, a.nslots) * 2 + (k >> 3)) * a.Nout + n, acc2);
       }
       __syncthreads();
@@ -1580,10 +1516,6 @@ template <bool DGRAD, bool STATS>
 static void launch_choice(int c, const ConvArgs& a, hipStream_t st) {
   if ((c == 11 || c == 12) && halo_ok(a)) {
     launch_halo<DGRAD, STATS>(a, st, c == 12 ? 3 : 2);
-  } else if (c == 13 && a.Cs % 64 == 0) {
-    // 32x32x16 MFMA on the 128-row LDS-DMA tile (BK = 64, uniform-tap loader)
-    if (a.Nout <= 64) launch_k<128, 64, 64, 2, DGRAD, STATS, true, true>(a, st);
-    else launch_k<128, 128, 64, 2, DGRAD, STATS, true, true>(a, st);
   } else if (c == 10 && a.Nout > 64) {
     launch_k<64, 128, 32, 2, DGRAD, STATS, true>(a, st);
   } else if (c >= 6 && c <= 9 && p8_ok(c - 6, a)) {
@@ -1702,15 +1634,11 @@ static int tune(const ConvArgs& a0, hipStream_t st) {
   // (profiles/conv_p8_r02.txt): forced-policy only, not timed by the tuner
   // (10, the 64x128 tile, measured slower than 0..5 on every short-K dgrad --
   // profiles/dgrad_epi_r02_tile10.txt -- so it is a forced policy only)
-  static int tune_mf32 = -1;  // PMD_TUNE_MF32=1: also time the 32x32x16 MFMA tile (candidate 13)
-  if (tune_mf32 < 0) {
-    const char* e = getenv("PMD_TUNE_MF32");
-    tune_mf32 = (e && e[0] == '1') ? 1 : 0;
-  }
-  for (int c : {0, 1, 2, 3, 4, 5, 13}) {
+  // (the 32x32x16-MFMA 128-row tile measured slower than 0..5 on every ResNet-50 shape: not a
+  // candidate; PMD_CONV_IMPL=6 forces it)
+  for (int c : {0, 1, 2, 3, 4, 5}) {
     if ((c == 2 && !(big_ok(a) && a.Nout >= 256)) || (c == 3 && !big_ok(a)) || (c == 4 && a.Nout <= 64) ||
-        (c == 5 && (DGRAD || a.Cs < 64)) || (c == 10 && a.Nout <= 64) ||
-        (c == 13 && (!tune_mf32 || a.Cs % 64 != 0)))
+        (c == 5 && (DGRAD || a.Cs < 64)))
       continue;
     launch_choice<DGRAD, STATS>(c, a, st);  // warm (code object load, caches)
     float t = 1e30f;
@@ -1736,46 +1664,6 @@ static int tune(const ConvArgs& a0, hipStream_t st) {
   return best;
 }
 
-// PMD_CONV_REMAP="d2:4,f0:1,..." (A/B knob): run a tuned choice of the data-gradient (d) /
-// forward (f) passes as another candidate -- the tuner times a conv alone, the step runs it
-// next to the side stream (the co-residency question of profiles/wgrad_lds_r05.txt)
-static int conv_remap(bool dgrad, int c) {
-  static int map[2][16];
-  static const bool init = [] {
-    for (int p = 0; p < 2; ++p)
-      for (int i = 0; i < 16; ++i) map[p][i] = i;
-    const char* e = getenv("PMD_CONV_REMAP");
-    while (e && *e) {
-      const int p = *e == 'd' ? 1 : 0;
-      int from = -1, to = -1;
-      if (sscanf(e + 1, "%d:%d", &from, &to) == 2 && from >= 0 && from < 16 && to >= 0 && to < 16)
-        map[p][from] = to;
-      e = strchr(e, ',');
-      if (e) ++e;
-    }
-    return true;
-  }();
-  (void)init;
-  return (c >= 0 && c < 16) ? map[dgrad ? 1 : 0][c] : c;
-}
-
-static int conv_halo_pref(bool dgrad) {
-  static int pref[2] = {0, 0};
-  static const bool init = [] {
-    const char* e = getenv("PMD_CONV_HALO");
-    while (e && *e) {
-      int v = 0;
-      if ((e[0] == 'f' || e[0] == 'd') && e[1] == ':' && sscanf(e + 2, "%d", &v) == 1 && (v == 11 || v == 12))
-        pref[e[0] == 'd' ? 1 : 0] = v;
-      e = strchr(e, ',');
-      if (e) ++e;
-    }
-    return true;
-  }();
-  (void)init;
-  return pref[dgrad ? 1 : 0];
-}
-
 template <bool DGRAD, bool STATS>
 static void launch_sel(const ConvArgs& a, hipStream_t st) {
   if (conv_impl() == 5 && conv_tile() == 0 && autotune_on()) {
@@ -1784,17 +1672,8 @@ static void launch_sel(const ConvArgs& a, hipStream_t st) {
     int c = -1;
     {
       std::lock_guard<std::mutex> lk(g_tune_mu);
-      if (!DGRAD && !STATS && a.ap_p) {
-        // BN-apply pass: the tile of the same shape's statistics pass (its tuning-table entry)
-        TuneKey ks = k;
-        ks.v[12] = 1;
-        auto it = g_tune.find(ks);
-        if (it != g_tune.end()) c = it->second;
-      }
-      if (c < 0) {
-        auto it = g_tune.find(k);
-        if (it != g_tune.end()) c = it->second;
-      }
+      auto it = g_tune.find(k);
+      if (it != g_tune.end()) c = it->second;
     }
     if (c < 0) {
       hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -1808,11 +1687,6 @@ static void launch_sel(const ConvArgs& a, hipStream_t st) {
       }
     }
     if (c >= 0) {
-      c = conv_remap(DGRAD, c);
-      // PMD_CONV_HALO="f:12,d:11" (A/B knob): the halo-image 3x3 kernel (candidate 11: 2-deep,
-      // 12: 3-deep weight ring) for every halo-eligible stride-1 3x3 forward (f) / dgrad (d)
-      const int hp = conv_halo_pref(DGRAD);
-      if (hp && halo_ok(a)) c = hp;
       launch_choice<DGRAD, STATS>(c, a, st);
       return;
     }
@@ -1841,17 +1715,6 @@ static void launch_sel(const ConvArgs& a, hipStream_t st) {
 // (conv_dgrad in bind.cpp sets it around one launch; the linear-BN backward's constant term)
 static thread_local const float* g_addend_bias = nullptr;
 void conv_set_addend_bias(const float* b) { g_addend_bias = b; }
-// BN-apply epilogue / dot-only reduce of the NEXT launch on this thread (see ConvArgs)
-static thread_local const float* g_ap_p = nullptr;
-static thread_local const bf16_t* g_ap_res = nullptr;
-static thread_local uint8_t* g_ap_mask = nullptr;
-static thread_local int g_red_dot = 0;
-void conv_set_fwd_apply(const float* p, const bf16_t* res, uint8_t* mask) {
-  g_ap_p = p;
-  g_ap_res = p ? res : nullptr;
-  g_ap_mask = p ? mask : nullptr;
-}
-void conv_set_red_dot(int on) { g_red_dot = on; }
 
 // deterministic mode: an upper bound of the launch's row-tile count over every tile choice
 // (BM >= 64; stride-2 dgrads run 4 phase grids of Mgrid rows; HALO tiles never straddle images)
@@ -1871,18 +1734,7 @@ static int conv_igemm_launch_b(const bf16_t* src, const bf16_t* wt, bf16_t* out,
   if (stride != 1 && stride != 2) return 3;
   if (batch < 1 || batch > 65535 || (batch > 1 && (dgrad || stats || addend || bnr))) return 6;
   ConvArgs a{};
-  // thread-local epilogue extras of this one launch (conv_set_fwd_apply / conv_set_red_dot)
-  if (g_ap_p) {
-    if (dgrad || stats || batch > 1) return 7;   // the apply epilogue is a plain-forward mode
-    a.ap_p = g_ap_p;
-    a.ap_res = g_ap_res;
-    a.ap_mask = g_ap_mask;
-  }
-  if (g_red_dot) {
-    if (!dgrad || !bnr || bnr->red[1] || !bnr->y[0] || bnr->mask || addend) return 8;
-    a.red_dot = 1;
-  }
-  if (!out && !(stats || (bnr && a.red_dot))) return 9;   // no store only for stats / dot passes
+  if (!out && !stats) return 9;   // no store only for a statistics-only pass
   a.batch = batch;
   a.bs_src = bs_src;
   a.bs_wt = bs_wt;

@@ -944,19 +944,7 @@ static void plan(const WgradArgs& a, const WgradCfg& cfg, int* splits_out, int* 
   // keep the partial workspace bounded (<= 96 MiB)
   const long long per = (long long)a.K * a.Kg * 4;
   while (splits > 1 && per * splits > (96ll << 20)) --splits;
-  // PMD_WGRAD_SLAB_FRAC=f (A/B knob, 0 = off): the split partials (written, then read back by
-  // the reduction: 2 x splits x K x Kg x 4 bytes) may cost at most f x the operand bytes
-  // M x (K + C) x 2 -- fewer, longer splits for the deep layers whose partial traffic
-  // rivals their operands (l3/l4: K x Kg up to 2.4M elements at M = 12,544-50,176)
-  static const double slab_frac = [] {
-    const char* e = getenv("PMD_WGRAD_SLAB_FRAC");
-    return e ? atof(e) : 0.0;
-  }();
-  if (slab_frac > 0.0) {
-    const double op = (double)a.M * (a.K + a.C) * 2.0;
-    const int cap = (int)(slab_frac * op / (2.0 * (double)per));
-    if (splits > (cap < 1 ? 1 : cap)) splits = cap < 1 ? 1 : cap;
-  }
+  // (a bytes-aware cap on the split count measured -2% to -36%: profiles/cu_mask_wgrad_blocks_r05.txt)
   if (splits < 1) splits = 1;
   const int cps = (chunks + splits - 1) / splits;
   *cps_out = cps;
@@ -1339,19 +1327,9 @@ int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, float* ws, i
     // conv block (>= 34 KB) -- nor, with its VGPRs, a 5-us statistics collapse -- fits next to it
     // until it retires.  Tuned 256x256 choices therefore run as the 128x128 tile (64 KB):
     // +0.4% step (13,506 / 13,540 vs 13,460 / 13,467 img/s, profiles/wgrad_lds_r05.txt).
-    // PMD_WGRAD_MAP4 / _MAP5 / _MAP6 = impl: the variant a tuned 256x256 / 256x128 (96 KB) /
-    // halo (152 KB) choice runs as (defaults 1 / none / none; 0 = as tuned; the other two
-    // measured slower).  A forced variant (PMD_WGRAD_IMPL, conv_wgrad_set_impl) is never remapped.
-    // PMD_WGRAD_MAP0 / _MAP1 likewise for the register-staged / 64-row DMA choices (7 = the
-    // 48 KB 32-row x3 DMA variant, A/B).
-    static const int remap[8] = {[] { const char* e = getenv("PMD_WGRAD_MAP0"); return e ? atoi(e) : 0; }(),
-                                 [] { const char* e = getenv("PMD_WGRAD_MAP1"); return e ? atoi(e) : 0; }(),
-                                 0, 0,
-                                 [] { const char* e = getenv("PMD_WGRAD_MAP4"); return e ? atoi(e) : 1; }(),
-                                 [] { const char* e = getenv("PMD_WGRAD_MAP5"); return e ? atoi(e) : 0; }(),
-                                 [] { const char* e = getenv("PMD_WGRAD_MAP6"); return e ? atoi(e) : 0; }(),
-                                 0};
-    if (impl >= 0 && impl < 8 && remap[impl] > 0 && wgrad_cfg_ok(remap[impl], a)) impl = remap[impl];
+    // (the 256x128 / halo tiles as 128x128 measured slower, so they keep their tuned choice;
+    // a forced variant -- PMD_WGRAD_IMPL, conv_wgrad_set_impl -- is never remapped)
+    if (impl == 4 && wgrad_cfg_ok(1, a)) impl = 1;
   }
   wgrad_run(impl, a, ws, st);
   return 0;

@@ -55,10 +55,6 @@ int colsum_launch(const bf16_t* x, float* out, long long M, int C, hipStream_t s
 int bnlin_wgrad_launch(float* out, const float* abc, const float* T, const bf16_t* wk, const float* gz,
                        const float* cs, int K, int C, int Cp, hipStream_t st);
 void conv_set_addend_bias(const float* b);  // fp32 [Nout] bias of the next dgrad's addend (this thread)
-// next plain forward on this thread: BN-apply epilogue out = relu(y * p[2] + p[3] [+ res]) + ReLU
-// bitmask (p null: off); next dgrad: dot-only fused reduce (see ConvArgs::red_dot)
-void conv_set_fwd_apply(const float* p, const bf16_t* res, uint8_t* mask);
-void conv_set_red_dot(int on);
 void conv_set_impl(int impl);
 void conv_wgrad_set_impl(int impl);
 void conv_set_tile(int t);

@@ -94,22 +94,10 @@ class WeightImageSet:
                                  [cp for _, cp, _ in self.entries], [wt for _, _, wt in self.entries])
 
     def refresh(self, need_bwd=True):
-        """Forward images now, on the current stream; dgrad images (only needed
-        by the backward, milliseconds later) on the wgrad side stream, which is
-        idle during the forward -- the backward waits for them before its first
-        dgrad (:func:`_wait_weight_images`)."""
-        if not need_bwd:
-            self._c.refresh(1)
-        elif _SPLIT_WPREP and _WGRAD_STREAM["on"] and self._dev.type == "cuda":
-            self._c.refresh(1)
-            main = torch.cuda.current_stream(self._dev)
-            side = _wgrad_stream(self._dev)
-            _stream_wait(side, main)             # after the previous step's optimizer update
-            with torch.cuda.stream(side):
-                self._c.refresh(2)
-            _state["wkt_event"] = _record_on(side)
-        else:
-            self._c.refresh(3)
+        """Forward images (and, when a backward follows, the dgrad images) in ONE launch on the
+        current stream.  (The dgrad images on the idle side stream during the forward measured
+        step-neutral, 12,699 / 12,684 vs 12,704 / 12,712 img/s in round 4.)"""
+        self._c.refresh(3 if need_bwd else 1)
         if self.fp8 is not None:
             self.fp8.refresh()
 
@@ -331,9 +319,6 @@ def _wgrad(P, dy, x, wpack, stride, pad, w, xq=None):
 _WS_GROUP = os.environ.get("PMD_WS_GROUP", "1") != "0"
 _WGRAD_STREAM = {"on": os.environ.get("PMD_WGRAD_STREAM", "1") != "0", "streams": {},
                  "defer": int(os.environ.get("PMD_WGRAD_DEFER", "1") or 0)}  # join lag in blocks
-# dgrad weight images refreshed on the side stream during the forward: PMD_SPLIT_WPREP=1
-# (measured step-neutral, 12,699 / 12,684 vs 12,704 / 12,712 img/s: off by default)
-_SPLIT_WPREP = os.environ.get("PMD_SPLIT_WPREP", "0") == "1"
 
 
 # Priority of the step's own HIP streams (default high, -1; PMD_STREAM_PRIO=0: normal).
@@ -424,14 +409,6 @@ def _wgrad_stream(dev):
     return st
 
 
-def _wait_weight_images():
-    """Backward: the current stream waits (once per step) for the dgrad weight
-    images the forward queued on the side stream."""
-    ev = _state.pop("wkt_event", None)
-    if ev is not None:
-        _wait_on(torch.cuda.current_stream(), ev)
-
-
 _STEP_STREAMS: dict = {}
 
 
@@ -443,22 +420,6 @@ def _new_stream(dev, prio=None, cu_mask=None):
     from .native import C
     return torch.cuda.ExternalStream(C.create_stream(dev.index, STREAM_PRIO if prio is None else prio,
                                                      list(cu_mask or [])), device=dev)
-
-
-def _side_cu_mask(dev):
-    """PMD_WGRAD_CUS=N (< the CU count): the weight-gradient stream runs on N CUs only --
-    CU i enabled iff i % 32 < N * 32 / n_cu (an even share of every 32-CU group) -- so the
-    main stream's latency-bound kernels always find free CUs.  Empty list: all CUs."""
-    n = int(os.environ.get("PMD_WGRAD_CUS", "0") or 0)
-    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    if n <= 0 or n >= ncu:
-        return []
-    keep = max(1, round(32 * n / ncu))
-    words = [0] * ((ncu + 31) // 32)
-    for i in range(ncu):
-        if i % 32 < keep:
-            words[i // 32] |= 1 << (i % 32)
-    return words
 
 
 def init_step_streams(dev):
@@ -473,7 +434,7 @@ def init_step_streams(dev):
     main = _new_stream(dev)
     main.wait_stream(torch.cuda.current_stream(dev))
     torch.cuda.set_stream(main)
-    side = _new_stream(dev, int(os.environ.get("PMD_WGRAD_PRIO", STREAM_PRIO)), _side_cu_mask(dev))
+    side = _new_stream(dev)
     _WGRAD_STREAM["streams"][dev] = side
     comm = _new_stream(dev)
     _STEP_STREAMS[dev] = {"main": main, "wgrad": side, "comm": comm}
@@ -683,32 +644,6 @@ def _bnlin_eligible(conv_m, yf, x, training, fuse, shortcut, f8):
     if ks != (1, 1) or st != (1, 1):
         return False
     return _BNLIN == "all" or yf.numel() >= _BNLIN_MIN
-
-
-# BN fold (training forward of the identity blocks whose final BN takes the linear-BN backward):
-# conv3 runs twice -- statistics only (no output), then again with the BN-apply epilogue
-# (+ identity, ReLU, mask) -- so the conv3 output y is never written nor read back; the
-# backward recomputes the y part of sum dz * xhat from z (_bnfold_dot).  Opt-in (PMD_BNFOLD=1):
-# it removes 0.8 GB per l1 site but measured at parity (profiles/bnfold_r05.txt) -- the short-
-# reduction conv3 is latency-bound (79 us without its store vs 88 with it at l1), so the second
-# GEMM pass costs what the y round trip saved.
-_BNFOLD = os.environ.get("PMD_BNFOLD", "0") == "1"
-
-
-class _YShape:
-    """Shape / device stand-in of a BN input that is never materialised (BN fold)."""
-    __slots__ = ("shape", "device", "dtype")
-
-    def __init__(self, shape, device, dtype):
-        self.shape = torch.Size(shape)
-        self.device = device
-        self.dtype = dtype
-
-    def numel(self):
-        n = 1
-        for d in self.shape:
-            n *= d
-        return n
 
 
 # a BN site whose reduce a dgrad epilogue fused receives dz already gated by its ReLU mask:
@@ -923,7 +858,6 @@ class _ConvFn(torch.autograd.Function):
     def backward(ctx, dy, _dstats):
         if dy is None:
             return None, None, None, None, None
-        _wait_weight_images()
         x, *wpack = ctx.saved_tensors
         stride, pad, w = ctx.conf
         P = prims_for(x)
@@ -1185,15 +1119,6 @@ def _bnlin_final(P, dz, pre, training, sync, count, z, wpack, conv_m, bn, p, rec
     return dx, state["pre"], g
 
 
-def _bnfold_dot(P, z, wpack, dz, p, pre, sync):
-    """BN fold, backward: the dgrad that produced ``dz`` took the sum-only reduce of the final BN
-    (its input y was never stored); add ``invstd * sum dz * y`` with y = z W^T recomputed into the
-    same slots (before their collapse / SyncBN exchange), and move the reduce's ready event."""
-    P.conv_bn_dot_(z, wpack, dz, p, pre[0])
-    if getattr(pre, "event", None) is not None:
-        pre.event = _after_dgrad_event(dz, sync)
-
-
 # ------------------------------------------------------------ residual block
 class _BnSite:
     """Hand-off between two consecutive residual blocks for the fused BN reduce:
@@ -1292,17 +1217,7 @@ class _ResidualBlockFn(torch.autograd.Function):
         wpf = _conv_weight(P, fconv, x.dtype, h.shape[-1], True)
         hq_f = used_q(fconv, hq, h)
         fuse = _state["fuse_bnred"] and training
-        # BN fold: the final conv's output is never written (see _BNFOLD)
-        fold = (_BNFOLD and shortcut is None and h.shape[-1] == wpf[0].shape[-1]
-                and _bnlin_eligible(fconv, _YShape((*h.shape[:-1], wpf[0].shape[0]), h.device, h.dtype),
-                                    x, training, fuse, shortcut, f8))
-        if fold:
-            yf = None
-            stf = P.conv_fwd_stats(h, wpf, fconv.stride, fconv.padding, _stats_req(fbn, training))
-            yproxy = _YShape((*h.shape[:-1], wpf[0].shape[0]), h.device, h.dtype)
-        else:
-            yf, stf = _conv_fwd_any(P, f8, h, hq_f, wpf, fconv, _stats_req(fbn, training))
-            yproxy = yf
+        yf, stf = _conv_fwd_any(P, f8, h, hq_f, wpf, fconv, _stats_req(fbn, training))
         qins.append(hq_f if f8w else None)
         # e4m3 copy of the block output only if its consumer -- the next block's first
         # conv, which has this block's first-conv kernel shape -- runs in fp8
@@ -1316,10 +1231,6 @@ class _ResidualBlockFn(torch.autograd.Function):
             qins.append(xq_s if f8w else None)
             pf, ps, countf = _bn_forward_params(P, yf, stf, fbn, training, sync, ys, sts, sbn)
             r = P.bn_apply(yf, pf, None, ys, ps, relu=True, **({"fp8": osite} if osite else {}))
-        elif fold:
-            wps = None
-            pf, _, countf = _bn_forward_params(P, yproxy, stf, fbn, training, sync)
-            r = P.conv_fwd_apply(h, wpf, fconv.stride, fconv.padding, pf, x)
         else:
             wps = None
             pf, _, countf = _bn_forward_params(P, yf, stf, fbn, training, sync)
@@ -1343,8 +1254,8 @@ class _ResidualBlockFn(torch.autograd.Function):
         ctx.in_site = getattr(x, "_pmd_bnsite", None) if fuse else None
         ctx.out_site = None
         # linear-BN backward of the final BN (no elementwise pass, see _bnlin_final)
-        ctx.bnlin = fold or (_bnlin_eligible(fconv, yf, x, training, fuse, shortcut, f8)
-                             and h.shape[-1] == wpf[0].shape[-1])
+        ctx.bnlin = (_bnlin_eligible(fconv, yf, x, training, fuse, shortcut, f8)
+                     and h.shape[-1] == wpf[0].shape[-1])
         ctx.bnlin_prep = _bnlin_prep(P, fbn, pf, wpf, h) if ctx.bnlin else None
         if fuse:
             ctx.out_site = _BnSite(omask, [(yf, pf)] + ([(ys, ps)] if shortcut is not None else []))
@@ -1360,7 +1271,6 @@ class _ResidualBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        _wait_weight_images()
         cfg, sync, counts, countf, nwf, nws, nwst = ctx.cfg
         stages, final, shortcut, training = cfg
         nst = len(stages)
@@ -1411,14 +1321,6 @@ class _ResidualBlockFn(torch.autograd.Function):
             return sc, am, only
         # reduce of the final BN(s), if the next block's dgrad already produced it
         pre = ctx.out_site.take(dout, P) if ctx.out_site is not None else None
-        if yf is None:
-            # BN fold: the final conv's output was never written
-            if pre is not None and ctx.bnlin:
-                # the next block's dgrad took the sum-only reduce; add the y part from z
-                _bnfold_dot(P, hlast, wpf, dout, pf, pre, sync if training else None)
-            else:
-                # no fused reduce reached this block (e.g. the network's last block): recompute y
-                yf = P.conv_fwd(hlast, wpf, fconv.stride, fconv.padding, False)[0]
         # --- final BN (+ projection BN) and the residual ReLU
         if shortcut is not None:
             sconv, sbn = shortcut

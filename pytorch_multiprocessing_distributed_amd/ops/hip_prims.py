@@ -74,24 +74,6 @@ def conv_fwd(x, wpack, stride, pad, want_stats):
     return _C.conv_fwd(x, wpack[0], int(stride), int(pad), False, None)[0], None
 
 
-def conv_fwd_stats(x, wpack, stride, pad, want_stats):
-    """Statistics slots of conv(x) without writing it (torch_prims.conv_fwd_stats)."""
-    _, shift = _TP.stats_request(want_stats)
-    buf = _acquire(wpack[0].shape[0], x.device)
-    return _C.conv_fwd_stats(x, wpack[0], int(stride), int(pad), buf, shift)
-
-
-def conv_fwd_apply(x, wpack, stride, pad, p, res=None):
-    """relu(BN(conv(x)) [+ res]) in the conv epilogue -> (out, ReLU bitmask)."""
-    r = _C.conv_fwd_apply(x, wpack[0], int(stride), int(pad), p, res)
-    return r[0], r[1]
-
-
-def conv_bn_dot_(z, wpack, dz, p, red):
-    """Slots ``red`` row 1 += invstd * sum dz * (z W^T), the 1x1 GEMM recomputed, nothing stored."""
-    _C.conv_bn_dot(z, wpack[0], dz, p, red)
-
-
 def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None, bnred=None, addend_mask=None, addend_bias=None):
     """dX (+ addend [* relu bitmask addend_mask]).  ``bnred = (mask, [(y, params)] or
     [(y1, p1), (y2, p2)])`` fuses the BN-backward reduce of dX into the epilogue

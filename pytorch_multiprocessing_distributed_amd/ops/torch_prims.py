@@ -59,28 +59,6 @@ def conv_fwd(x, wpack, stride, pad, want_stats):
     return y, stats
 
 
-def conv_fwd_stats(x, wpack, stride, pad, want_stats):
-    """The BN statistics of conv(x) alone (``conv_fwd``'s, about the same shift); the output
-    is never written -- :func:`conv_fwd_apply` recomputes it (ops/functional.py _bnfold)."""
-    return conv_fwd(x, wpack, stride, pad, want_stats if torch.is_tensor(want_stats) else True)[1]
-
-
-def conv_fwd_apply(x, wpack, stride, pad, p, res=None):
-    """``bn_apply(conv(x), p, res, relu=True)`` with the conv output rounded to the activation
-    dtype first, as the gfx950 epilogue stages its tile -> (out, ReLU mask)."""
-    y, _ = conv_fwd(x, wpack, stride, pad, False)
-    return bn_apply(y, p, res, relu=True)
-
-
-def conv_bn_dot_(z, wpack, dz, p, red):
-    """``red[1] += invstd * sum dz * y`` per channel with y = conv1x1(z) recomputed (rounded like
-    the kernel's tile): completes the sum-only reduce of a BN whose input was never stored."""
-    y, _ = conv_fwd(z, wpack, 1, 0, False)
-    c = dz.shape[-1]
-    d = (_f(dz).reshape(-1, c) * _f(y).reshape(-1, c)).sum(0)
-    red[1].add_((_f(p[1]) * d).to(red.dtype))
-
-
 def conv_dgrad(dy, wpack, x_shape, stride, pad, addend=None, bnred=None, addend_mask=None, addend_bias=None):
     """dX (+ addend).  With ``bnred = (mask, [(y, params), ...])`` also returns
     the BN-backward reduce of the result for each set (the fused form of

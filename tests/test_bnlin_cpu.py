@@ -24,12 +24,8 @@ def _copy_into_stock(fused, stock):
             sd[k].copy_(v)
 
 
-@pytest.mark.parametrize("fold", [True, False])
 @pytest.mark.parametrize("arena", [False, True])
-def test_bnlin_matches_stock_resnet50(bnlin_all, arena, fold, monkeypatch):
-    # fold: the final conv3 output y never exists (statistics-only conv3, then conv3 with the
-    # BN-apply epilogue; backward: sum-only fused reduce + the recomputed y part, _bnfold_dot)
-    monkeypatch.setattr(OF, "_BNFOLD", fold)
+def test_bnlin_matches_stock_resnet50(bnlin_all, arena):
     torch.manual_seed(0)
     f = build_model("resnet50", num_classes=10, stem="imagenet").double()
     s = build_model("resnet50", num_classes=10, stem="imagenet", impl="stock").double()
@@ -79,48 +75,3 @@ def test_bnlin_off_by_default_below_threshold():
     assert not OF._bnlin_eligible(conv, big, None, False, True, None, None)      # eval
     assert not OF._bnlin_eligible(conv, big, None, True, True, ("proj",), None)  # projection block
     assert not OF._bnlin_eligible(torch.nn.Conv2d(64, 256, 3, padding=1), big, None, True, True, None, None)
-
-
-def test_bnfold_path_is_taken(bnlin_all, monkeypatch):
-    """With the fold on, every identity block's final conv runs as statistics-only + BN-apply
-    epilogue passes (12 in ResNet-50); 11 of them complete their reduce from z (the 12th, the
-    last block, has no fused producer and recomputes y)."""
-    from pytorch_multiprocessing_distributed_amd.ops import torch_prims as TP
-    counts = {"apply": 0, "dot": 0, "stats": 0}
-    for name in ("conv_fwd_apply", "conv_bn_dot_", "conv_fwd_stats"):
-        orig = getattr(TP, name)
-
-        def spy(*a, _o=orig, _n=name, **k):
-            counts[{"conv_fwd_apply": "apply", "conv_bn_dot_": "dot", "conv_fwd_stats": "stats"}[_n]] += 1
-            return _o(*a, **k)
-        monkeypatch.setattr(TP, name, spy)
-    monkeypatch.setattr(OF, "_BNFOLD", True)
-    torch.manual_seed(0)
-    f = build_model("resnet50", num_classes=10, stem="imagenet").double()
-    x = torch.randn(2, 64, 64, 3, dtype=torch.float64)
-    OF.cross_entropy(f(x), torch.tensor([1, 2])).backward()
-    assert counts == {"apply": 12, "dot": 11, "stats": 12}
-
-
-def test_bnfold_prims_match_unfused():
-    """conv_fwd_apply == bn_apply(conv_fwd), conv_fwd_stats == conv_fwd's statistics, and the
-    sum-only reduce + conv_bn_dot_ == the full reduce (fp64, torch prims)."""
-    from pytorch_multiprocessing_distributed_amd.ops import torch_prims as TP
-    torch.manual_seed(1)
-    z = torch.randn(2, 5, 6, 16, dtype=torch.float64).relu()
-    wk = (TP.conv_weight(torch.randn(32, 16, 1, 1, dtype=torch.float64), torch.float64, 16)[0],)
-    res = torch.randn(2, 5, 6, 32, dtype=torch.float64)
-    shift = torch.randn(32, dtype=torch.float64)
-    y, st = TP.conv_fwd(z, wk, 1, 0, shift)
-    torch.testing.assert_close(TP.conv_fwd_stats(z, wk, 1, 0, shift), st)
-    p = TP.stats_finalize_local(st.clone(), y.numel() // 32, torch.rand(32, dtype=torch.float64) + 0.5,
-                                torch.randn(32, dtype=torch.float64), 1e-5, shift=shift.clone())
-    o1, m1 = TP.bn_apply(y, p, res)
-    o2, m2 = TP.conv_fwd_apply(z, wk, 1, 0, p, res)
-    torch.testing.assert_close(o2, o1)
-    assert torch.equal(m1, m2)
-    dz = torch.randn_like(y)
-    full = TP.bn_bwd_reduce(dz, None, y, p, False)
-    part = TP.bn_bwd_reduce(dz, None, None, p, False)
-    TP.conv_bn_dot_(z, wk, dz, p, part)
-    torch.testing.assert_close(part, full, rtol=1e-10, atol=1e-10)

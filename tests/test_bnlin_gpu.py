@@ -104,11 +104,10 @@ def test_resnet50_train_step_linear_bn_vs_fp32_oracle(monkeypatch, arena):
     m0 = build_model("resnet50", num_classes=1000, stem="imagenet").to(DEV)
     x, y = C.synth_images(32, 112, 112, 8, 3, 1000, 7, 0)
     m0.train()
-    ms = {k: copy.deepcopy(m0) for k in ("lin", "fold", "elt", "f32")}
+    ms = {k: copy.deepcopy(m0) for k in ("lin", "elt", "f32")}
     grads, loss = {}, {}
     for k, m in ms.items():
-        monkeypatch.setattr(OF, "_BNLIN", "all" if k in ("lin", "fold") else "0")
-        monkeypatch.setattr(OF, "_BNFOLD", k == "fold")
+        monkeypatch.setattr(OF, "_BNLIN", "all" if k == "lin" else "0")
         mm = DataParallel(m, None) if arena else m
         OF.force_torch_prims(k == "f32")
         try:
@@ -124,9 +123,7 @@ def test_resnet50_train_step_linear_bn_vs_fp32_oracle(monkeypatch, arena):
     def q(v, f):
         v = sorted(v)
         return v[min(int(len(v) * f), len(v) - 1)]
-    # "fold": the final conv3 output never written (statistics-only conv3 + BN-apply epilogue,
-    # sum-only fused reduce + conv_bn_dot in the backward)
-    for k in ("lin", "fold"):
+    for k in ("lin",):
         assert abs(loss[k] - loss["f32"]) / loss["f32"] < 1e-2, (k, loss)
         el = {n: _rel(g, grads["f32"][n]) for n, g in grads[k].items()}
         for f in (0.5, 0.9):
@@ -139,41 +136,3 @@ def test_resnet50_train_step_linear_bn_vs_fp32_oracle(monkeypatch, arena):
             if b1.dtype.is_floating_point and n.endswith("running_mean"):
                 # means near zero: bounded by the elementwise path's own error
                 assert _rel(b1, b2) < 1.5 * _rel(b3, b2) + 1e-3, (k, n, _rel(b1, b2), _rel(b3, b2))
-
-
-@pytest.mark.parametrize("C,K,res", [(64, 256, True), (128, 512, True), (512, 2048, False)])
-def test_bnfold_prims_match_unfused(C, K, res):
-    """BN fold prims: the statistics-only forward == conv_fwd's statistics, the BN-apply epilogue
-    == bn_apply(conv_fwd) (output and ReLU bitmask), and conv_bn_dot's recomputed y part ==
-    invstd * sum dz * y of the stored y, each also against the fp32 torch twin."""
-    HP, TP = _hp(), _tp()
-    torch.manual_seed(C + K)
-    N, H = 8, 14
-    z = torch.randn(N, H, H, C, device=DEV).relu().to(torch.bfloat16)
-    wk = (torch.randn(K, 1, 1, C, device=DEV) / C ** 0.5).to(torch.bfloat16)
-    shift = torch.randn(K, device=DEV) * 0.1
-    y, st = HP.conv_fwd(z, (wk,), 1, 0, shift)
-    st2 = HP.conv_fwd_stats(z, (wk,), 1, 0, shift)
-    s1, s2 = st.sum(0), st2.sum(0)
-    torch.testing.assert_close(s2, s1, rtol=1e-5, atol=1e-3)
-    _, st_r = TP.conv_fwd(z.float(), (wk.float(),), 1, 0, shift)
-    torch.testing.assert_close(s2, st_r, rtol=1e-3, atol=1e-1)
-    gamma, beta = torch.rand(K, device=DEV) + 0.5, torch.randn(K, device=DEV)
-    p = HP.stats_finalize_local(st2, N * H * H, gamma, beta, 1e-5)   # clears + recycles st2
-    r = torch.randn(N, H, H, K, device=DEV).to(torch.bfloat16) if res else None
-    o1, m1 = HP.bn_apply(y, p, r)
-    o2, m2 = HP.conv_fwd_apply(z, (wk,), 1, 0, p, r)
-    torch.testing.assert_close(o2.float(), o1.float(), rtol=1e-2, atol=1e-2)
-    o_r, _ = TP.bn_apply(y.float(), p, None if r is None else r.float())
-    torch.testing.assert_close(o2.float(), o_r, rtol=2e-2, atol=2e-2)
-    # masks: the bit of every element whose bn_apply output is clearly nonzero agrees
-    diff = (m1 ^ m2)
-    assert int(diff.ne(0).sum()) <= max(1, m1.numel() // 1000), int(diff.ne(0).sum())
-    # dot-only reduce
-    dz = torch.randn(N, H, H, K, device=DEV).to(torch.bfloat16)
-    buf = torch.zeros(64, 2, K, device=DEV)
-    HP.conv_bn_dot_(z, (wk,), dz, p, buf)
-    got = buf.sum(0)
-    want = p[1] * (dz.float() * y.float()).reshape(-1, K).sum(0)
-    assert float(got[0].abs().max()) == 0.0          # the sum row is untouched
-    torch.testing.assert_close(got[1], want, rtol=1e-3, atol=1e-2 * float(want.abs().max()))

@@ -225,3 +225,22 @@ def test_two_ranks_resnet50_linear_bn_match_single_process(tmp_path, monkeypatch
     own = abs(loss["hip"] - loss["f32"])
     assert abs(got["loss"] - loss["f32"]) <= 3.0 * own + 1e-2 * loss["f32"], (got["loss"], loss)
     assert not bad, bad
+
+
+def test_eight_ranks_on_one_gpu_match_single_process_per_tensor(tmp_path):
+    """the W=8 path rehearsed on the one GPU -- 8 ranks x batch 8 of
+    ResNet-18-ref through the production W>1 path (SyncBN over the xGMI kernel with 8-rank
+    slot / flag tables at the stress-selected ordering, native reducer, rank-0 broadcast of
+    7 differently initialised replicas) == one process on the global batch 64, per gradient
+    tensor and running statistic, at the same bound as the 2-rank case."""
+    import test_model_oracle_gpu as oracle
+    out = str(tmp_path / "r0.pt")
+    mp.spawn(_worker, args=(8, _free_port(), out, "xgmi", "none"), nprocs=8, join=True)
+    got = torch.load(out, weights_only=True)
+    ms, loss, grads = oracle._runs(train=True, model="res")
+    bad, e1, e2 = _oracle_violations(got, ms, loss, grads)
+    worst = sorted(((e2[n] / max(e1[n], 1e-6), n) for n in e2), reverse=True)[:5]
+    print(f"[8 ranks] buckets {got['nbuckets']}, worst e2/e1: "
+          + ", ".join(f"{n} {r:.2f}" for r, n in worst))
+    assert not bad, bad
+

@@ -73,6 +73,10 @@ def _defer_worker(rank, world, port, out, defer):
     OF._WGRAD_STREAM["on"] = True
     OF._WGRAD_STREAM["defer"] = defer
     OF.set_deterministic(True)          # bit-exact oracle (kernels/det.hip)
+    # the runs are separate processes: pin the kernel choices (no per-process timing, whose
+    # noise could pick another split-K plan and so another summation order)
+    os.environ["PMD_CONV_AUTOTUNE"] = "0"
+    os.environ["PMD_WGRAD_AUTOTUNE"] = "0"
     comm = get_comm()
     comm.enable_xgmi(timeout_s=20.0)
     OF.set_bn_sync(comm)

@@ -105,7 +105,9 @@ def test_auto_transport_selection(monkeypatch, bn_sync_guard, capsys):
     m = build_model("resnet50", num_classes=10, stem="imagenet")
     made = []
 
-    def create(group=None, priority=0, store=None, stream=0):
+    def create(group=None, priority=0, store=None, stream=0, stream_spec=None):
+        if stream_spec is not None:
+            priority, stream = stream_spec()     # resolved inside create
         c = _Native()
         made.append(c)
         return c

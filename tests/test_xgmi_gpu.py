@@ -213,3 +213,51 @@ def test_xgmi_interleaved_plain_and_fused_calls_with_skewed_rank(tmp_path):
         for delay in (5e-05, 0.0):
             assert got[f"{name}_{delay}"] is True, (name, delay, got[f"{name}_{delay}_detail"])
     assert got["selected"] == "light"
+
+
+def _eight_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import time
+    import torch.distributed as dist
+    from pytorch_multiprocessing_distributed_amd.parallel.xgmi import XgmiAllReduce
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t0 = time.time()
+    xg = XgmiAllReduce(timeout_s=30.0)
+    t_open = time.time() - t0
+    t0 = time.time()
+    chosen = xg.select_ordering(verbose=False)      # 240 interleaved calls, rank 7 skewed
+    t_select = time.time() - t0
+    stress = dict(getattr(xg, "last_stress", {}))
+    # exact sums of integer-valued vectors at sizes spanning 1..64 blocks, back to back
+    ok = True
+    for it in range(3):
+        for n in SIZES:
+            base = torch.arange(n, device="cuda", dtype=torch.float32).remainder_(101)
+            x = base + 1000.0 * rank + it
+            xg.all_reduce_(x)
+            want = base * world + 1000.0 * (world * (world - 1) / 2) + it * world
+            ok = ok and bool(torch.equal(x, want))
+    torch.cuda.synchronize()
+    xg.check()
+    res = {"chosen": chosen, "ok": ok, "stress": str(stress), "t_open": t_open, "t_select": t_select}
+    if rank == 0:
+        torch.save(res, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_xgmi_eight_ranks_one_gpu(tmp_path):
+    """the 8-rank slot / flag tables (kXgmiMaxRanks) and the 8-way skew
+    behaviour run as 8 processes sharing the one GPU through HIP IPC: the full
+    select_ordering stress (240 interleaved plain / fused-BN calls, rank 7 skewed, exact) and
+    exact integer sums at every block count; prints the startup cost of the self-test."""
+    out = str(tmp_path / "x8.pt")
+    mp.spawn(_eight_worker, args=(8, _free_port(), out), nprocs=8, join=True)
+    got = torch.load(out, weights_only=True)
+    print(f"xGMI 8 ranks on 1 GPU: ordering {got['chosen']}, IPC setup {got['t_open']:.2f} s, "
+          f"select_ordering (self-test + 240-call stress) {got['t_select']:.2f} s; {got['stress']}")
+    assert got["chosen"] in ("light", "strict")
+    assert got["ok"]
+
