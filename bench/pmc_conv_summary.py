@@ -24,7 +24,7 @@ def load(d):
     per = defaultdict(dict)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "conv" not in r["Kernel_Name"]:
+            if "conv" not in r["Kernel_Name"] and "winograd" not in r["Kernel_Name"]:
                 continue
             i = int(r["Dispatch_Id"])
             per[i][r["Counter_Name"]] = per[i].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])

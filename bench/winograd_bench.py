@@ -1,7 +1,8 @@
 """Winograd F(2x2,3x3) vs the implicit-GEMM MFMA conv on the ResNet-50 stride-1
 3x3 layers at per-GPU batch 256: forward (+BN stats) and dgrad, with the
 Winograd phase breakdown (filter / input transform / 16 GEMMs on the native MFMA kernel,
-with hipBLASLt bmm timed alongside as a comparator / output).
+with hipBLASLt bmm timed alongside as a comparator / output), and the FUSED forward
+(filter transform + one kernel, ops/winograd.py conv_fwd_fused).
 
     python bench/winograd_bench.py [--batch 256] > profiles/winograd_r01.txt
 """
@@ -35,8 +36,8 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     a = ap.parse_args()
     print(f"# batch {a.batch}; times in us; TF = useful direct-conv TFLOP/s")
-    print(f"{'layer':>16} | {'igemm fwd':>9} {'wino fwd':>9} | {'filt':>6} {'in':>7} {'gemm':>7} {'(bmm)':>8} {'out':>7} |"
-          f" {'igemm dg':>9} {'wino dg':>9}")
+    print(f"{'layer':>16} | {'igemm fwd':>9} {'wino fwd':>9} {'fused':>7} {'(kern)':>7} | {'filt':>6} {'in':>7} {'gemm':>7}"
+          f" {'(bmm)':>8} {'out':>7} | {'igemm dg':>9} {'wino dg':>9}")
     for c, h in ((64, 56), (128, 28), (256, 14), (512, 7)):
         k = c
         x = torch.randn(a.batch, h, h, c, device="cuda").to(torch.bfloat16)
@@ -56,7 +57,14 @@ def main():
         U = C.winograd_filter(wp[0], False)
         V = C.winograd_input(x)
         M = C.winograd_gemm(V, U)
-        t_ig, t_wg = timeit(ig), timeit(wg)
+        def fu():
+            y, st = WG.conv_fwd_fused(x, wp[0], True, HP._acquire(k, x.device))
+            HP._release(st)
+        C.conv_set_tile(1)     # the implicit GEMM alone (the tuner's candidate 14 IS the fused kernel)
+        t_ig = timeit(ig)
+        C.conv_set_tile(0)
+        t_wg, t_fu = timeit(wg), timeit(fu)
+        t_fk = timeit(lambda: C.winograd_fused_fwd(x, U, False))
         t_f = timeit(lambda: C.winograd_filter(wp[0], False))
         t_i = timeit(lambda: C.winograd_input(x))
         t_b = timeit(lambda: C.winograd_gemm(V, U))
@@ -65,8 +73,8 @@ def main():
         t_igd = timeit(lambda: HP.conv_dgrad(dy, wp, tuple(x.shape), 1, 1))
         t_wgd = timeit(lambda: WG.conv_dgrad(dy, wp[0], tuple(x.shape)))
         name = f"C{c}_H{h}_K{k}_R3"
-        print(f"{name:>16} | {t_ig:9.1f} {t_wg:9.1f} | {t_f:6.1f} {t_i:7.1f} {t_b:7.1f} ({t_bl:6.1f}) {t_o:7.1f} |"
-              f" {t_igd:9.1f} {t_wgd:9.1f}   (igemm {flops / t_ig / 1e6:.0f} TF, wino {flops / t_wg / 1e6:.0f} TF)",
+        print(f"{name:>16} | {t_ig:9.1f} {t_wg:9.1f} {t_fu:7.1f} ({t_fk:5.1f}) | {t_f:6.1f} {t_i:7.1f} {t_b:7.1f} ({t_bl:6.1f}) {t_o:7.1f} |"
+              f" {t_igd:9.1f} {t_wgd:9.1f}   (igemm {flops / t_ig / 1e6:.0f} TF, fused wino {flops / t_fu / 1e6:.0f} TF)",
               flush=True)
 
 

@@ -249,6 +249,34 @@ std::vector<Tensor> winograd_output(Tensor M, int64_t N, int64_t H, int64_t W, b
   return {y};
 }
 
+// fused Winograd forward: y [N,H,W,K] (+ [S,2,K] BN statistics about `shift`) from x [N,H,W,C] and the
+// transformed filter U [16,K,C] (winograd_filter) in ONE kernel (kernels/winograd.hip)
+std::vector<Tensor> winograd_fused_fwd(Tensor x, Tensor U, bool want_stats, c10::optional<Tensor> stats_buf,
+                                       c10::optional<Tensor> shift) {
+  CHECK_DEV(x); CHECK_BF16(x); CHECK_CONT(x);
+  CHECK_DEV(U); CHECK_BF16(U); CHECK_CONT(U);
+  TORCH_CHECK(x.dim() == 4 && U.dim() == 3 && U.size(0) == 16 && U.size(2) == x.size(3),
+              "winograd_fused_fwd: x [N,H,W,C], U [16,K,C]");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), K = U.size(1);
+  c10::DeviceGuard g(x.device());
+  Tensor y = torch::empty({N, H, W, K}, x.options());
+  Tensor stats;
+  if (want_stats) {
+    if (stats_buf && stats_buf->defined()) {
+      TORCH_CHECK(stats_buf->numel() == pmd_slots() * 2 * K, "stats buffer must be [S,2,K]");
+      opt_f32(stats_buf, "stats_buf");
+      stats = *stats_buf;
+    } else {
+      stats = pmd_zeros({pmd_slots(), 2, K}, x.options().dtype(torch::kFloat32));
+    }
+  }
+  CHECK_RC(pmd::winograd_fused_fwd_launch(bfp(x), bfp(U), bfp_mut(y), want_stats ? stats.data_ptr<float>() : nullptr,
+                                          want_stats ? shift_ptr(shift, K) : nullptr, N, H, W, C, K, cur_stream()),
+           "winograd_fused_fwd");
+  if (want_stats) return {y, stats};
+  return {y};
+}
+
 // dx[N,H,W,Cp] from dy[N,P,Q,K] and wkt[Cp,R,S,K]
 // addend: optional [N,H,W,Cp] bf16 added in the epilogue (dx = dgrad + addend)
 // bn_*: optional fused BN-backward reduce of the output (see pmd::BnReduceArgs);
@@ -1144,6 +1172,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("winograd_filter", &winograd_filter);
   m.def("winograd_input", &winograd_input);
   m.def("winograd_gemm", &winograd_gemm, py::arg("V"), py::arg("U"));
+  m.def("winograd_fused_fwd", &winograd_fused_fwd, py::arg("x"), py::arg("U"), py::arg("want_stats"),
+        py::arg("stats_buf") = py::none(), py::arg("shift") = py::none());
   m.def("winograd_output", &winograd_output, py::arg("M"), py::arg("N"), py::arg("H"), py::arg("W"),
         py::arg("want_stats"), py::arg("stats_buf"), py::arg("shift") = py::none());
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wkt"), py::arg("H"), py::arg("W"),

@@ -1467,13 +1467,15 @@ static void launch_big(const ConvArgs& a, hipStream_t st) {
 // Tile policy (conv_set_tile or PMD_CONV_TILE): 0 auto (autotuned per shape, else
 // 128-row tiles), 1 128-row tiles only, 2 256x128 wherever legal, 3 256x256
 // wherever legal (Nout >= 256), 4/5 8-wave 128-row tiles (see launch_w8),
-// 6..9 the P8 pipeline shapes 0..3 (see launch_p8) wherever legal.
+// 6..9 the P8 pipeline shapes 0..3 (see launch_p8) wherever legal, 10 the 64x128 tile, 11 / 12
+// the halo-image 3x3 kernel, 14 the fused Winograd forward (kernels/winograd.hip) wherever legal.
 static int g_conv_tile = -1;
 void conv_set_tile(int t) { g_conv_tile = t; }
 static int conv_tile() {
   if (g_conv_tile < 0) {
     const char* e = getenv("PMD_CONV_TILE");
-    g_conv_tile = (e && e[0] >= '0' && e[0] <= '9') ? e[0] - '0' : 0;
+    const int v = e ? atoi(e) : 0;
+    g_conv_tile = (v >= 0 && v <= 14) ? v : 0;
   }
   return g_conv_tile;
 }
@@ -1512,8 +1514,20 @@ static bool p8_ok(int shape, const ConvArgs& a) {
 //   10 64x128 tile, LDS-DMA BK=32 x2 stages (Nout > 64): half the rows per block, so
 //      an epilogue-bound short-reduction dgrad gets twice the blocks (and half the
 //      serial epilogue rows per thread) in flight
+//   14 fused Winograd F(2x2,3x3) forward (kernels/winograd.hip: filter transform + one kernel with
+//      the input transform, 16 MFMA GEMMs, output transform and the statistics epilogue)
+static bool wino_ok(const ConvArgs& a) {
+  return a.R == 3 && a.S == 3 && a.stride == 1 && a.pad == 1 && a.OH == a.H && a.OW == a.W &&
+         a.Cs % 64 == 0 && a.Nout % 64 == 0 && a.batch == 1 && a.out && !a.addend && !a.f8_sa;
+}
 template <bool DGRAD, bool STATS>
 static void launch_choice(int c, const ConvArgs& a, hipStream_t st) {
+  if constexpr (!DGRAD) {
+    if (c == 14 && wino_ok(a) &&
+        winograd_conv_fwd_run(a.src, a.wt, a.out, STATS ? a.stats : nullptr, STATS ? a.shift : nullptr, a.N, a.H,
+                              a.W, a.Cs, a.Nout, a.nslots, st) == 0)
+      return;   // (a failed launch -- e.g. its scratch cannot grow inside a capture -- runs the GEMM)
+  }
   if ((c == 11 || c == 12) && halo_ok(a)) {
     launch_halo<DGRAD, STATS>(a, st, c == 12 ? 3 : 2);
   } else if (c == 10 && a.Nout > 64) {
@@ -1630,15 +1644,18 @@ static int tune(const ConvArgs& a0, hipStream_t st) {
   }
   int best = -1;
   float best_ms = 1e30f;
+  char all[256];   // PMD_CONV_AUTOTUNE_LOG=2: every candidate's time
+  int alln = 0;
+  all[0] = 0;
   // the P8 shapes (6..9) measured equal or slower than 0..5 on every R50 layer
   // (profiles/conv_p8_r02.txt): forced-policy only, not timed by the tuner
   // (10, the 64x128 tile, measured slower than 0..5 on every short-K dgrad --
   // profiles/dgrad_epi_r02_tile10.txt -- so it is a forced policy only)
   // (the 32x32x16-MFMA 128-row tile measured slower than 0..5 on every ResNet-50 shape: not a
   // candidate; PMD_CONV_IMPL=6 forces it)
-  for (int c : {0, 1, 2, 3, 4, 5}) {
+  for (int c : {0, 1, 2, 3, 4, 5, 14}) {
     if ((c == 2 && !(big_ok(a) && a.Nout >= 256)) || (c == 3 && !big_ok(a)) || (c == 4 && a.Nout <= 64) ||
-        (c == 5 && (DGRAD || a.Cs < 64)))
+        (c == 5 && (DGRAD || a.Cs < 64)) || (c == 14 && (DGRAD || !wino_ok(a))))
       continue;
     launch_choice<DGRAD, STATS>(c, a, st);  // warm (code object load, caches)
     float t = 1e30f;
@@ -1655,12 +1672,13 @@ static int tune(const ConvArgs& a0, hipStream_t st) {
       best_ms = t;
       best = c;
     }
+    if (alln < 200) alln += snprintf(all + alln, sizeof(all) - alln, " %d:%.1f", c, t * 1e3f);
   }
   const char* lg = getenv("PMD_CONV_AUTOTUNE_LOG");
-  if (lg && lg[0] == '1')
-    fprintf(stderr, "[pmd autotune] %s N=%d H=%d W=%d C=%d -> %dx%d K=%d R=%d s=%d: choice %d (%.1f us)\n",
+  if (lg && (lg[0] == '1' || lg[0] == '2'))
+    fprintf(stderr, "[pmd autotune] %s N=%d H=%d W=%d C=%d -> %dx%d K=%d R=%d s=%d: choice %d (%.1f us)%s%s\n",
             DGRAD ? "dgrad" : "fwd", a.N, a.H, a.W, a.Cs, a.OH, a.OW, a.Nout, a.R, a.stride, best,
-            best_ms * 1e3f);
+            best_ms * 1e3f, lg[0] == '2' ? " | us per candidate:" : "", lg[0] == '2' ? all : "");
   return best;
 }
 
@@ -1692,7 +1710,9 @@ static void launch_sel(const ConvArgs& a, hipStream_t st) {
     }
   }
   const int t = conv_tile();
-  if ((t == 11 || t == 12) && halo_ok(a)) {
+  if (t == 14 && !DGRAD) {
+    launch_choice<DGRAD, STATS>(14, a, st);   // fused Winograd wherever eligible (forced policy)
+  } else if ((t == 11 || t == 12) && halo_ok(a)) {
     launch_choice<DGRAD, STATS>(t, a, st);
   } else if (t == 10 && a.Nout > 64) {
     launch_choice<DGRAD, STATS>(10, a, st);

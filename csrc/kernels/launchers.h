@@ -46,6 +46,15 @@ int winograd_filter_launch(const bf16_t* wk, bf16_t* U, int K, int Cp, bool flip
 int winograd_input_launch(const bf16_t* x, bf16_t* V, int N, int H, int W, int C, hipStream_t st);
 int winograd_output_launch(const bf16_t* M, bf16_t* y, float* stats, int N, int H, int W, int K,
                            hipStream_t st, const float* shift = nullptr);
+// the fused forward (input transform, 16 MFMA GEMMs, output transform + BN statistics in one kernel)
+// from the transformed filter U [16][K][C]; C % 64 == 0, K % 64 == 0
+int winograd_fused_fwd_launch(const bf16_t* x, const bf16_t* U, bf16_t* y, float* stats, const float* shift,
+                              int N, int H, int W, int C, int K, hipStream_t st);
+int winograd_fused_fwd_run(const bf16_t* x, const bf16_t* U, bf16_t* y, float* stats, const float* shift, int N,
+                           int H, int W, int C, int K, int nslots, hipStream_t st);
+// filter transform of the weight image wk [K][3][3][C] into a per-stream scratch + the fused kernel
+int winograd_conv_fwd_run(const bf16_t* x, const bf16_t* wk, bf16_t* y, float* stats, const float* shift, int N,
+                          int H, int W, int C, int K, int nslots, hipStream_t st);
 // linear-BN backward helpers (kernels/bnlin.hip)
 int bnlin_coeff_launch(const float* red, const float* count, float count_h, const float* gamma, const float* params,
                        const bf16_t* wk, bf16_t* g, float* bias, float* abc, int K, int C, int Cp, hipStream_t st);

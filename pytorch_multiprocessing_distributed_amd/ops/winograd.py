@@ -12,12 +12,18 @@ implicit-GEMM MFMA kernel (``C.winograd_gemm``; no library GEMM):
     y  = winograd_output(M)             [N, H, W, K] (A^T M A) + fused BN statistics
 
 Dgrad of the same layer is the same pipeline on dY with the flipped,
-channel-transposed filter.  NOT on the training path: an explicit API
-(:func:`conv_fwd` / :func:`conv_dgrad`, tests and bench/winograd_bench.py only).
-The implicit-GEMM MFMA kernel is faster on every ResNet-50 layer on MI355X: the
-transformed operands are 4x the activation bytes and the transforms alone run at
-the HBM roofline (profiles/winograd_r02_native_gemm.txt, counters in
-profiles/pmc_winograd_r03.txt; the fused-kernel bound in docs/ARCHITECTURE.md).
+channel-transposed filter (explicit API, :func:`conv_dgrad`): the unfused pipeline moves
+the transformed operands (4x the activation bytes) through HBM and loses to the implicit
+GEMM on every ResNet-50 layer (profiles/winograd_r02_native_gemm.txt,
+profiles/pmc_winograd_r03.txt).
+
+The FUSED forward (:func:`conv_fwd_fused`, ``winograd_fused_fwd_kernel``) keeps V and M on
+the CU: per block the input transform of 32 tiles x 64 channels goes into LDS, 4 waves run
+the 16 transformed-domain GEMMs on v_mfma_f32_16x16x32_bf16 (4 positions each), and the
+output transform + BN-statistics epilogue read the accumulators back through LDS.  It is
+candidate 14 of the conv autotuner (kernels/conv_igemm.hip: the filter transform + the fused
+kernel, timed against the implicit-GEMM tiles on the live operands), so the tuning tables
+adopt it for exactly the stride-1 3x3 shapes where it wins (profiles/winograd_fused_r06.txt).
 
 ``conv_ref`` is the same algorithm in plain torch fp32 -- the CPU numerics
 reference of the transforms (tests/test_winograd_cpu.py).
@@ -92,3 +98,19 @@ def conv_dgrad(dy, wk, x_shape):
     M = C.winograd_gemm(V, U)                        # [16, T, Cp]
     N, H, W, _ = x_shape
     return C.winograd_output(M, N, H, W, False, None)[0]
+
+
+def fused_eligible(wk_shape, stride, pad) -> bool:
+    """The fused forward's contract: stride-1 pad-1 3x3 with C % 64 == 0 and K % 64 == 0."""
+    K, R, S, C = wk_shape
+    return R == 3 and S == 3 and int(stride) == 1 and int(pad) == 1 and C % 64 == 0 and K % 64 == 0
+
+
+def conv_fwd_fused(x, wk, want_stats, stats_buf=None, shift=None):
+    """Forward (+ conv_fwd-compatible [slots,2,K] statistics about ``shift``) in ONE fused
+    kernel after the filter transform."""
+    C = _c()
+    U = C.winograd_filter(wk, False)                 # [16, K, C]
+    out = C.winograd_fused_fwd(x, U, bool(want_stats), stats_buf, shift)
+    return (out[0], out[1]) if want_stats else (out[0], None)
+
