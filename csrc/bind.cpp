@@ -847,6 +847,42 @@ Tensor stem_pool_bwd_elemt(Tensor dout, Tensor arg, Tensor y, Tensor params, Ten
   return dy;
 }
 
+// Fused stem backward: the stem conv's weight gradient dws [64,4,4,16] (the space-to-depth
+// image's 4x4 conv, fp32) straight from the pooled gradient -- the max-pool + BN(+ReLU)
+// backward elementwise pass runs inside the weight-gradient kernel, so dy [N,112,112,64] is never
+// materialised (kernels/conv_wgrad.hip stem_wgrad_fused_kernel).  Undefined tensor when the
+// geometry is outside the kernel's plan (the caller runs stem_pool_bwd_elemt + conv_wgrad).
+Tensor stem_wgrad_fused(Tensor dout, Tensor arg, Tensor y, Tensor params, Tensor gamma, Tensor red,
+                        c10::optional<Tensor> count, double count_h, Tensor xs, int64_t pad) {
+  CHECK_DEV(dout); CHECK_BF16(dout); CHECK_CONT(dout); CHECK_CONT(arg);
+  CHECK_DEV(y); CHECK_BF16(y); CHECK_CONT(y); CHECK_F32(params); CHECK_CONT(params);
+  CHECK_DEV(xs); CHECK_BF16(xs); CHECK_CONT(xs);
+  const int N = xs.size(0), H = xs.size(1), W = xs.size(2), C = xs.size(3);
+  const int P = y.size(1), Q = y.size(2), K = y.size(3), P2 = dout.size(1), Q2 = dout.size(2);
+  TORCH_CHECK(y.size(0) == N && dout.size(0) == N && dout.size(3) == K && arg.sizes() == dout.sizes(),
+              "stem_wgrad_fused: shapes");
+  TORCH_CHECK(params.numel() == 4 * K && red.numel() == 2 * K && gamma.numel() == K, "stem_wgrad_fused: BN sizes");
+  Tensor gm = gamma.contiguous().to(torch::kFloat32), rr = red.contiguous(), cc;
+  if (count && count->defined()) cc = count->contiguous();
+  c10::DeviceGuard g(y.device());
+  int splits = 0;
+  const int q = pmd::stem_wgrad_fused_launch(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f,
+                                             nullptr, nullptr, nullptr, N, H, W, C, P, Q, K, 4, 4, (int)pad, P2, Q2,
+                                             &splits, cur_stream());
+  if (q != 0) return Tensor();
+  Tensor dw = pmd_zeros({K, 4, 4, C}, y.options().dtype(torch::kFloat32));
+  Tensor ws;
+  if (splits > 1) ws = torch::empty({splits, K, 16 * C}, y.options().dtype(torch::kFloat32));
+  CHECK_RC(pmd::stem_wgrad_fused_launch(bfp(dout), arg.data_ptr<uint8_t>(), bfp(y), params.data_ptr<float>(),
+                                        gm.data_ptr<float>(), rr.data_ptr<float>(),
+                                        cc.defined() ? cc.data_ptr<float>() : nullptr, (float)count_h, bfp(xs),
+                                        dw.data_ptr<float>(), splits > 1 ? ws.data_ptr<float>() : nullptr, N, H, W, C,
+                                        P, Q, K, 4, 4, (int)pad, P2, Q2, nullptr, cur_stream()),
+           "stem_wgrad_fused");
+  keep_ws(ws);
+  return dw;
+}
+
 Tensor avgpool_fwd(Tensor x) {
   CHECK_DEV(x); CHECK_BF16(x); CHECK_CONT(x);
   const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
@@ -1169,6 +1205,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_s2d_input", &stem_s2d_input);
   m.def("stem_s2d_weight", &stem_s2d_weight);
   m.def("stem_s2d_wgrad_fold", &stem_s2d_wgrad_fold);
+  m.def("stem_wgrad_fused", &stem_wgrad_fused, py::arg("dout"), py::arg("arg"), py::arg("y"), py::arg("params"),
+        py::arg("gamma"), py::arg("red"), py::arg("count"), py::arg("count_h"), py::arg("xs"), py::arg("pad"));
   m.def("winograd_filter", &winograd_filter);
   m.def("winograd_input", &winograd_input);
   m.def("winograd_gemm", &winograd_gemm, py::arg("V"), py::arg("U"));

@@ -21,6 +21,7 @@
 // single-carry increments, so the gather costs no integer divisions in the
 // main loop.
 #include "common.h"
+#include "stem_tile.h"
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -814,6 +815,230 @@ static bool halo_cfg(const WgradArgs& a, HaloArgs* h, int* nich) {
 
 static int halo_splits(const HaloArgs& h) { return (h.bands + h.bpb - 1) / h.bpb; }
 
+// ---------------------------------------------------------------------------
+// Fused ImageNet-stem backward: the max-pool + BatchNorm(+ReLU) backward elementwise pass
+// (stem.hip stem_pool_bwd_elemt_kernel: dy = a * dz + b * y + c, dz = the pooled gradient
+// routed to each window's argmax, gated by the ReLU of BN(y)) computes each band's dY rows
+// straight into the halo weight gradient's dY stage (same swizzled [224][64] layout the
+// LDS-DMA fills in conv_wgrad_halo_kernel), so the [N,112,112,64] stem gradient is never
+// written nor read back: per step 2 x 411 MB of HBM traffic and one launch less at the end
+// of the backward's critical path.  Band b = (image n, pooled row pb) = output rows 2 pb,
+// 2 pb + 1 (the halo plan's 2-row bands of the 112-wide stem output), whose candidate windows
+// are pooled rows pb and pb + 1, staged in LDS.  The next band's y rows, pooled rows and halo
+// are in flight while this band's MFMAs run.
+struct StemDyArgs {
+  const bf16_t* dout;   // pooled gradient [N, P2, Q2, 64]
+  const uint8_t* arg;   // window argmax taps [N, P2, Q2, 64]
+  const bf16_t* y;      // stem conv output = BN input [N, P, Q, 64]
+  const float* params;  // BN [4][64]: mean, invstd, scale, shift
+  const float* gamma;   // [64]
+  const float* red;     // [2][64] global sums of dz, dz * xhat
+  const float* count;   // [1] global element count per channel, or null: count_h
+  float count_h;
+  int P2, Q2;
+};
+constexpr int kStemPoolMaxQ = 64;  // staged pooled row width (LDS)
+
+__global__ __launch_bounds__(512, 1) void stem_wgrad_fused_kernel(WgradArgs a, HaloArgs h, StemDyArgs s) {
+  // 8 waves (2 per SIMD): one wave's in-kernel dY production overlaps another's MFMAs; a
+  // two-stage ring (the next band's halo / y / pooled rows in flight during this band's MFMAs)
+  constexpr int NT = 512, NI = 2, HCH = 1280;
+  constexpr int KS = kHaloRows / 32;
+  constexpr int HBYTES = HCH * 16;
+  constexpr int DBYTES = kHaloRows * 128;
+  constexpr int STAGE = HBYTES + DBYTES;
+  constexpr int HPT = (HCH + NT - 1) / NT;
+  constexpr int YPT = (kHaloRows * 8 + NT - 1) / NT;        // dY chunks produced per thread (3.5)
+  constexpr int PBYTES = 2 * kStemPoolMaxQ * 64 * 3;        // pooled gradient + taps of 2 rows
+  constexpr int PPT = (2 * kStemPoolMaxQ * 8 + NT - 1) / NT;  // staged pooled chunks per thread
+  static_assert(2 * STAGE + PBYTES <= 160 * 1024, "fused stem wgrad LDS");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + PBYTES];
+  bf16_t* dl = reinterpret_cast<bf16_t*>(smem + 2 * STAGE);
+  uint8_t* al = reinterpret_cast<uint8_t*>(smem + 2 * STAGE + 2 * kStemPoolMaxQ * 64 * 2);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wid_s = __builtin_amdgcn_readfirstlane(wid);
+  const int b0 = blockIdx.x * h.bpb;
+  if (b0 >= h.bands) return;
+  const int b1 = min(b0 + h.bpb, h.bands);
+
+  // BN-backward coefficients of this thread's fixed 8-channel chunk (j & 7 == tid & 7)
+  const int cc = tid & 7;
+  float sc[8], sh[8], ca[8], cb[8], cz[8];
+  {
+    const float inv_cnt = 1.f / (s.count ? s.count[0] : s.count_h);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = cc * 8 + k;
+      const float mean = s.params[c], inv = s.params[64 + c], gm = s.gamma[c];
+      sc[k] = s.params[128 + c];
+      sh[k] = s.params[192 + c];
+      stem_bwd_coeffs(gm, inv, mean, s.red[c] * inv_cnt, s.red[64 + c] * inv_cnt, ca[k], cb[k], cz[k]);
+    }
+  }
+  int hsrc[HPT];
+#pragma unroll
+  for (int t = 0; t < HPT; ++t) {
+    const int L = t * NT + wid * 64 + lane;
+    const int o = L / h.pitchC, pix = L - o * h.pitchC;
+    hsrc[t] = (L < HCH && o < h.CO && pix < h.HR * h.HWp) ? ((o << 20) | ((pix / h.HWp) << 12) | (pix % h.HWp)) : -1;
+  }
+  uint4 yv[YPT], pg[PPT];
+  uint2 pa[PPT];
+  // global loads of band `band`: halo (LDS-DMA into stage buf), y rows and pooled rows (registers)
+  auto issue = [&](int band, int buf) {
+    const int n = band / h.bands_img, pb = band - n * h.bands_img;
+    const int p0 = pb * h.PB;
+    char* Hs = smem + buf * STAGE;
+#pragma unroll
+    for (int t = 0; t < HPT; ++t) {
+      const int e = hsrc[t];
+      if (e >= 0) {
+        const int o = e >> 20, hr = (e >> 12) & 0xff, hc = e & 0xfff;
+        const int ih = p0 - a.pad + hr, iw = hc - a.pad;
+        const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        const void* src = ok ? (const void*)(a.x + ((((size_t)n * a.H + ih) * a.W + iw) << a.log2C) + 8 * o)
+                             : (const void*)g_wzero16;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(Hs + (t * NT + wid_s * 64) * 16),
+                                         16, 0, 0);
+      }
+    }
+    const size_t yrow0 = ((size_t)n * a.P + p0) * a.Q;
+#pragma unroll
+    for (int t = 0; t < YPT; ++t) {
+      const int row = (t * NT + tid) >> 3;            // < PB * Q rows (launcher: PB * Q == 224)
+      if (row < kHaloRows) yv[t] = *reinterpret_cast<const uint4*>(s.y + (yrow0 + row) * 64 + cc * 8);
+    }
+    const int prow = pb + 1 < s.P2 ? 2 : 1;
+    const size_t pbase = ((size_t)n * s.P2 + pb) * s.Q2 * 8;
+#pragma unroll
+    for (int t = 0; t < PPT; ++t) {
+      const int i = t * NT + tid;
+      if (i < prow * s.Q2 * 8) {
+        pg[t] = reinterpret_cast<const uint4*>(s.dout)[pbase + i];
+        pa[t] = reinterpret_cast<const uint2*>(s.arg)[pbase + i];
+      }
+    }
+  };
+  // dY rows of band `band` into the dY stage of buf (from the registers `issue` filled)
+  auto produce = [&](int band, int buf) {
+    const int n = band / h.bands_img, pb = band - n * h.bands_img;
+    (void)n;
+    const int prow = pb + 1 < s.P2 ? 2 : 1;
+#pragma unroll
+    for (int t = 0; t < PPT; ++t) {
+      const int i = t * NT + tid;
+      if (i < prow * s.Q2 * 8) {
+        reinterpret_cast<uint4*>(dl)[i] = pg[t];
+        reinterpret_cast<uint2*>(al)[i] = pa[t];
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    char* Ds = smem + buf * STAGE + HBYTES;
+    const StemBwdTile tl{dl, al, pb, s.P2, s.Q2, 8};
+#pragma unroll
+    for (int t = 0; t < YPT; ++t) {
+      const int row = (t * NT + tid) >> 3;
+      if (row >= kHaloRows) break;
+      const int r = row / a.Q, w = row - r * a.Q;
+      float v[8], d[8], o[8];
+      unpack8(yv[t], v);
+      tl.dz(pb * 2 + r, w, cc, v, sc, sh, d);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = stem_bwd_dy(ca[k], cb[k], cz[k], d[k], v[k]);
+      *reinterpret_cast<uint4*>(Ds + row * 128 + ((((cc >> 1) ^ swz<128>(row)) << 5) | ((cc & 1) << 4))) = pack8(o);
+    }
+  };
+
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  int rofs[KS][2];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int hl = 0; hl < 2; ++hl) {
+      const int mr = ks * 32 + 8 * g + q4 + 4 * hl;
+      const int pr = mr / a.Q;
+      rofs[ks][hl] = mr < h.PB * a.Q ? 16 * (pr * h.HWp + (mr - pr * a.Q)) : 0;
+    }
+  int cofs[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int kgc = wid * (16 * NI) + j * 16 + 4 * p4;
+    const int tap = kgc >> a.log2C, c = kgc & (a.C - 1);
+    const int r = tap / a.S, sx = tap - r * a.S;
+    cofs[j] = (c >> 3) * h.pitchC * 16 + 16 * (r * h.HWp + sx) + 8 * ((c >> 2) & 1);
+  }
+  f32x4 acc[4][NI];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  auto compute = [&](int buf) {
+    const char* Hs = smem + buf * STAGE;
+    const char* Ds = Hs + HBYTES;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 af[4], bfg[NI];
+      const int r0 = ks * 32 + 8 * g + q4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int col = i * 16 + 4 * p4;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(Ds + toff<64>(r0, col)));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(Ds + toff<64>(r0 + 4, col)));
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(Hs + cofs[j] + rofs[ks][0]));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(Hs + cofs[j] + rofs[ks][1]));
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfg[j] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  issue(b0, 0);
+  for (int b = b0; b < b1; ++b) {
+    const int buf = (b - b0) & 1;
+    wg_wait_vmcnt<0>();
+    // every wave is done with the previous band's MFMAs (the other stage) and its dz reads
+    // of the staged pooled rows, which produce() overwrites
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    produce(b, buf);
+    if (b + 1 < b1) issue(b + 1, buf ^ 1);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // dY stage of band b published
+    compute(buf);
+  }
+
+  float* dst = a.ws ? a.ws + (size_t)blockIdx.x * 64 * a.Kg : a.dw;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = i * 16 + (lane >> 4) * 4 + e;
+        const int gg = wid * (16 * NI) + j * 16 + (lane & 15);
+        float* pp = dst + (size_t)k * a.Kg + gg;
+        if (a.ws)
+          stfn<NT_WS_ST>(pp, acc[i][j][e]);
+        else
+          *pp += acc[i][j][e];
+      }
+}
+
 static int ilog2w(int v) {
   int l = 0;
   while ((1 << l) < v) ++l;
@@ -1332,6 +1557,39 @@ int conv_wgrad_launch(const bf16_t* dy, const bf16_t* x, float* dw, float* ws, i
     if (impl == 4 && wgrad_cfg_ok(1, a)) impl = 1;
   }
   wgrad_run(impl, a, ws, st);
+  return 0;
+}
+
+
+// Fused stem backward (stem_wgrad_fused_kernel): the stem conv's weight gradient from the pooled
+// gradient, with its dY produced in-kernel.  Geometry of the stem conv as for conv_wgrad_launch
+// (x = the space-to-depth input [N,H,W,16], P x Q = the conv output = the BN input y); returns
+// the split count through *splits (query with dw == nullptr), nonzero when the halo plan does not
+// give 2-row bands of the pooled grid (the caller then runs the unfused passes).
+int stem_wgrad_fused_launch(const bf16_t* dout, const uint8_t* arg, const bf16_t* y, const float* params,
+                            const float* gamma, const float* red, const float* count, float count_h,
+                            const bf16_t* x, float* dw, float* ws, int N, int H, int W, int C, int P, int Q,
+                            int K, int R, int S, int pad, int P2, int Q2, int* splits, hipStream_t st) {
+  if (K != 64 || C != 16 || R != 4 || S != 4) return 1;
+  if ((long long)N * P * Q >= (1ll << 31)) return 4;
+  WgradArgs a;
+  a.dy = nullptr;
+  a.x = x;
+  a.dw = dw;
+  fill_args(a, N, H, W, C, P, Q, K, R, S, 1, pad);
+  HaloArgs h;
+  int ni;
+  if (!halo_cfg(a, &h, &ni) || ni != 4 || h.PB != 2 || h.PB * a.Q != kHaloRows || P % 2 || P2 * 2 != P ||
+      h.bands_img != P2 || Q2 > kStemPoolMaxQ || (Q + 1) / 2 != Q2)
+    return 2;
+  const int sp = halo_splits(h);
+  if (splits) *splits = sp;
+  if (!dw) return 0;
+  if (sp > 1 && !ws) return 3;
+  a.ws = sp > 1 ? ws : nullptr;
+  StemDyArgs s{dout, arg, y, params, gamma, red, count, count_h, P2, Q2};
+  hipLaunchKernelGGL(stem_wgrad_fused_kernel, dim3(sp), dim3(512), 0, st, a, h, s);
+  if (sp > 1) wgrad_reduce_launch(a, sp, st);
   return 0;
 }
 

@@ -151,6 +151,12 @@ int stem_pool_bwd_elemt_launch(const bf16_t* dout, const uint8_t* arg, const bf1
                                const float* gamma, const float* red, const float* count, float count_h,
                                bf16_t* dy, int N, int H, int W, int C, int P, int Q, bool eval_mode,
                                hipStream_t st);
+// the fused stem backward: stem conv weight gradient with its dY (max-pool + BN backward) produced
+// in-kernel (kernels/conv_wgrad.hip); dw == nullptr: only report the workspace split count
+int stem_wgrad_fused_launch(const bf16_t* dout, const uint8_t* arg, const bf16_t* y, const float* params,
+                            const float* gamma, const float* red, const float* count, float count_h,
+                            const bf16_t* x, float* dw, float* ws, int N, int H, int W, int C, int P, int Q,
+                            int K, int R, int S, int pad, int P2, int Q2, int* splits, hipStream_t st);
 int maxpool_fwd_launch(const bf16_t* x, bf16_t* out, uint8_t* arg, int N, int H, int W, int C, int P,
                        int Q, hipStream_t st);
 int maxpool_bwd_launch(const bf16_t* dout, const uint8_t* arg, bf16_t* dx, int N, int H, int W, int C,

@@ -10,6 +10,7 @@
 // Reference: model/resnet.py:97 (conv -> SyncBN -> relu) followed by the
 // ImageNet max-pool this framework adds for 224x224 inputs.
 #include "common.h"
+#include "stem_tile.h"
 
 namespace pmd {
 
@@ -75,63 +76,6 @@ __global__ __launch_bounds__(256) void stem_pool_fwd_kernel(const bf16_t* __rest
   packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
   packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
   reinterpret_cast<uint2*>(arg)[o] = packed;
-}
-
-// Backward of the fused stem tail.  Block = (image n, pooled row p): it owns
-// input rows 2p and 2p+1 -- exactly the rows whose windows lie in pooled rows p
-// and p+1 -- and stages those two pooled rows of dout and argmax taps in LDS
-// once, so every input pixel reads its (1, 2 or 4) candidate windows from LDS
-// instead of gathering 4 clamped windows from L2 (8 global loads per 16-B
-// output chunk before; profiles/pool_bench).  Candidates are visited in
-// ascending (p, q) order, the order of the composite maxpool_bwd sum.
-struct StemBwdTile {
-  const bf16_t* dl;   // LDS [2][Q][C] pooled gradient of rows p, p+1
-  const uint8_t* al;  // LDS [2][Q][C] argmax taps
-  int p, P, Q, C8;
-  // dz of the 8-channel chunk (h, w, cc): bf16-rounded sum of the dout of the
-  // windows whose argmax is this pixel, gated by the ReLU of BN(y)
-  __device__ __forceinline__ void dz(int h, int w, int cc, const float (&v)[8], const float (&sc)[8],
-                                     const float (&sh)[8], float (&out)[8]) const {
-    float acc[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-    const int odd_h = h & 1, odd_w = w & 1;
-    const int q0 = w >> 1;
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {      // pooled row p + a
-      if (a == 1 && (!odd_h || p + 1 >= P)) break;
-      const int dh = odd_h ? (a == 0 ? 2 : 0) : 1;
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {    // pooled col q0 + b
-        if (b == 1 && (!odd_w || q0 + 1 >= Q)) break;
-        const int dw = odd_w ? (b == 0 ? 2 : 0) : 1;
-        const int tp = dh * 3 + dw;
-        const int o = (a * Q + q0 + b) * C8 + cc;
-        const uint4 gv = reinterpret_cast<const uint4*>(dl)[o];
-        const uint2 av = reinterpret_cast<const uint2*>(al)[o];
-        float g[8];
-        unpack8(gv, g);
-        const uint32_t aw[2] = {av.x, av.y};
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if ((int)((aw[k >> 2] >> ((k & 3) * 8)) & 0xff) == tp) acc[k] += g[k];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) out[k] = (v[k] * sc[k] + sh[k] > 0.f) ? round_bf(acc[k]) : 0.f;
-  }
-};
-
-// stage pooled rows p, p+1 (the second only if it exists) of image n into LDS
-__device__ __forceinline__ void stem_stage_pooled(const bf16_t* __restrict__ dout, const uint8_t* __restrict__ arg,
-                                                  bf16_t* dl, uint8_t* al, int n, int p, int P, int Q, int C8) {
-  const int per_row = Q * C8;
-  const int rows = p + 1 < P ? 2 : 1;
-  const size_t base = ((size_t)n * P + p) * per_row;
-  for (int i = threadIdx.x; i < rows * per_row; i += blockDim.x) {
-    reinterpret_cast<uint4*>(dl)[i] = reinterpret_cast<const uint4*>(dout)[base + i];
-    reinterpret_cast<uint2*>(al)[i] = reinterpret_cast<const uint2*>(arg)[base + i];
-  }
 }
 
 // Pass 1: per-channel sum(dz), sum(dz * xhat) into kStatSlots slot copies.
@@ -226,13 +170,7 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_elemt_kernel(
     ld8(red + c0, q0);
     ld8(red + C + c0, q1);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float a = g[k] * inv[k];
-      const float mdy = q0[k] * inv_cnt, mdyx = q1[k] * inv_cnt;
-      ca[k] = a;
-      cb[k] = -a * inv[k] * mdyx;
-      ccf[k] = a * (mean[k] * inv[k] * mdyx - mdy);
-    }
+    for (int k = 0; k < 8; ++k) stem_bwd_coeffs(g[k], inv[k], mean[k], q0[k] * inv_cnt, q1[k] * inv_cnt, ca[k], cb[k], ccf[k]);
   }
   __syncthreads();
   const StemBwdTile t{dl, al, p, P, Q, C8};
@@ -247,7 +185,7 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_elemt_kernel(
     unpack8(ld16n<NT_STEM>(reinterpret_cast<const uint4*>(y) + i), v);
     t.dz(h, w, cc, v, sc, sh, d);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) o[k] = EVAL ? ca[k] * d[k] : ca[k] * d[k] + cb[k] * v[k] + ccf[k];
+    for (int k = 0; k < 8; ++k) o[k] = EVAL ? ca[k] * d[k] : stem_bwd_dy(ca[k], cb[k], ccf[k], d[k], v[k]);
     reinterpret_cast<uint4*>(dy)[i] = pack8(o);
   }
 }

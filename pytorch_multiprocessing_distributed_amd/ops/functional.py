@@ -887,6 +887,7 @@ class _StemS2DConvFn(torch.autograd.Function):
         buf = HP._acquire(w.shape[0], x.device) if want else None
         out = C.conv_fwd_hw(xs, ws, 1, 2, oh, ow, want, buf, shift)
         y = out[0]
+        y._pmd_s2d = True       # its gradient may arrive lazily from the fused stem tail
         stats = out[1] if want else _empty(x.device)
         ctx.save_for_backward(xs)
         ctx.w = w
@@ -901,7 +902,17 @@ class _StemS2DConvFn(torch.autograd.Function):
         w = ctx.w
         if dy is None or not ctx.needs_input_grad[1] or not w.requires_grad:
             return None, None, None
-        dws = C.conv_wgrad(dy.contiguous(), xs, 4, 4, 1, 2, None)   # fp32 [K, 4, 4, 16]
+        lazy = getattr(dy, "_pmd_stem", None)
+        dws = None
+        if lazy is not None:
+            # the fused stem tail handed over its backward elementwise pass (_StemPoolFn): the
+            # weight gradient produces dy itself, which is never written
+            from . import hip_prims as HP
+            dws = HP.stem_wgrad_fused(*lazy, xs, 2)
+            if dws is None:                                          # outside the fused plan
+                dy = HP.stem_pool_bwd_elemt(*lazy[:7])
+        if dws is None:
+            dws = C.conv_wgrad(dy.contiguous(), xs, 4, 4, 1, 2, None)   # fp32 [K, 4, 4, 16]
         tgt = _grad_target(w)
         if tgt is not None:
             C.stem_s2d_wgrad_fold(dws, w.shape[1], tgt.permute(0, 2, 3, 1))
@@ -1009,6 +1020,9 @@ class _StemPoolFn(torch.autograd.Function):
         sync = _state["bn_sync"] if training else None
         p, _, count = _bn_forward_params(P, y, st, bn, training, sync, k1=k1)
         out, arg = P.stem_pool_fwd(y, p)
+        # the producer is the space-to-depth stem conv (its only consumer is this node): the
+        # backward may hand it the elementwise pass instead of a materialised dy
+        ctx.lazy = bool(getattr(y, "_pmd_s2d", False)) and training and _STEM_LAZY
         ctx.cfg = (bn, training, sync, count)
         ctx.arg = arg
         ctx.save_for_backward(y, p)
@@ -1024,11 +1038,26 @@ class _StemPoolFn(torch.autograd.Function):
         red = P.stem_pool_bwd_reduce(dout, arg, y, p)
 
         def elemt(r, cnt):
+            if ctx.lazy and r is not None:
+                # dy for the stem conv's weight gradient, produced inside that kernel
+                # (_StemS2DConvFn.backward -> stem_wgrad_fused): a stand-in of y's shape without
+                # storage, carrying the elementwise pass's operands
+                lz = torch.empty((), dtype=y.dtype, device=y.device).expand(y.shape)
+                lz._pmd_stem = (dout, arg, y, p, bn.weight, r.contiguous(), cnt)
+                return lz
             return P.stem_pool_bwd_elemt(dout, arg, y, p, bn.weight, r, cnt, eval_mode=not training)
         dy, _, _, g = _bn_backward(P, dout, None, True, training, sync, count, y, p, bn, pre=[red],
                                    elemt_fn=elemt)
         ctx.arg = None
         return None, dy, None, g[0], g[1]
+
+
+# PMD_STEM_LAZY=1: the stem's backward elementwise pass inside the stem conv's weight gradient
+# (kernels/conv_wgrad.hip stem_wgrad_fused_kernel: dy [N,112,112,64] never written nor re-read, -0.8 GB
+# per step; bit-identical to the two passes, tests/test_stem_s2d_gpu.py).  Measured step-neutral
+# (18.587 vs 18.567 ms, 3 interleaved rounds, profiles/stem_fused_r06.txt): the end of the backward is
+# bounded by the side stream's layer-1 weight gradients, not by the stem -- off by default.
+_STEM_LAZY = os.environ.get("PMD_STEM_LAZY", "0") == "1"
 
 
 def fused_stem_enabled():

@@ -237,6 +237,16 @@ def stem_pool_bwd_elemt(dout, arg, y, p, gamma, red, count, eval_mode=False):
                                   float(count or 1.0), bool(eval_mode))
 
 
+def stem_wgrad_fused(dout, arg, y, p, gamma, red, count, xs, pad):
+    """Stem conv weight gradient (s2d image, fp32 [64,4,4,16]) with the stem's max-pool + BN
+    backward elementwise pass inside the kernel; None when the geometry is outside its plan."""
+    if torch.is_tensor(count):
+        r = _C.stem_wgrad_fused(dout, arg, y, p, gamma.detach(), red, count, 0.0, xs, int(pad))
+    else:
+        r = _C.stem_wgrad_fused(dout, arg, y, p, gamma.detach(), red, None, float(count or 1.0), xs, int(pad))
+    return r if r is not None and r.numel() > 0 else None
+
+
 def avgpool_fwd(x):
     return _C.avgpool_fwd(x)
 

@@ -66,3 +66,44 @@ def test_s2d_stem_resnet50_step():
             OF.set_s2d_stem(True)
     assert abs(res[True][0] - res[False][0]) < 1e-2 * max(1.0, abs(res[False][0]))
     assert _rel(res[True][1], res[False][1]) < 5e-2
+
+
+@pytest.mark.parametrize("n,h,fused", [(3, 224, True), (2, 96, False)])
+def test_fused_stem_backward_matches_two_pass(n, h, fused, monkeypatch):
+    """The stem's max-pool + BN(+ReLU) backward elementwise pass run INSIDE the stem weight
+    gradient (stem_wgrad_fused: dy never materialised) == the two-pass path (stem_pool_bwd_elemt
+    writes dy, the halo wgrad reads it back): bit for bit, in the deterministic statistics mode
+    with the halo weight-gradient variant pinned.  96x96 inputs are outside the fused plan
+    (3-row bands): the stand-in dy falls back to the two passes."""
+    from pytorch_multiprocessing_distributed_amd.models import ResNet50
+    from pytorch_multiprocessing_distributed_amd.ops import functional as OF
+    from pytorch_multiprocessing_distributed_amd.ops import hip_prims as HP
+    from pytorch_multiprocessing_distributed_amd.ops.native import C
+    x, y = C.synth_images(n, h, h, 8, 3, 1000, 11, 0)
+    calls = {"fused": 0}
+    orig = HP.stem_wgrad_fused
+
+    def spy(*a, **k):
+        r = orig(*a, **k)
+        calls["fused"] += r is not None
+        return r
+    monkeypatch.setattr(HP, "stem_wgrad_fused", spy)
+    C.conv_wgrad_set_impl(6)
+    OF.set_deterministic(True)
+    res = {}
+    try:
+        for lazy in (True, False):
+            monkeypatch.setattr(OF, "_STEM_LAZY", lazy)
+            torch.manual_seed(0)
+            m = ResNet50(num_classes=1000, stem="imagenet").to(DEV)
+            loss = OF.cross_entropy(m(x), y)
+            loss.backward()
+            torch.cuda.synchronize()
+            res[lazy] = (loss.detach().clone(), m.conv1.weight.grad.clone(), m.bn1.weight.grad.clone(),
+                         m.bn1.bias.grad.clone())
+    finally:
+        OF.set_deterministic(False)
+        C.conv_wgrad_set_impl(-1)
+    assert calls["fused"] == (1 if fused else 0)
+    for a, b in zip(res[True], res[False]):
+        assert torch.equal(a, b)
