@@ -314,6 +314,9 @@ def _wgrad(P, dy, x, wpack, stride, pad, w, xq=None):
     return dwk.permute(0, 3, 1, 2)                                   # [K,C,R,S] channels_last
 
 
+# PMD_SIDE_SHORTCUT=0: the projection-shortcut convs of the forward stay on the main stream
+_SIDE_SHORTCUT = os.environ.get("PMD_SIDE_SHORTCUT", "1") != "0"
+
 # the split-K reductions of one block's side-stream weight gradients as ONE grouped launch
 # (kernels/conv_wgrad.hip wgrad_flush) instead of one per weight gradient; PMD_WS_GROUP=0: per wgrad
 _WS_GROUP = os.environ.get("PMD_WS_GROUP", "1") != "0"
@@ -1222,6 +1225,24 @@ class _ResidualBlockFn(torch.autograd.Function):
 
         def used_q(conv_m, hq_, h_):
             return hq_ if (hq_ is not None and fp8_eligible(conv_m, h_.shape[-1])) else None
+        # projection shortcut of a two-stream step: its conv (+ BN statistics) on the side stream,
+        # which is idle during the forward, concurrent with the main path's convs; joined before
+        # the final BN-apply that adds it
+        sc_pre = None
+        if shortcut is not None and _SIDE_SHORTCUT and x.is_cuda and _WGRAD_STREAM["on"] \
+                and not _state["force_torch"] and not torch.cuda.is_current_stream_capturing():
+            sconv, sbn = shortcut
+            wps = _conv_weight(P, sconv, x.dtype, x.shape[-1], x.requires_grad)
+            xq_s = used_q(sconv, xq, x)
+            main = torch.cuda.current_stream(x.device)
+            side = _wgrad_stream(x.device)
+            _stream_wait(side, main)
+            with torch.cuda.stream(side):
+                ys, sts = _conv_fwd_any(P, f8, x, xq_s, wps, sconv, _stats_req(sbn, training))
+            x.record_stream(side)
+            if xq_s is not None:
+                xq_s[0].record_stream(side)
+            sc_pre = (wps, xq_s, ys, sts, _record_on(side), main)
         h = x
         recs, qins = [], []
         nxt_convs = [c for c, _ in stages[1:]] + [final[0]]
@@ -1254,9 +1275,16 @@ class _ResidualBlockFn(torch.autograd.Function):
                  else None)
         if shortcut is not None:
             sconv, sbn = shortcut
-            wps = _conv_weight(P, sconv, x.dtype, x.shape[-1], x.requires_grad)
-            xq_s = used_q(sconv, xq, x)
-            ys, sts = _conv_fwd_any(P, f8, x, xq_s, wps, sconv, _stats_req(sbn, training))
+            if sc_pre is not None:
+                wps, xq_s, ys, sts, ev, main = sc_pre
+                _wait_on(main, ev)
+                ys.record_stream(main)               # allocated on the side stream, used here
+                if sts is not None:
+                    sts.record_stream(main)
+            else:
+                wps = _conv_weight(P, sconv, x.dtype, x.shape[-1], x.requires_grad)
+                xq_s = used_q(sconv, xq, x)
+                ys, sts = _conv_fwd_any(P, f8, x, xq_s, wps, sconv, _stats_req(sbn, training))
             qins.append(xq_s if f8w else None)
             pf, ps, countf = _bn_forward_params(P, yf, stf, fbn, training, sync, ys, sts, sbn)
             r = P.bn_apply(yf, pf, None, ys, ps, relu=True, **({"fp8": osite} if osite else {}))

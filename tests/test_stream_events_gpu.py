@@ -147,3 +147,20 @@ def test_dropped_fork_is_caught(det_two_stream):
     assert _differences(got[0], ref[0]), "a dropped fork went unnoticed"
     # the control breaks only the weight gradient it hands off: the main-stream state agrees
     assert not _differences(got[1], ref[1])
+
+
+def test_side_stream_shortcut_is_bit_exact(det_two_stream, monkeypatch):
+    """The forward's projection-shortcut convs on the side stream (concurrent with the main path,
+    joined before the final BN-apply) == the same step with them on the main stream, bit for bit
+    (gradients, running statistics, losses), with the main stream held back so the side stream
+    really runs ahead."""
+    from pytorch_multiprocessing_distributed_amd.ops import functional as OF
+    m0, batches = det_two_stream
+    monkeypatch.setattr(OF, "_SIDE_SHORTCUT", False)
+    ref = _grads(1, m0, batches)
+    monkeypatch.setattr(OF, "_SIDE_SHORTCUT", True)
+    for lag in (0, 20000):
+        got = _grads(1, m0, batches, lag)
+        for what, a, b in zip(("grads", "running", "losses"), got, ref):
+            bad = _differences(a, b)
+            assert not bad, (lag, what, bad[:10])
