@@ -87,6 +87,8 @@ def parse():
     ap.add_argument("--timeline", action="store_true",
                     help="print the gradient-bucket launch/overlap timeline of the last step")
     ap.add_argument("--profile", default="", help="write a torch.profiler table here (rank 0)")
+    ap.add_argument("--data_prefetch", default="on", choices=["on", "off"],
+                    help="two-stream steps: generate each synthetic batch one step ahead on the side stream")
     ap.add_argument("--step_mode", default="auto", choices=["auto", "two_stream", "one_stream", "graph"],
                     help="GPU step schedule (engine/train.py resolve_step_mode): auto = two_stream for the "
                          "224x224 headline, graph (W=1) / one_stream (W>1) for small images")
@@ -184,8 +186,13 @@ def bench_rank(rank, world, a):
 
     graphed = {}
 
+    prefetch = step_mode == "two_stream" and a.data_prefetch == "on"
+    if prefetch:
+        # each step's batch is generated one step ahead on the side stream (idle in the forward)
+        data.prefetch(OF._wgrad_stream(dev))
+
     def step(i):
-        x, y = data.batch_at(i)
+        x, y = data.next_batch(i) if prefetch else data.batch_at(i)
         g = graphed.get("g")
         if g is not None:
             return g(x, y)[1]               # the captured step, replayed on this batch
@@ -275,7 +282,8 @@ def bench_rank(rank, world, a):
             "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(1000.0 * dt / a.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
-            "data": "synthetic (on-device generated ImageNet-shaped batches, random-init weights)",
+            "data": "synthetic (ImageNet-shaped batches generated on device every step" +
+                    (", one step ahead on the side stream" if prefetch else "") + "; random-init weights)",
             "config": {"model": model_name, "global_batch": a.batch * world,
                        "seq_len": None,
                        "image_size": a.image, "per_gpu_batch": a.batch,

@@ -119,9 +119,41 @@ class SyntheticImageNet:
         self.seed = seed
         self.epoch = 0
         self.dataset_len = dataset_len
+        self._pf_stream = None
+        self._pf = {}
 
     def set_epoch(self, epoch):
         self.epoch = epoch
+        self._pf.clear()
+
+    def prefetch(self, stream):
+        """Generate every batch one step ahead on ``stream`` (the two-stream step's weight-gradient
+        stream, idle during the forward): :meth:`next_batch` ``(i)`` hands out batch i -- made on
+        ``stream`` while step i-1 ran, the current stream waiting for it -- and queues batch i+1.
+        The same batches and the same per-step generation work, off the main stream's critical
+        path (a prefetching data loader).  ``None``: generate in place."""
+        self._pf_stream = stream
+        self._pf.clear()
+
+    def _made_on_side(self, i):
+        with torch.cuda.stream(self._pf_stream):
+            x, y = self.batch_at(i)
+            ev = torch.cuda.Event()
+            ev.record(self._pf_stream)
+        return x, y, ev
+
+    def next_batch(self, i):
+        if self._pf_stream is None or self.device.type != "cuda":
+            return self.batch_at(i)
+        cur = torch.cuda.current_stream(self.device)
+        b = self._pf.pop(i, None)
+        x, y, ev = b if b is not None else self._made_on_side(i)
+        cur.wait_event(ev)
+        x.record_stream(cur)            # allocated on the prefetch stream, consumed here
+        y.record_stream(cur)
+        if i + 1 < self.steps:
+            self._pf[i + 1] = self._made_on_side(i + 1)
+        return x, y
 
     def __len__(self):
         return self.steps
@@ -142,4 +174,4 @@ class SyntheticImageNet:
 
     def __iter__(self):
         for i in range(self.steps):
-            yield self.batch_at(i)
+            yield self.next_batch(i)

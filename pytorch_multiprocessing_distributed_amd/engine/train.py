@@ -318,6 +318,8 @@ def _run(rank, world_size, args, dev):
     args.step_mode_resolved = resolve_step_mode(getattr(args, "step_mode", "auto"), world_size, on_gpu,
                                                 args.image_size, args.dtype)
     OF.set_wgrad_stream(args.step_mode_resolved == "two_stream")
+    if on_gpu and args.step_mode_resolved == "two_stream" and isinstance(train_loader, SyntheticImageNet):
+        train_loader.prefetch(OF._wgrad_stream(dev))   # batches generated one step ahead
     if rank == 0 and on_gpu:
         print(f"[pmd] step mode: {args.step_mode_resolved}", flush=True)
     model = DataParallel(model, comm, bucket_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb,
