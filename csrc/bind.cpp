@@ -1182,6 +1182,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("det_stats_on", &pmd::det_stats_on);
   m.def("gpu_sleep", [](int64_t us) { CHECK_RC(pmd::gpu_sleep_launch((int)us, cur_stream()), "gpu_sleep"); },
         "test utility: idle the current stream for `us` microseconds (<= 1 s)");
+  m.def("conv_probe_set", [](torch::Tensor buf) {
+          TORCH_CHECK(buf.is_cuda() && buf.scalar_type() == torch::kInt64 && buf.dim() == 2 && buf.size(1) == 16,
+                      "probe buffer: int64 [records, 16] on the GPU");
+          return (int64_t)pmd::conv_probe_set(buf.data_ptr(), (int)buf.size(0));
+        },
+        "data-gradient section probe buffer (PMD_DGRAD_PROBE builds: returns 1; production builds: 0, no-op)");
+  m.def("conv_probe_count", []() { return (int64_t)pmd::conv_probe_count(); });
   m.def("conv_set_tile", &pmd::conv_set_tile,
         "conv fwd/dgrad tile policy: 0 auto, 1 128-row only, 2 256x128, 3 256x256 where legal");
   m.def("conv_set_big_pipe", &pmd::conv_set_big_pipe,

@@ -117,6 +117,20 @@ __device__ __forceinline__ void wait_vmcnt() {
 #define PMD_TIMING_NO_ATOMICS 0  // bit 0 / 1: drop the forward BN statistics / the dgrad fused-reduce atomics
                                  // (WRONG numerics; timing A/B only)
 #endif
+// PMD_DGRAD_PROBE=1 (timing-only variant build, bench/dgrad_probe.py): every data-gradient
+// block's wave 0 stamps its sections -- entry, main loop done, C tile staged (+ the first
+// epilogue row group's operand prefetch), epilogue rows done, fused BN-reduce done -- and
+// appends one 16-word record to a device buffer (conv_probe_set).
+#ifndef PMD_DGRAD_PROBE
+#define PMD_DGRAD_PROBE 0
+#endif
+#if PMD_DGRAD_PROBE
+__device__ unsigned long long* g_probe_buf;
+// 256 counters, each owning cap/256 records (one counter for the whole grid serialised every
+// block's append on one L2 line: ~1 ms per 12k-block launch)
+__device__ unsigned int g_probe_ctr[256 * 32];  // one 128-B line per counter
+__device__ unsigned int g_probe_cap;
+#endif
 #ifndef PMD_F8_MINB
 // min blocks per CU of the single-stage fp8 dgrad with 0 / 1 fused BN-reduce sets: 4 = the
 // 128-VGPR cap (4 waves/SIMD; no spills with one B fragment held, NJ = 1); the 2-set
@@ -286,6 +300,19 @@ __global__ __launch_bounds__(64 * WM * WN,
   const int n0 = (L % tilesN) * BN;
   if (HALO) Mp = m0 + min(BM, hw_out - halo_t * BM);  // rows of this image only
   if (m0 >= Mp) return;  // uniform per block, before any barrier
+#if PMD_DGRAD_PROBE
+  unsigned long long pt[5] = {0, 0, 0, 0, 0};
+  const unsigned long long pwc0 = wall_clock64();
+  pt[0] = clock64();
+#define PMD_PROBE_AT(k) \
+  do {                  \
+    pt[k] = clock64();  \
+  } while (0)
+#else
+#define PMD_PROBE_AT(k) \
+  do {                  \
+  } while (0)
+#endif
 
   // ---- per-thread A-row precompute
   // register staging: thread -> (row rsub + 32 i, chunk tid & 7)
@@ -883,6 +910,7 @@ __global__ __launch_bounds__(64 * WM * WN,
       __syncthreads();
     }
   }
+  PMD_PROBE_AT(1);
 
   // ---- epilogue
   constexpr int CPR = BN / 8;  // 16-B chunks per output row
@@ -1090,6 +1118,7 @@ __global__ __launch_bounds__(64 * WM * WN,
     }
   }
   __syncthreads();
+  PMD_PROBE_AT(2);
   if (STATS) {
     const float* st = reinterpret_cast<const float*>(smem + SMEM);
     for (int c = tid; c < 2 * BN; c += NT) {
@@ -1201,6 +1230,13 @@ __global__ __launch_bounds__(64 * WM * WN,
       }
     }
   }
+#if PMD_DGRAD_PROBE
+  if constexpr (DGRAD) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's epilogue stores have landed
+    __syncthreads();
+  }
+#endif
+  PMD_PROBE_AT(3);
   if (nbn && n_ok) {
 #pragma unroll
     for (int t = 0; t < NBA; ++t)
@@ -1233,7 +1269,54 @@ __global__ __launch_bounds__(64 * WM * WN,
       __syncthreads();
     }
   }
+#if PMD_DGRAD_PROBE
+  if constexpr (DGRAD) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    PMD_PROBE_AT(4);
+    const unsigned long long pwc1 = wall_clock64();
+    if (tid == 0 && g_probe_buf) {
+      const unsigned int q = (blockIdx.x + 7u * blockIdx.y) & 255u, per = g_probe_cap >> 8;
+      const unsigned int slot = atomicAdd(&g_probe_ctr[q * 32], 1u);
+      if (slot < per) {
+        unsigned long long* r = g_probe_buf + ((size_t)q * per + slot) * 16;
+        r[0] = pwc0;
+        r[1] = pwc1;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) r[2 + k] = pt[k];
+        r[7] = ((unsigned long long)a.M << 32) | ((unsigned long long)a.Nout << 16) | (unsigned)a.Kg;
+        r[8] = ((unsigned long long)BM << 48) | ((unsigned long long)BN << 32) | ((unsigned long long)BK << 16) |
+               (NST << 8) | (F8 ? 16 : 0) | (NST1 ? 32 : 0) | (HALO ? 64 : 0) | (P8 ? 128 : 0);
+        r[9] = ((unsigned long long)a.stride << 32) | (nbn << 8) | (has_add ? 1 : 0) | (NW << 16);
+        r[10] = blockIdx.x | ((unsigned long long)blockIdx.y << 32);
+        r[11] = (unsigned long long)(size_t)a.out;
+      }
+    }
+  }
+#endif
 }
+
+#if PMD_DGRAD_PROBE
+// probe buffer (cap records of 16 words, cap/256 per counter; nullptr: off); returns 1 in a probe build
+int conv_probe_set(void* buf, int cap) {
+  unsigned long long* p = reinterpret_cast<unsigned long long*>(buf);
+  static const unsigned int zero[256 * 32] = {0};
+  const unsigned int c = (unsigned int)cap;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_probe_buf), &p, sizeof(p)) != hipSuccess) return -1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_probe_cap), &c, sizeof(c)) != hipSuccess) return -1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_probe_ctr), zero, sizeof(zero)) != hipSuccess) return -1;
+  return 1;
+}
+int conv_probe_count() {  // the largest per-counter fill (records beyond cap/256 were dropped)
+  static unsigned int c[256 * 32];
+  if (hipMemcpyFromSymbol(c, HIP_SYMBOL(g_probe_ctr), sizeof(c)) != hipSuccess) return -1;
+  unsigned int m = 0;
+  for (int i = 0; i < 256; ++i) m = c[32 * i] > m ? c[32 * i] : m;
+  return (int)m;
+}
+#else
+int conv_probe_set(void*, int) { return 0; }
+int conv_probe_count() { return 0; }
+#endif
 
 // fp32 param (physical K,R,S,C = channels_last [K,C,R,S]) -> bf16 images:
 //   wk  [K][R][S][Cp]   (B^T of the forward GEMM, zero-padded channels)

@@ -31,6 +31,9 @@ void det_stats_set(bool on);
 int det_begin(DetStats& d, float** p0, float** p1, int nslots_bound, int width, hipStream_t st);
 int det_end(DetStats& d, hipStream_t st);
 int gpu_sleep_launch(int us, hipStream_t st);  // test utility: idle the stream for us microseconds
+// data-gradient section probe (PMD_DGRAD_PROBE variant builds; 0 otherwise): records of 16 words
+int conv_probe_set(void* buf, int cap);
+int conv_probe_count();
 // stats (optional): BN statistic slots [kStatSlots][2][Nout] of (sum (y-K), sum (y-K)^2) with
 // K = shift[n] (nullable: 0) -- see bn_moments in common.h
 int conv_igemm_launch(const bf16_t* src, const bf16_t* wt, bf16_t* out, float* stats, int N, int H,

@@ -64,3 +64,12 @@ def test_step_runs_only_framework_kernels(dtype):
     assert len(copies) == 0, f"{len(copies)} device copies / fills in a steady-state step: {sorted(set(copies))}"
     foreign = sorted(n for n in kernels if "pmd::" not in n)
     assert not foreign, f"non-framework kernels on the step: {foreign[:10]}"
+
+
+def test_production_library_has_no_dgrad_probe():
+    """The data-gradient section probe (conv_igemm.hip PMD_DGRAD_PROBE, bench/dgrad_probe.py) exists
+    only in variant builds: the production library's conv_probe_set is a no-op returning 0."""
+    from pytorch_multiprocessing_distributed_amd.ops.native import C
+    buf = torch.zeros(256, 16, dtype=torch.int64, device="cuda")
+    assert C.conv_probe_set(buf) == 0
+    assert C.conv_probe_count() == 0
