@@ -1,9 +1,12 @@
 """Contention attribution of the two-stream step (kernel traces of bench.py): for every main-stream
 kernel instance, its duration next to the side stream minus its duration in a single-stream run of
 the same step (PMD_WGRAD_STREAM=0, same order), attributed to the side-stream kernel families it
-overlapped (by overlap time).  python bench/contention.py <two-stream.csv> <single-stream.csv> [--step 8]"""
+overlapped (by overlap time).  python bench/contention.py <two-stream trace> <single-stream trace> [--step 8]
+(a trace: a rocprofv3 kernel_trace.csv, or a directory holding one; bash bench/contention.sh runs both)."""
 import argparse
 import csv
+import glob
+import os
 import re
 from collections import defaultdict
 
@@ -13,9 +16,13 @@ def nm(r):
 
 
 def step_rows(path, step):
+    if os.path.isdir(path):
+        path = glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    marks = [i for i, r in enumerate(rows) if "synth_images" in r["Kernel_Name"]]
-    return rows[marks[step]:marks[step + 1]]
+    # a step ends with its optimizer kernel (the next step's batch may be generated on the side
+    # stream during this step's forward, so the data kernel is no step boundary)
+    marks = [i for i, r in enumerate(rows) if "sgd_kernel" in r["Kernel_Name"]]
+    return rows[marks[step] + 1:marks[step + 1] + 1]
 
 
 def main():
@@ -26,7 +33,7 @@ def main():
     x = ap.parse_args()
     A = step_rows(x.two, x.step)
     B = step_rows(x.one, x.step)
-    mq = A[0]["Queue_Id"]
+    mq = A[-1]["Queue_Id"]          # the optimizer kernel runs on the main stream
     main_a = [r for r in A if r["Queue_Id"] == mq]
     side_a = [r for r in A if r["Queue_Id"] != mq]
     side_names = {nm(r) for r in side_a}

@@ -20,7 +20,7 @@ for p in "$@"; do
     longfp8)   specs+=("longfp8:400:python bench.py --steps 300 --warmup 20 --dtype fp8") ;;
     prof)      specs+=("prof:300:rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o prof -- python3 bench.py --steps 10 --warmup 5") ;;
     pmc)       specs+=("pmc:600:bash bench/pmc_step.sh") ;;
-    contention) specs+=("contention:600:python bench/contention.py") ;;
+    contention) specs+=("contention:600:bash bench/contention.sh") ;;
     *) echo "unknown preset $p" >&2; exit 2 ;;
   esac
 done
