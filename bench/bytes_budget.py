@@ -55,7 +55,7 @@ def main():
         streams[s] += d
     main_s = max(streams, key=streams.get)          # the stream with the most kernel time
     step_ms = (t1 - t0) / 1e6 / a.steps
-    print(f"# bytes budget of one ResNet-50 bs256 bf16 step, MI355X{(' -- ' + a.title) if a.title else ''}")
+    print(f"# bytes budget of one ResNet-50 bs256 step, MI355X{(' -- ' + a.title) if a.title else ''}")
     print(f"# GB: rocprofv3 --pmc of the last step (2 x FETCH_SIZE + WRITE_SIZE); serial ms: that counter run")
     print(f"# main/side ms: per timed step of the two-stream kernel trace (stream {main_s} = main); "
           f"@6TB/s: GB / 6 TB/s")

@@ -21,6 +21,8 @@ for p in "$@"; do
     prof)      specs+=("prof:300:rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o prof -- python3 bench.py --steps 10 --warmup 5") ;;
     pmc)       specs+=("pmc:600:bash bench/pmc_step.sh") ;;
     contention) specs+=("contention:600:bash bench/contention.sh") ;;
+    bytes)     specs+=("bytes:900:bash bench/bytes_budget.sh bf16") ;;
+    bytesfp8)  specs+=("bytesfp8:900:bash bench/bytes_budget.sh fp8") ;;
     *) echo "unknown preset $p" >&2; exit 2 ;;
   esac
 done
