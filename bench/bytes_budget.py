@@ -43,9 +43,11 @@ def main():
             if "WRITE_SIZE" in cs:
                 gb[k][1] += per[i].get("WRITE_SIZE", 0.0) * 1024
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
-    marks = [i for i, r in enumerate(rows) if "synth_images" in r["Kernel_Name"]]
-    lo, hi = marks[a.warmup], marks[a.warmup + a.steps]
-    t0, t1 = int(rows[lo]["Start_Timestamp"]), int(rows[hi]["Start_Timestamp"])
+    # steps end with the optimizer kernel (the next batch may be generated on the side stream
+    # during a step's forward, so the data kernel is no step boundary)
+    marks = [i for i, r in enumerate(rows) if "sgd_kernel" in r["Kernel_Name"]]
+    lo, hi = marks[a.warmup - 1] + 1, marks[a.warmup + a.steps - 1] + 1
+    t0, t1 = int(rows[lo]["Start_Timestamp"]), int(rows[hi - 1]["End_Timestamp"])
     streams = defaultdict(float)
     two = defaultdict(lambda: defaultdict(float))
     for r in rows[lo:hi]:

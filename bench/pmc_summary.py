@@ -48,11 +48,16 @@ def load_pass(d):
     return per, dur
 
 
-def last_step(per, marker="synth_images_kernel"):
+def last_step(per, marker="sgd_kernel"):
+    """Dispatches of the run's last step: after the next-to-last optimizer kernel, through the
+    last (a step ends with its optimizer kernel; with the data prefetch, a batch is generated
+    during the previous step, so the data kernel is no step boundary)."""
     ids = sorted(per)
     marks = [i for i in ids if marker in per[i]["name"]]
-    start = marks[-1] if marks else ids[0]
-    return [i for i in ids if i >= start]
+    if not marks:
+        return ids
+    start = marks[-2] + 1 if len(marks) >= 2 else ids[0]
+    return [i for i in ids if start <= i <= marks[-1]]
 
 
 def main():
