@@ -189,7 +189,7 @@ def bench_rank(rank, world, a):
     prefetch = step_mode == "two_stream" and a.data_prefetch == "on"
     if prefetch:
         # each step's batch is generated one step ahead on the side stream (idle in the forward)
-        data.prefetch(OF._wgrad_stream(dev))
+        data.prefetch(OF._wgrad_stream(dev), transform=OF.s2d_input_prefetch(model))
 
     def step(i):
         x, y = data.next_batch(i) if prefetch else data.batch_at(i)

@@ -120,24 +120,31 @@ class SyntheticImageNet:
         self.epoch = 0
         self.dataset_len = dataset_len
         self._pf_stream = None
+        self._pf_transform = None
         self._pf = {}
 
     def set_epoch(self, epoch):
         self.epoch = epoch
         self._pf.clear()
 
-    def prefetch(self, stream):
+    def prefetch(self, stream, transform=None):
         """Generate every batch one step ahead on ``stream`` (the two-stream step's weight-gradient
         stream, idle during the forward): :meth:`next_batch` ``(i)`` hands out batch i -- made on
         ``stream`` while step i-1 ran, the current stream waiting for it -- and queues batch i+1.
         The same batches and the same per-step generation work, off the main stream's critical
-        path (a prefetching data loader).  ``None``: generate in place."""
+        path (a prefetching data loader).  ``None``: generate in place.  ``transform``: applied to
+        each batch's images on ``stream`` too (the model's input layout step,
+        ops/functional.py s2d_input_prefetch); tensors it attaches as ``x._pmd_*`` attributes
+        are handed to the consuming stream with the batch."""
         self._pf_stream = stream
+        self._pf_transform = transform
         self._pf.clear()
 
     def _made_on_side(self, i):
         with torch.cuda.stream(self._pf_stream):
             x, y = self.batch_at(i)
+            if self._pf_transform is not None:
+                x = self._pf_transform(x)
             ev = torch.cuda.Event()
             ev.record(self._pf_stream)
         return x, y, ev
@@ -151,6 +158,9 @@ class SyntheticImageNet:
         cur.wait_event(ev)
         x.record_stream(cur)            # allocated on the prefetch stream, consumed here
         y.record_stream(cur)
+        xs = getattr(x, "_pmd_s2d_in", None)
+        if xs is not None:
+            xs.record_stream(cur)
         if i + 1 < self.steps:
             self._pf[i + 1] = self._made_on_side(i + 1)
         return x, y

@@ -319,7 +319,8 @@ def _run(rank, world_size, args, dev):
                                                 args.image_size, args.dtype)
     OF.set_wgrad_stream(args.step_mode_resolved == "two_stream")
     if on_gpu and args.step_mode_resolved == "two_stream" and isinstance(train_loader, SyntheticImageNet):
-        train_loader.prefetch(OF._wgrad_stream(dev))   # batches generated one step ahead
+        # batches generated (and laid out for the stem) one step ahead
+        train_loader.prefetch(OF._wgrad_stream(dev), transform=OF.s2d_input_prefetch(model))
     if rank == 0 and on_gpu:
         print(f"[pmd] step mode: {args.step_mode_resolved}", flush=True)
     model = DataParallel(model, comm, bucket_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb,

@@ -883,7 +883,11 @@ class _StemS2DConvFn(torch.autograd.Function):
     def forward(ctx, x, w, want_stats):
         from . import hip_prims as HP
         from .native import C
-        xs = C.stem_s2d_input(x)                       # [N, H/2, W/2, 16]
+        xs = getattr(x, "_pmd_s2d_in", None)           # made by the data prefetch (s2d_input_prefetch)
+        if xs is not None:
+            x._pmd_s2d_in = None
+        if xs is None or tuple(xs.shape) != (x.shape[0], x.shape[1] // 2, x.shape[2] // 2, 16):
+            xs = C.stem_s2d_input(x)                   # [N, H/2, W/2, 16]
         ws = C.stem_s2d_weight(w.detach())             # [K, 4, 4, 16] bf16
         oh, ow = x.shape[1] // 2, x.shape[2] // 2
         want, shift = HP._TP.stats_request(want_stats)
@@ -935,6 +939,25 @@ def set_s2d_stem(flag: bool):
 
 def _pair(v):
     return tuple(v) if isinstance(v, (tuple, list)) else (v, v)
+
+
+def s2d_input_prefetch(model):
+    """The space-to-depth stem's input transform as a data-prefetch step (data/loader.py
+    SyntheticImageNet.prefetch ``transform``), or None when ``model`` has no such stem: the
+    prefetching stream lays each batch out for the 4x4 stem conv one step ahead
+    (``x._pmd_s2d_in``), so the step's first main-stream kernel is the stem conv itself."""
+    m = getattr(model, "module", model)
+    c = getattr(m, "conv1", None)
+    if (not _S2D_STEM or os.environ.get("PMD_S2D_PREFETCH", "1") == "0" or c is None or getattr(c, "weight", None) is None or tuple(c.weight.shape[2:]) != (7, 7)
+            or _pair(c.stride) != (2, 2) or _pair(c.padding) != (3, 3)):
+        return None
+
+    def transform(x):
+        if x.is_cuda and x.dim() == 4 and x.shape[-1] == 8 and x.shape[1] % 2 == 0 and x.shape[2] % 2 == 0:
+            from .native import C
+            x._pmd_s2d_in = C.stem_s2d_input(x)
+        return x
+    return transform
 
 
 def _s2d_stem_ok(x, conv_mod):

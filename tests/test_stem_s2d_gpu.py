@@ -107,3 +107,39 @@ def test_fused_stem_backward_matches_two_pass(n, h, fused, monkeypatch):
     assert calls["fused"] == (1 if fused else 0)
     for a, b in zip(res[True], res[False]):
         assert torch.equal(a, b)
+
+
+def test_s2d_input_prefetched_with_the_batch_is_bit_exact():
+    """The stem's space-to-depth input layout made by the data prefetch on the side stream
+    (ops/functional.py s2d_input_prefetch, data/loader.py prefetch transform) gives the same
+    two-stream ResNet-50 steps, bit for bit (deterministic statistics mode), as the stem laying
+    the batch out itself -- and the prefetched layout is what the stem consumed."""
+    from pytorch_multiprocessing_distributed_amd.data.loader import SyntheticImageNet
+    from pytorch_multiprocessing_distributed_amd.models import ResNet50
+    from pytorch_multiprocessing_distributed_amd.ops import functional as OF
+    dev = torch.device(DEV, 0)
+    OF.init_step_streams(dev)
+    OF.set_deterministic(True)
+    try:
+        res = []
+        for pre in (False, True):
+            torch.manual_seed(0)
+            m = ResNet50(num_classes=1000, stem="imagenet").to(dev)
+            data = SyntheticImageNet(4, 64, 1000, steps=3, device=dev, dtype=torch.bfloat16, cpad=8, seed=5)
+            tf = OF.s2d_input_prefetch(m) if pre else None
+            assert (tf is not None) == pre
+            data.prefetch(OF._wgrad_stream(dev), transform=tf)
+            losses = []
+            for i in range(3):
+                x, y = data.next_batch(i)
+                assert (getattr(x, "_pmd_s2d_in", None) is not None) == pre
+                loss = OF.cross_entropy(m(x), y)
+                assert getattr(x, "_pmd_s2d_in", None) is None      # consumed by the stem
+                loss.backward(OF.loss_seed(loss))
+                losses.append(loss.detach().clone())
+            torch.cuda.synchronize()
+            res.append((torch.stack(losses), m.conv1.weight.grad.clone(), m.bn1.running_mean.clone()))
+    finally:
+        OF.set_deterministic(False)
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
