@@ -14,6 +14,9 @@ def pytest_configure(config):
 
 
 def pytest_collection_modifyitems(config, items):
+    # the multi-process tests run last: they take most of the suite's time, and under -x a
+    # failure there no longer hides the single-process kernel / model tests behind it
+    items[:] = [it for it in items if "slow" not in it.keywords] + [it for it in items if "slow" in it.keywords]
     import torch
     if torch.cuda.is_available():
         return
