@@ -41,6 +41,9 @@ def _worker(rank, world, port, out, stats_comm="gloo", fault="none", model_name=
     from pytorch_multiprocessing_distributed_amd.parallel import dp as DP
     from pytorch_multiprocessing_distributed_amd.parallel.comm import get_comm
     torch.cuda.set_device(0)
+    # the rank's step streams (main / weight gradients / collectives) created before the process
+    # group, as launch.init_process does for every production rank
+    OF.init_step_streams(torch.device("cuda", 0))
     if det:
         # the production kernel choices (committed tables, no per-process online tuning of 8
         # processes sharing the GPU) and the deterministic statistics mode
