@@ -6,7 +6,8 @@ set -o pipefail
 dt=${1:-bf16}
 out=${2:-gpurun_out/bytes_$dt}
 mkdir -p "$out"
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+root=$(pwd)
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$root}"
 export PMD_NO_AUTOBUILD=1
 bash bench/pmc_step.sh "$out/pmc" -- python3 bench.py --steps 2 --warmup 1 --dtype "$dt" || exit 1
 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$out/trace" -o run -- \

@@ -5,7 +5,8 @@
 set -o pipefail
 out=${1:-gpurun_out/contention}; shift || true
 mkdir -p "$out"
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+root=$(pwd)
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$root}"
 export PMD_NO_AUTOBUILD=1
 for m in two_stream one_stream; do
   timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$out/$m" -o run -- \

@@ -8,7 +8,8 @@ out=${1:-gpurun_out/pmc}; shift || true
 [ "${1:-}" = "--" ] && shift
 if [ $# -eq 0 ]; then set -- python3 bench.py --steps 2 --warmup 1; fi
 mkdir -p "$out"
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+root=$(pwd)
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$root}"
 export PMD_NO_AUTOBUILD=1
 PA="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"
 PB="FETCH_SIZE TCC_HIT_sum GRBM_GUI_ACTIVE"
