@@ -31,7 +31,7 @@ class _NoWork:
         pass
 
 
-def _worker(rank, world, port, out, stats_comm="gloo", fault="none", model_name="res", det=False):
+def _worker(rank, world, port, out, stats_comm="gloo", fault="none", model_name="res", det=False, streams=True):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -43,7 +43,8 @@ def _worker(rank, world, port, out, stats_comm="gloo", fault="none", model_name=
     torch.cuda.set_device(0)
     # the rank's step streams (main / weight gradients / collectives) created before the process
     # group, as launch.init_process does for every production rank
-    OF.init_step_streams(torch.device("cuda", 0))
+    if streams:
+        OF.init_step_streams(torch.device("cuda", 0))
     if det:
         # the production kernel choices (committed tables, no per-process online tuning of 8
         # processes sharing the GPU) and the deterministic statistics mode
