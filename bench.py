@@ -343,6 +343,7 @@ def bench_rank(rank, world, a):
         with open(a.profile, "w") as f:
             f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=80))
     if world > 1 or rehearsal:
+        model.close()           # the native reducer holds the process group: release it first
         launch.shutdown()
 
 

@@ -365,3 +365,4 @@ def _run(rank, world_size, args, dev):
     if rank == 0 and not args.no_plot:
         from ..utils.plot import draw_plot
         draw_plot(args.save_path)
+    model.close()       # release the native reducer (it holds the process group) before shutdown

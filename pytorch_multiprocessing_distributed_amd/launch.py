@@ -65,6 +65,10 @@ def init_process(rank, world_size, backend="auto", device="auto", master_addr=No
 
 def shutdown():
     if dist.is_available() and dist.is_initialized():
+        # unreachable DataParallel wrappers (kept in cycles by their gradient hooks) and the
+        # native reducer that holds the process group go first, then the group itself
+        import gc
+        gc.collect()
         dist.destroy_process_group()
 
 

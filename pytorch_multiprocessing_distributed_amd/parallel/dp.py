@@ -289,6 +289,17 @@ class DataParallel(nn.Module):
     def _direct_only(self):
         return self.post_hooks == "auto" and getattr(self.module, "impl", None) == "fused"
 
+    def close(self):
+        """Release the native reducer (which holds the process group) and the gradient hooks
+        now, before the process group is destroyed: the hooks' closures keep this object in
+        a reference cycle, which Python may otherwise collect only at interpreter exit --
+        destroying a gloo process group there, after the rest of the runtime, could abort the
+        process.  The wrapped module keeps its parameters and gradients."""
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        self._native = None
+
     def _install_hooks(self):
         for h in self._hooks:
             h.remove()

@@ -14,9 +14,12 @@ def pytest_configure(config):
 
 
 def pytest_collection_modifyitems(config, items):
-    # the multi-process tests run last: they take most of the suite's time, and under -x a
-    # failure there no longer hides the single-process kernel / model tests behind it
-    items[:] = [it for it in items if "slow" not in it.keywords] + [it for it in items if "slow" in it.keywords]
+    # the multi-process GPU tests run last: they take most of the GPU suite's time, and under -x
+    # a failure there no longer hides the single-process kernel / model tests behind it (the CPU
+    # suite keeps its file order)
+    last = [it for it in items if "slow" in it.keywords and "gpu" in it.keywords]
+    if last:
+        items[:] = [it for it in items if not ("slow" in it.keywords and "gpu" in it.keywords)] + last
     import torch
     if torch.cuda.is_available():
         return

@@ -47,6 +47,7 @@ def worker(rank, world):
         assert dp.num_iterations == 3, dp.num_iterations
         assert dp.rebuilt_order is not None
         dp.bucket_timeline()
+        dp.close()
     C.conv_autotune_import(C.conv_autotune_export())
     OF.set_bn_sync(None)
     dist.destroy_process_group()

@@ -80,6 +80,7 @@ def _worker(rank, world, port, out_path, reducer="native", compress="none"):
         torch.save({"state": dp.module.state_dict(), "loss": gl[0] / world,
                     "grad": _grads(dp), "order": dp.rebuilt_order}, out_path)
     OF.set_bn_sync(None)
+    dp.close()                  # the native reducer holds the process group: release it first
     dist.destroy_process_group()
 
 
@@ -172,6 +173,7 @@ def _no_sync_worker(rank, world, port):
     assert dp.num_iterations == 1
     allg = comm.all_gather(dp.flat.grad_arena.clone())
     assert torch.equal(allg[0], allg[1])
+    dp.close()                  # the native reducer holds the process group
     dist.destroy_process_group()
 
 

@@ -124,6 +124,7 @@ def _worker(rank, world, port, out, stats_comm="gloo", fault="none", model_name=
                     "lin_calls": lin_calls["n"] if model_name == "resnet50" else 0,
                     "nbuckets": len(dp.buckets)}, out)
     OF.set_bn_sync(None)
+    dp.close()                  # the native reducer holds the process group
     dist.destroy_process_group()
 
 

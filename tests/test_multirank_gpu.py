@@ -108,6 +108,7 @@ def _defer_worker(rank, world, port, out, defer):
         torch.save({"iters": dp.num_iterations, "nb": len(dp.buckets), "launches": launches,
                     "grads": grads, "loss": float(loss)}, out)
     OF.set_bn_sync(None)
+    dp.close()                  # the native reducer holds the process group
     dist.destroy_process_group()
 
 
@@ -194,6 +195,7 @@ def test_native_rccl_comm_single_rank_reducer():
             rel = ((grads["rccl"][n] - g).float().norm() / g.float().norm().clamp_min(1e-12)).item()
             assert rel < 1e-6, (n, rel)
     finally:
+        dp.close()                  # the native reducer holds the process group
         dist.destroy_process_group()
 
 
@@ -242,6 +244,7 @@ def test_auto_transport_picks_native_rccl_with_selftest_and_error_check():
             comm.raise_if_failed()
     finally:
         OF.set_bn_sync(None)
+        dp.close()                  # the native reducer holds the process group
         dist.destroy_process_group()
 
 
